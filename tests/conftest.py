@@ -1,0 +1,42 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_ROOT = os.path.join(REPO, "flow-matching-and-diffusion-models_amd")
+for p in (REPO, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP library")
+
+
+def _gpu_ok():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_ok():
+        return
+    skip = pytest.mark.skip(reason="no ROCm GPU in this container")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    import torch
+    d = os.path.join(REPO, "tests", "golden")
+    tensors = torch.load(os.path.join(d, "golden.pt"), weights_only=True)
+    meta = json.load(open(os.path.join(d, "golden.json")))
+    return tensors, meta

@@ -1,0 +1,148 @@
+"""Pin the CPU oracle against fixtures produced by the reference itself (tests/golden/make_golden.py)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import schedulers as OS
+from oracle import spec as S
+from oracle import train_step as OT
+from oracle import unet as U
+
+MODEL_CASES = ["ldct_fm_test", "mnist_ddpm_diffusers", "mnist_fm_compvis", "ldct_fm_b64", "ldct_fm_diffusers_b64"]
+
+
+def _spec(meta):
+    tr = meta["training"]
+    return S.derive_spec(meta["unet"], tr["conditioning"], tr["channels"] or 1)
+
+
+def _params(spec, seed):
+    # leaf tensors with requires_grad: matches nn.Parameter dispatch (bit-exact F.linear path)
+    return {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, seed).items()}
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_unet_forward_bit_exact(golden, name):
+    T, M = golden
+    m = M[name]
+    spec = _spec(m)
+    sd = _params(spec, m["seed"])
+    with torch.no_grad():
+        y = U.unet_forward(sd, spec, T[f"{name}/x"], T[f"{name}/t"], context=T.get(f"{name}/cond"))
+    assert y.shape == T[f"{name}/y"].shape
+    assert torch.equal(y, T[f"{name}/y"]), (y - T[f"{name}/y"]).abs().max()
+
+
+def test_fm_train_step(golden):
+    T, M = golden
+    m = M["fm_step"]
+    spec = _spec(m)
+    sd = _params(spec, m["seed"])
+    loss, scaled = OT.fm_loss(sd, spec, T["fm_step/clean"], T["fm_step/ldct"], T["fm_step/noise"], T["fm_step/t"],
+                              m["num_train_timesteps"])
+    scaled.backward()
+    assert torch.equal(loss.detach(), T["fm_step/loss"])
+    names = m["param_names"]
+    gs = torch.stack([sd[k].grad.double().sum() for k in names])
+    gq = torch.stack([sd[k].grad.double().pow(2).sum() for k in names])
+    torch.testing.assert_close(gs, T["fm_step/grad_sum"], rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(gq, T["fm_step/grad_sq"], rtol=1e-9, atol=1e-12)
+    OT.adamw_step(sd, m["lr"], 1, {})
+    ps = torch.stack([sd[k].detach().double().sum() for k in names])
+    torch.testing.assert_close(ps, T["fm_step/param_sum_after"], rtol=1e-7, atol=1e-7)
+
+
+def test_self_attention_raw_reshape(golden):
+    T, M = golden
+    m = M["attn"]
+    shapes = {"norm.weight": (512,), "norm.bias": (512,), "qkv.weight": (768, 512, 1), "qkv.bias": (768,),
+              "proj_out.weight": (512, 256, 1), "proj_out.bias": (512,)}
+    p = U.seeded_tensors(shapes, m["seed"])
+    sd = {f"a.{k}": v for k, v in p.items()}
+    L = dict(prefix="a", heads=4, dim_head=64, linear=False)
+    with torch.no_grad():
+        y = U.self_attention(sd, L, T["attn/x"])
+    assert torch.equal(y, T["attn/y"])
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_resblock(golden, i):
+    T, M = golden
+    m = M[f"res{i}"]
+    import oracle.unet as UU
+    names = m["names"]
+    shapes = {}
+    cin, cout = m["cin"], m["cout"]
+    for n in names:
+        if n.startswith("norm1"):
+            shapes[n] = (cin,)
+        elif n.startswith("norm2"):
+            shapes[n] = (cout,)
+        elif n == "conv1.conv.weight":
+            shapes[n] = (cout, cin, 3, 3)
+        elif n == "conv2.conv.weight":
+            shapes[n] = (cout, cout, 3, 3)
+        elif n.endswith("conv.bias"):
+            shapes[n] = (cout,)
+        elif n == "emb_layers.weight":
+            shapes[n] = (2 * cout if m["scale_shift"] else cout, 512)
+        elif n == "emb_layers.bias":
+            shapes[n] = (2 * cout if m["scale_shift"] else cout,)
+        elif n == "skip_connection.conv.weight":
+            shapes[n] = (cout, cin, 1, 1)
+    p = UU.seeded_tensors(shapes, m["seed"])
+    sd = {f"r.{k}": v.requires_grad_() for k, v in p.items()}
+    L = S.res_layer("r", cin, cout, scale_shift=m["scale_shift"], emb_act=m["emb_act"], add_emb=m["add_emb"])
+    with torch.no_grad():
+        y = U.resblock(sd, L, T[f"res{i}/x"], T[f"res{i}/emb"], 2)
+    assert torch.equal(y, T[f"res{i}/y"])
+
+
+def test_timestep_embedding(golden):
+    T, _ = golden
+    t = T["temb/t"]
+    assert torch.equal(U.timestep_embedding(t, 128, flip_sin_to_cos=True), T["temb/flip"])
+    assert torch.equal(U.timestep_embedding(t, 128, flip_sin_to_cos=False), T["temb/noflip"])
+    assert torch.equal(U.timestep_embedding(t, 33, flip_sin_to_cos=False, freq_shift=1), T["temb/odd"])
+
+
+# ---- scheduler KATs (closed form): parity otherwise unpinned
+def test_flowmatch_kat():
+    s = OS.FlowMatchEuler(1000)
+    assert s.sigma_min == 0.0010000000474974513
+    s.set_timesteps(50)
+    ts = s.timesteps
+    assert ts.dtype == torch.float32
+    assert ts[:3].tolist() == [1000.0, 979.6122436523438, 959.2244873046875]
+    assert ts[-1].item() == 1.0
+    assert s.sigmas[-1].item() == 0.0 and len(s.sigmas) == 51
+
+
+def test_ddpm_kat():
+    s = OS.DDPM(1000, beta_start=0.00085, beta_end=0.012)
+    ac = s.alphas_cumprod
+    assert abs(ac[0].item() - 0.99914998) < 1e-7
+    assert abs(ac[499].item() - 0.16181217) < 1e-7
+    assert abs(ac[999].item() - 0.00157896) < 1e-7
+    s.set_timesteps(50)
+    assert s.timesteps.tolist() == list(range(980, -1, -20))
+    assert s.timesteps.dtype == torch.int64
+
+
+def test_fm_train_timesteps_bitexact():
+    t = torch.tensor([0.0, 0.5, 0.999999, 1e-7, 0.3333333])
+    assert OT.fm_timesteps(t, 1000).tolist() == [0, 499, 998, 0, 332]
+
+
+def test_cosine_schedule_matches_transformers():
+    tf = pytest.importorskip("transformers.optimization")
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=1.0)
+    sch = tf.get_cosine_schedule_with_warmup(opt, num_warmup_steps=5, num_training_steps=40)
+    for step in range(40):
+        assert math.isclose(opt.param_groups[0]["lr"], OS.cosine_with_warmup(step, 5, 40), rel_tol=1e-12)
+        opt.step()
+        sch.step()
