@@ -1,0 +1,251 @@
+"""Headline benchmark: LDCT 256x256 flow-matching UNet, train images/s + 50-step sampler, on MI355X.
+
+Workload (BASELINE.json configs[1]): EfficientUNetND built
+from the reference's ``configs/flow_matching/ldct_flow_matching.json`` ``model.unet``
+block (113,008,257 params), concatenate conditioning (2 input channels), batch 8
+per GPU, 256x256, synthetic LDCT-shaped tensors (clean in [0,1], ldct = clamp(clean
++ 0.05 N(0,1))), random init.  One "step" = one full FM train step (noise/t draw,
+x_t, forward, MSE, backward, [RCCL gradient all-reduce], AdamW + cosine LR) on the
+HIP engine, captured as a hipGraph on 1 GPU.  The sampler leg times a 50-step
+FlowMatchEuler sampling of 8 images (one UNet forward + Euler update per step).
+
+Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``;
+each rank trains on its own batch of 8 (weak scaling) with a real gradient
+all-reduce; the timed region is bracketed by barrier + synchronize and the max
+over ranks is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "flow-matching-and-diffusion-models_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# model.unet block of the reference's configs/flow_matching/ldct_flow_matching.json
+LDCT_FM_UNET = {
+    "sample_size": 256, "in_channels": 1, "out_channels": 1, "layers_per_block": 2,
+    "block_out_channels": [128, 128, 256, 256, 512, 512],
+    "down_block_types": ["DownBlock2D", "DownBlock2D", "DownBlock2D", "DownBlock2D", "AttnDownBlock2D", "DownBlock2D"],
+    "up_block_types": ["UpBlock2D", "AttnUpBlock2D", "UpBlock2D", "UpBlock2D", "UpBlock2D", "UpBlock2D"],
+    "attention_resolutions": [], "cross_attention_resolutions": [], "emb_activation_before_proj": False,
+}
+FWD_GFLOP_PER_IMAGE = 493.15          # SURVEY.md 8(a) a6 / Appendix A (torch.utils.flop_counter on the reference)
+TRAIN_GFLOP_PER_IMAGE = 3 * FWD_GFLOP_PER_IMAGE
+PEAK_BF16_TFLOPS = 2500.0            # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def conv_roofline(dev, iters=20):
+    """Time the dominant kernel live with HIP events: the fused GN+SiLU -> 3x3 conv implicit GEMM
+    at the 256^2 level (128 -> 128 channels, batch 8), the problem that carries 8+3 of the 96
+    convs and ~55% of the UNet's FLOPs."""
+    from fmdiff.runtime import ops
+    N, H, W, C, K = 8, 256, 256, 128, 128
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
+    w = ops.prep_weights(torch.randn(K, C, 3, 3, device=dev, generator=g) * 0.03, 0)
+    a = torch.rand(N, C, device=dev) + 0.5
+    b = torch.randn(N, C, device=dev) * 0.1
+    bias = torch.zeros(K, device=dev)
+    out = torch.empty(N, H, W, K, device=dev, dtype=torch.bfloat16)
+    for _ in range(3):
+        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * N * H * W * K * C * 9
+    return dict(kernel="conv_igemm<128,128,2,2,64> (GN+SiLU prologue, 3x3, 8x256x256x128->128)",
+                ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
+
+
+def cpu_baseline(iters=2):
+    """The oracle (fp32 PyTorch-CPU restatement of the reference, proven bit-exact in
+    tests/test_oracle_golden.py) timed on this host: one FM train step (fwd+bwd+AdamW) at
+    batch 1 on the config-B model, median of ``iters`` after one warm-up."""
+    from oracle import spec as S
+    from oracle import train_step as OT
+    from oracle import unet as U
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    spec = S.derive_spec(LDCT_FM_UNET, "concatenate", 1)
+    sd = {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, 0).items()}
+    g = torch.Generator().manual_seed(0)
+    B = 1
+    clean = torch.rand(B, 1, 256, 256, generator=g)
+    ldct = (clean + 0.05 * torch.randn(B, 1, 256, 256, generator=g)).clamp(0, 1)
+    state = {}
+    times = []
+    for i in range(iters + 1):
+        noise = torch.randn(B, 1, 256, 256, generator=g)
+        t = torch.rand(B, generator=g)
+        t0 = time.perf_counter()
+        for p in sd.values():
+            p.grad = None
+        _, sc = OT.fm_loss(sd, spec, clean, ldct, noise, t, 1000)
+        sc.backward()
+        OT.adamw_step(sd, 1e-4, i + 1, state)
+        dt = time.perf_counter() - t0
+        if i:
+            times.append(dt)
+    times.sort()
+    med = times[len(times) // 2]
+    return dict(value=B / med, unit="train images/s", cores=threads, kind="port",
+                sample=f"oracle FM train step (fwd+bwd+AdamW), batch {B}, 256x256, config-B EfficientUNetND fp32, "
+                       f"median of {iters} after 1 warm-up ({med:.2f} s/step)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--img", type=int, default=256)
+    ap.add_argument("--sampler-steps", type=int, default=50)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sampler", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.pipelines.train.fused import FusedFlowSampler, FusedTrainStep
+
+    torch.manual_seed(1234 + rank)
+    model = DiffusionUNetFactory().build(LDCT_FM_UNET, "concatenate", 1).to(dev)
+    if world > 1:   # identical initial replicas
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    B, HW = args.batch, args.img
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    clean = torch.rand(B, 1, HW, HW, device=dev, generator=g)
+    ldct = (clean + 0.05 * torch.randn(B, 1, HW, HW, device=dev, generator=g)).clamp(0, 1)
+
+    trainer = FusedTrainStep(model, lr=1e-4, warmup=500, total_steps=100 * 1000, num_train_timesteps=1000)
+    use_graph = (not args.no_graph) and world == 1
+    if use_graph:
+        trainer.capture(clean, ldct, warmup_iters=2)
+        run = trainer.replay
+    else:
+        def run():
+            return trainer.step(clean, ldct)
+    for _ in range(args.warmup):
+        loss = run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    loss_v = float(loss.item())
+    ms_step = dt / args.steps * 1e3
+    train_ips = world * B * args.steps / dt
+    log(f"[bench] train: {ms_step:.2f} ms/step, {train_ips:.2f} img/s (world {world}), loss {loss_v:.4f}")
+
+    samp = {}
+    if not args.no_sampler:
+        sampler = FusedFlowSampler(model, args.sampler_steps)
+        init = torch.randn(B, 1, HW, HW, device=dev, generator=g)
+        sampler.sample(init, ldct, use_graph=use_graph)      # warm-up
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        sampler.sample(init, ldct, use_graph=use_graph)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ds = torch.tensor([time.perf_counter() - t0], device=dev)
+        if world > 1:
+            dist.all_reduce(ds, op=dist.ReduceOp.MAX)
+        ds = float(ds.item())
+        samp = dict(sampler_images_per_sec=world * B / ds, sampler_steps_per_sec=args.sampler_steps / ds,
+                    sampler_ms_per_step=ds / args.sampler_steps * 1e3, sampler_steps=args.sampler_steps,
+                    sampler_mfma_frac=(world * B / ds) * args.sampler_steps * FWD_GFLOP_PER_IMAGE
+                    / (world * PEAK_BF16_TFLOPS * 1e3))
+        log(f"[bench] sampler: {samp['sampler_images_per_sec']:.2f} img/s, {samp['sampler_ms_per_step']:.2f} ms/step")
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    roof = conv_roofline(dev)
+    step_tflops = train_ips / world * TRAIN_GFLOP_PER_IMAGE / 1e3
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline()
+        except Exception as e:  # pragma: no cover
+            cpu = dict(value=None, error=str(e))
+    res = {
+        "metric": "train images/sec + sampler steps/sec, LDCT 256x256 UNet at 1/2/4/8 MI355X",
+        "value": train_ips,
+        "unit": "train images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic LDCT-shaped tensors (clean U[0,1], ldct = clamp(clean + 0.05 N(0,1))), random init",
+        "config": {"workload": "LDCT 2D 256x256 flow-matching train step (configs/flow_matching/ldct_flow_matching.json,"
+                               " EfficientUNetND 113M, concatenate conditioning) + 50-step FlowMatchEuler sampler",
+                   "global_batch": world * B, "per_gpu_batch": B, "img": HW, "parallelism": f"dp{world}",
+                   "hipgraph": use_graph},
+        "train_loss": loss_v,
+        "train_mfma_frac": step_tflops / PEAK_BF16_TFLOPS,
+        **samp,
+        "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": None, "kernel": roof["kernel"],
+                     "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

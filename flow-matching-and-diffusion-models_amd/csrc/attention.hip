@@ -1,0 +1,232 @@
+// Token self-attention for the UNet attention blocks (gfx950).
+//
+// q/k/v come straight out of the fused qkv 1x1-conv (NHWC bf16 [B][T][3*inner]);
+// the head split is done by index arithmetic in the loads, so both layouts
+// of the reference run without a copy:
+//   raw = 1: SpatialSelfAttention's raw reshape (src/nn/blocks/attention.py:111-115):
+//            the channel-major (3*inner, T) buffer is reinterpreted as
+//            (heads, T, 3*dh): Q[h][r][d] = flat[h*T*3dh + r*3dh + d], K +dh, V +2dh,
+//            flat f = c*T + t;  output (heads, T, dh) reinterpreted as (inner, T).
+//   raw = 0: DiffusersAttentionND's view/transpose split (attention.py:262-268):
+//            Q[h][r][d] = qkv[r][h*dh + d], K at +inner, V at +2*inner.
+// Forward: one wave per 64 query rows of one (batch, head), online softmax in
+// fp32, K/V staged through LDS in 64-key blocks.  Saves the log-sum-exp so the
+// backward recomputes P (flash-style) without storing the T x T scores.
+// Replaces F.scaled_dot_product_attention (attention.py:42-44).
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+constexpr int DMAX = 64;
+
+struct Map {
+  int T, heads, dh, inner, raw;
+  // element offset of (which in {0:q,1:k,2:v}, head, row, d) inside one batch's [T][3*inner] slab
+  FMD_DEV long off(int which, int h, int r, int d) const {
+    if (raw) {
+      const long f = (long)h * T * 3 * dh + (long)r * 3 * dh + which * dh + d;
+      const long c = f / T, t = f - (f / T) * T;
+      return t * 3 * inner + c;
+    }
+    return (long)r * 3 * inner + which * inner + h * dh + d;
+  }
+  // output element (head, row, d) inside one batch's [T][inner] slab
+  FMD_DEV long ooff(int h, int r, int d) const {
+    if (raw) {
+      const long g = (long)h * T * dh + (long)r * dh + d;
+      const long c = g / T, t = g - (g / T) * T;
+      return t * inner + c;
+    }
+    return (long)r * inner + h * dh + d;
+  }
+};
+
+__global__ __launch_bounds__(64) void attn_fwd_kernel(const bf16r* __restrict__ qkv, Map mp, bf16r* __restrict__ o,
+                                                      float* __restrict__ lse) {
+  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = mp.T, dh = mp.dh;
+  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
+  const int r = qblk * 64 + threadIdx.x;
+  const bool live = r < T;
+  const float scale = 1.0f / sqrtf((float)dh);
+  float q[DMAX], acc[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    q[d] = (live && d < dh) ? bf2f(base[mp.off(0, h, r, d)]) * scale : 0.f;
+    acc[d] = 0.f;
+  }
+  __shared__ float ks[64][DMAX + 1], vs[64][DMAX + 1];
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < T; k0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * dh; i += 64) {
+      const int kr = i / dh, d = i - (i / dh) * dh;
+      const bool ok = k0 + kr < T;
+      ks[kr][d] = ok ? bf2f(base[mp.off(1, h, k0 + kr, d)]) : 0.f;
+      vs[kr][d] = ok ? bf2f(base[mp.off(2, h, k0 + kr, d)]) : 0.f;
+    }
+    __syncthreads();
+    const int nk = min(64, T - k0);
+    for (int j = 0; j < nk; ++j) {
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) sc += q[d] * ks[j][d];
+      const float mn = fmaxf(m, sc);
+      const float corr = __expf(m - mn);
+      const float p = __expf(sc - mn);
+      l = l * corr + p;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) acc[d] = acc[d] * corr + p * vs[j][d];
+      m = mn;
+    }
+  }
+  if (!live) return;
+  const float inv = 1.f / l;
+  bf16r* ob = o + (size_t)b * T * mp.inner;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d)
+    if (d < dh) ob[mp.ooff(h, r, d)] = (bf16r)f2bf(acc[d] * inv);
+  lse[((size_t)b * mp.heads + h) * T + r] = m + logf(l);
+}
+
+// pass 1 (per query row): delta = sum_d dO*O, dQ = scale * sum_k dS K
+__global__ __launch_bounds__(64) void attn_bwd_q_kernel(const bf16r* __restrict__ qkv, const bf16r* __restrict__ o,
+                                                        const bf16r* __restrict__ dout, const float* __restrict__ lse,
+                                                        Map mp, float* __restrict__ delta,
+                                                        bf16r* __restrict__ dqkv) {
+  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = mp.T, dh = mp.dh;
+  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
+  const bf16r* ob = o + (size_t)b * T * mp.inner;
+  const bf16r* dob = dout + (size_t)b * T * mp.inner;
+  const int r = qblk * 64 + threadIdx.x;
+  const bool live = r < T;
+  const float scale = 1.0f / sqrtf((float)dh);
+  float q[DMAX], dq[DMAX], dov[DMAX];
+  float dl = 0.f;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    const bool ok = live && d < dh;
+    q[d] = ok ? bf2f(base[mp.off(0, h, r, d)]) * scale : 0.f;
+    dov[d] = ok ? bf2f(dob[mp.ooff(h, r, d)]) : 0.f;
+    dl += ok ? dov[d] * bf2f(ob[mp.ooff(h, r, d)]) : 0.f;
+    dq[d] = 0.f;
+  }
+  const float L = live ? lse[((size_t)b * mp.heads + h) * T + r] : 0.f;
+  __shared__ float ks[64][DMAX + 1], vs[64][DMAX + 1];
+  for (int k0 = 0; k0 < T; k0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * dh; i += 64) {
+      const int kr = i / dh, d = i - (i / dh) * dh;
+      const bool ok = k0 + kr < T;
+      ks[kr][d] = ok ? bf2f(base[mp.off(1, h, k0 + kr, d)]) : 0.f;
+      vs[kr][d] = ok ? bf2f(base[mp.off(2, h, k0 + kr, d)]) : 0.f;
+    }
+    __syncthreads();
+    const int nk = min(64, T - k0);
+    for (int j = 0; j < nk; ++j) {
+      float sc = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) { sc += q[d] * ks[j][d]; dp += dov[d] * vs[j][d]; }
+      const float p = __expf(sc - L);
+      const float ds = p * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) dq[d] += ds * ks[j][d];
+    }
+  }
+  if (!live) return;
+  delta[((size_t)b * mp.heads + h) * T + r] = dl;
+  bf16r* db = dqkv + (size_t)b * T * 3 * mp.inner;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d)
+    if (d < dh) db[mp.off(0, h, r, d)] = (bf16r)f2bf(dq[d] * scale);
+}
+
+// pass 2 (per key row): dV = sum_q P dO,  dK = scale * sum_q dS Q
+__global__ __launch_bounds__(64) void attn_bwd_kv_kernel(const bf16r* __restrict__ qkv, const bf16r* __restrict__ dout,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, Map mp,
+                                                         bf16r* __restrict__ dqkv) {
+  const int kblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = mp.T, dh = mp.dh;
+  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
+  const bf16r* dob = dout + (size_t)b * T * mp.inner;
+  const int r = kblk * 64 + threadIdx.x;
+  const bool live = r < T;
+  const float scale = 1.0f / sqrtf((float)dh);
+  float kv[DMAX], vv[DMAX], dk[DMAX], dv[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    const bool ok = live && d < dh;
+    kv[d] = ok ? bf2f(base[mp.off(1, h, r, d)]) : 0.f;
+    vv[d] = ok ? bf2f(base[mp.off(2, h, r, d)]) : 0.f;
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+  __shared__ float qs[64][DMAX + 1], dos[64][DMAX + 1], ls[64], dls[64];
+  for (int q0 = 0; q0 < T; q0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * dh; i += 64) {
+      const int qr = i / dh, d = i - (i / dh) * dh;
+      const bool ok = q0 + qr < T;
+      qs[qr][d] = ok ? bf2f(base[mp.off(0, h, q0 + qr, d)]) * scale : 0.f;
+      dos[qr][d] = ok ? bf2f(dob[mp.ooff(h, q0 + qr, d)]) : 0.f;
+    }
+    if (q0 + (int)threadIdx.x < T) {
+      ls[threadIdx.x] = lse[((size_t)b * mp.heads + h) * T + q0 + threadIdx.x];
+      dls[threadIdx.x] = delta[((size_t)b * mp.heads + h) * T + q0 + threadIdx.x];
+    }
+    __syncthreads();
+    const int nq = min(64, T - q0);
+    for (int j = 0; j < nq; ++j) {
+      float sc = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) { sc += qs[j][d] * kv[d]; dp += dos[j][d] * vv[d]; }
+      const float p = __expf(sc - ls[j]);
+      const float ds = p * (dp - dls[j]);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < dh) { dv[d] += p * dos[j][d]; dk[d] += ds * qs[j][d]; }
+    }
+  }
+  if (!live) return;
+  bf16r* db = dqkv + (size_t)b * T * 3 * mp.inner;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d)
+    if (d < dh) {
+      db[mp.off(1, h, r, d)] = (bf16r)f2bf(dk[d]);   // qs already carries the scale
+      db[mp.off(2, h, r, d)] = (bf16r)f2bf(dv[d]);
+    }
+}
+
+}  // namespace
+
+extern "C" int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw,
+                                 void* o, float* lse, fmd_stream_t s) {
+  if (dh > DMAX || dh < 1) return -1;
+  Map mp{T, heads, dh, heads * dh, raw};
+  dim3 grid((T + 63) / 64, heads, B);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, mp, (bf16r*)o, lse);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* delta,
+                                  int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw, void* dqkv,
+                                  fmd_stream_t s) {
+  if (dh > DMAX || dh < 1) return -1;
+  Map mp{T, heads, dh, heads * dh, raw};
+  dim3 grid((T + 63) / 64, heads, B);
+  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)o,
+                     (const bf16r*)dout, lse, mp, delta, (bf16r*)dqkv);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)dout, lse,
+                     delta, mp, (bf16r*)dqkv);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,58 @@
+// Shared device helpers for the fmdiff gfx950 (MI355X / CDNA4) kernels.
+// Activations are NHWC bf16 ("pixel rows, channels contiguous"), statistics and
+// accumulators fp32.  Wave = 64 lanes; MFMA = v_mfma_f32_16x16x32_bf16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FMD_DEV __device__ __forceinline__
+
+typedef uint16_t bf16r;                                           // raw bf16 bits in memory
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;        // MFMA A/B fragment (4 VGPR)
+typedef __attribute__((ext_vector_type(4))) float f32x4;          // MFMA 16x16 accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;   // 16-byte vector
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;   // 8-byte vector
+typedef __attribute__((ext_vector_type(4))) short s16x4;          // ds_read_tr16_b64 result
+
+FMD_DEV float bf2f(unsigned int raw16) { return __uint_as_float(raw16 << 16); }
+FMD_DEV float bf_lo(unsigned int w) { return __uint_as_float(w << 16); }
+FMD_DEV float bf_hi(unsigned int w) { return __uint_as_float(w & 0xffff0000u); }
+
+// round-to-nearest-even fp32 -> bf16 (hipcc emits v_cvt_pk_bf16_f32; keeps NaN a NaN)
+FMD_DEV unsigned int f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return (unsigned int)__builtin_bit_cast(unsigned short, b);
+}
+FMD_DEV unsigned int pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+
+FMD_DEV float sigmoidf_(float z) { return 1.0f / (1.0f + __expf(-z)); }
+FMD_DEV float siluf_(float z) { return z * sigmoidf_(z); }
+// d silu / dz
+FMD_DEV float silu_grad(float z) {
+  float s = sigmoidf_(z);
+  return s * (1.0f + z * (1.0f - s));
+}
+
+FMD_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// gfx950 ds_read_b64_tr_b16: 16-lane group reads a 4-row x 16-col bf16 block;
+// lane 4q+p supplies &T[row q][col 4p], lane i receives column i (rows 0..3).
+FMD_DEV s16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_ptr));
+}
+
+FMD_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// XCD-aware bijective block remap: blocks b, b+8, ... share one XCD's L2; give
+// each XCD a contiguous range of the logical grid (cdna_hip_programming.md T1).
+FMD_DEV int xcd_remap(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = b & 7, k = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}

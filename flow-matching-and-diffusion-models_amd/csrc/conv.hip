@@ -1,0 +1,485 @@
+// Implicit-GEMM convolution for gfx950 (forward and data-gradient modes).
+//
+// GEMM view: D[cout][pixel] = sum_{tap, cin} W[cout][tap][cin] * G[pixel][tap][cin]
+// where G is the im2col gather of the (virtually concatenated, optionally
+// nearest-x2-upsampled, GroupNorm-affine+SiLU-transformed) NHWC bf16 input.
+// MFMA A operand = weight tile (cout rows), B operand = gathered pixel tile,
+// so each lane ends with 4 consecutive output channels of one pixel (8-byte
+// bf16 stores).  Tiles are staged through LDS with a 16-byte-chunk XOR swizzle
+// (conflict-free ds_read_b128), double buffered with register prefetch.
+//
+// Replaces (reference): ConvND/nn.Conv2d (src/nn/ops/convolution.py:8-54),
+// GroupNorm+SiLU(+scale/shift) feeding a conv (src/nn/blocks/residual.py:95-117),
+// F.interpolate nearest x2 + conv (src/nn/ops/upsampling.py:27-29), stride-2
+// DownsampleND (upsampling.py:49-56), torch.cat([h, skip]) (src/models/unet/unet.py:322),
+// the 1x1 skip conv + residual add (residual.py:77-82,120), and their autograd
+// data gradients (transposed gather).
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+struct KArgs {
+  fmd_conv_desc d;
+  int M;          // N*Ho*Wo
+  int T;          // ks*ks taps
+  int C;          // C0 + C1
+  int nk1;        // K-iterations of the main segment: ceil(C/BK)*T
+  int nk;         // total K-iterations (main + 1x1 segment)
+  int per_split;  // K-iterations per split
+  int ntp, ntc;   // pixel tiles, cout tiles
+  int stats_rows; // pixels per stats slab row (64) or 0
+};
+
+template <int BCO, int BPX, int WM, int WN, int BK>
+__global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
+  constexpr int NT = 256;
+  constexpr int CH = BK / 8;                  // 16-byte chunks per LDS row
+  constexpr int RPP = NT / CH;                // rows covered per load pass
+  constexpr int AW = (BCO + RPP - 1) / RPP;   // weight chunks per thread
+  constexpr int AX = BPX / RPP;               // pixel chunks per thread
+  constexpr int TM = BCO / (WM * 16);
+  constexpr int TN = BPX / (WN * 16);
+  constexpr int KS = BK / 32;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(BPX % RPP == 0, "pixel tile");
+  __shared__ __attribute__((aligned(16))) bf16r lds[2 * (BCO + BPX) * BK];
+
+  const fmd_conv_desc& d = A.d;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int nwg = A.ntp * A.ntc;
+  const int b = xcd_remap(blockIdx.x, nwg);
+  const int tco = b % A.ntc, tpx = b / A.ntc;
+  const int co0 = tco * BCO, px0 = tpx * BPX;
+  const int split = blockIdx.y;
+  const int kk0 = split * A.per_split;
+  const int kk1 = min(A.nk, kk0 + A.per_split);
+
+  const int HWo = d.Ho * d.Wo;
+  const int cch = tid % CH;      // this thread's 16B chunk within a BK slice
+  const int rbase = tid / CH;
+
+  // per-thread pixel rows
+  int pn[AX], poy[AX], pox[AX];
+#pragma unroll
+  for (int j = 0; j < AX; ++j) {
+    const int p = px0 + rbase + j * RPP;
+    if (p < A.M) {
+      const int n = p / HWo;
+      const int rem = p - n * HWo;
+      pn[j] = n;
+      poy[j] = rem / d.Wo;
+      pox[j] = rem - poy[j] * d.Wo;
+    } else {
+      pn[j] = -1; poy[j] = 0; pox[j] = 0;
+    }
+  }
+
+  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
+  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
+  const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
+  const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
+  const int C23 = d.C2 + d.C3;
+  const bf16r* __restrict__ w1 = (const bf16r*)d.wgt;
+  const bf16r* __restrict__ w2 = (const bf16r*)d.wgt2;
+  const bool pro = d.pro_a != nullptr;
+
+  u32x4 rw[AW], rx[AX];
+  bool vx[AX];
+  int cur_c = 0, cur_seg = 0;
+
+  auto load = [&](int kk) {
+    int c, tap = 0, seg;
+    if (kk < A.nk1) {
+      const int cb = kk / A.T;
+      tap = kk - cb * A.T;
+      c = cb * BK + cch * 8;
+      seg = 0;
+    } else {
+      c = (kk - A.nk1) * BK + cch * 8;
+      seg = 1;
+    }
+    cur_c = c;
+    cur_seg = seg;
+    const int ky = tap / d.ks, kx = tap - (tap / d.ks) * d.ks;
+    // weights
+#pragma unroll
+    for (int j = 0; j < AW; ++j) {
+      const int r = rbase + j * RPP;
+      const int co = co0 + r;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (r < BCO && co < d.K) {
+        if (seg == 0) {
+          if (c < A.C) v = *(const u32x4*)(w1 + ((size_t)co * A.T + tap) * A.C + c);
+        } else {
+          if (c < C23) v = *(const u32x4*)(w2 + (size_t)co * C23 + c);
+        }
+      }
+      rw[j] = v;
+    }
+    // activations (gather)
+#pragma unroll
+    for (int j = 0; j < AX; ++j) {
+      const int n = pn[j];
+      bool ok = n >= 0;
+      const bf16r* ptr = nullptr;
+      if (seg == 0) {
+        int sy, sx;
+        if (!d.transposed) {
+          const int iy = poy[j] * d.stride + ky - d.pad;
+          const int ix = pox[j] * d.stride + kx - d.pad;
+          if (d.upsample) {
+            ok = ok && iy >= 0 && iy < 2 * d.Hs && ix >= 0 && ix < 2 * d.Ws;
+            sy = iy >> 1; sx = ix >> 1;
+          } else {
+            ok = ok && iy >= 0 && iy < d.Hs && ix >= 0 && ix < d.Ws;
+            sy = iy; sx = ix;
+          }
+        } else {
+          const int ny = poy[j] + d.pad - ky;
+          const int nx = pox[j] + d.pad - kx;
+          ok = ok && ny >= 0 && nx >= 0;
+          if (d.stride == 2) {
+            ok = ok && !(ny & 1) && !(nx & 1);
+            sy = ny >> 1; sx = nx >> 1;
+          } else {
+            sy = ny; sx = nx;
+          }
+          ok = ok && sy < d.Hs && sx < d.Ws;
+        }
+        ok = ok && c < A.C;
+        if (ok) {
+          const size_t pix = ((size_t)n * d.Hs + sy) * d.Ws + sx;
+          ptr = (c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0);
+        }
+      } else {
+        ok = ok && c < C23;
+        if (ok) {
+          const size_t pix = (size_t)(px0 + rbase + j * RPP);
+          ptr = (c < d.C2) ? s2 + pix * d.C2 + c : s3 + pix * d.C3 + (c - d.C2);
+        }
+      }
+      vx[j] = ok;
+      rx[j] = ok ? *(const u32x4*)ptr : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  auto transform = [&]() {
+    if (!pro || cur_seg != 0) return;
+    const int c = cur_c;
+#pragma unroll
+    for (int j = 0; j < AX; ++j) {
+      if (!vx[j]) continue;
+      const float* pa = d.pro_a + (size_t)pn[j] * A.C + c;
+      const float* pb = d.pro_b + (size_t)pn[j] * A.C + c;
+      const f32x4 a0 = *(const f32x4*)pa, a1 = *(const f32x4*)(pa + 4);
+      const f32x4 b0 = *(const f32x4*)pb, b1 = *(const f32x4*)(pb + 4);
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      u32x4 v = rx[j];
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = bf_lo(v[e]) * av[2 * e] + bv[2 * e];
+        float hi = bf_hi(v[e]) * av[2 * e + 1] + bv[2 * e + 1];
+        if (d.pro_silu) { lo = siluf_(lo); hi = siluf_(hi); }
+        o[e] = pack2(lo, hi);
+      }
+      rx[j] = o;
+    }
+  };
+
+  auto store = [&](int buf) {
+    bf16r* la = lds + buf * (BCO + BPX) * BK;
+    bf16r* lx = la + BCO * BK;
+#pragma unroll
+    for (int j = 0; j < AW; ++j) {
+      const int r = rbase + j * RPP;
+      if (r < BCO) *(u32x4*)(la + r * BK + 8 * (cch ^ (r & (CH - 1)))) = rw[j];
+    }
+#pragma unroll
+    for (int j = 0; j < AX; ++j) {
+      const int r = rbase + j * RPP;
+      *(u32x4*)(lx + r * BK + 8 * (cch ^ (r & (CH - 1)))) = rx[j];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int l16 = lane & 15, lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16r* la = lds + buf * (BCO + BPX) * BK;
+    const bf16r* lx = la + BCO * BK;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kc = 4 * ks + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * (BCO / WM) + 16 * i + l16;
+        af[i] = *(const bf16x8*)(la + r * BK + 8 * (kc ^ (r & (CH - 1))));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * (BPX / WN) + 16 * j + l16;
+        bfr[j] = *(const bf16x8*)(lx + r * BK + 8 * (kc ^ (r & (CH - 1))));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+  };
+
+  if (kk0 < kk1) {
+    load(kk0);
+    transform();
+    store(0);
+    __syncthreads();
+    for (int kk = kk0; kk < kk1; ++kk) {
+      const int buf = (kk - kk0) & 1;
+      const bool nxt = kk + 1 < kk1;
+      if (nxt) load(kk + 1);
+      compute(buf);
+      if (nxt) {
+        transform();
+        store(buf ^ 1);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------ epilogue
+  const int K = d.K;
+  if (d.splits > 1) {
+    float* ws = d.ws + (size_t)split * A.M * K;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = co0 + wm * (BCO / WM) + 16 * i + 4 * lq;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int p = px0 + wn * (BPX / WN) + 16 * j + l16;
+        if (p >= A.M) continue;
+        float* dst = ws + (size_t)p * K + co;
+        if (co + 3 < K) {
+          *(f32x4*)dst = acc[i][j];
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) dst[r] = acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
+
+  const bool stats = d.stats != nullptr;
+  const bool dep = d.ep_a != nullptr;
+  const bool hasx = d.ep_x0 != nullptr;
+  float st1[TM][4], st2[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { st1[i][r] = 0.f; st2[i][r] = 0.f; }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = co0 + wm * (BCO / WM) + 16 * i + 4 * lq;
+    if (co >= K) continue;
+    const bool full = co + 3 < K;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (d.bias) {
+      for (int r = 0; r < 4; ++r) bias[r] = (co + r < K) ? d.bias[co + r] : 0.f;
+    }
+    if (d.bias2) {
+      for (int r = 0; r < 4; ++r) bias[r] += (co + r < K) ? d.bias2[co + r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int p = px0 + wn * (BPX / WN) + 16 * j + l16;
+      if (p >= A.M) continue;
+      const int n = p / HWo;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[r];
+      if (d.bias_nc) {
+        for (int r = 0; r < 4; ++r)
+          if (co + r < K) v[r] += d.bias_nc[(size_t)n * K + co + r];
+      }
+      if (d.resid) {
+        const bf16r* rp = (const bf16r*)d.resid + (size_t)p * K + co;
+        if (full) {
+          const u32x2 rr = *(const u32x2*)rp;
+          v[0] += bf_lo(rr[0]); v[1] += bf_hi(rr[0]); v[2] += bf_lo(rr[1]); v[3] += bf_hi(rr[1]);
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) v[r] += bf2f(rp[r]);
+        }
+      }
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (hasx) {
+        // data-gradient epilogue: dz = d(act) * silu'(a*x + b), x = forward GN input
+        const int C0e = d.ep_C0;
+        for (int r = 0; r < 4; ++r) {
+          const int c = co + r;
+          if (c >= K) continue;
+          const bf16r* xp = (c < C0e) ? (const bf16r*)d.ep_x0 + (size_t)p * C0e + c
+                                      : (const bf16r*)d.ep_x1 + (size_t)p * (K - C0e) + (c - C0e);
+          const float x = bf2f(*xp);
+          xv[r] = x;
+          if (dep) {
+            const float z = d.ep_a[(size_t)n * K + c] * x + d.ep_b[(size_t)n * K + c];
+            v[r] *= silu_grad(z);
+          }
+        }
+      }
+      if (d.out_f32) {
+        float* op = (float*)d.out + (size_t)p * K + co;
+        for (int r = 0; r < 4; ++r)
+          if (co + r < K) op[r] = d.accumulate ? op[r] + v[r] : v[r];
+      } else {
+        bf16r* op = (bf16r*)d.out + (size_t)p * K + co;
+        if (full) {
+          if (d.accumulate) {
+            const u32x2 o = *(const u32x2*)op;
+            v[0] += bf_lo(o[0]); v[1] += bf_hi(o[0]); v[2] += bf_lo(o[1]); v[3] += bf_hi(o[1]);
+          }
+          u32x2 o;
+          o[0] = pack2(v[0], v[1]);
+          o[1] = pack2(v[2], v[3]);
+          *(u32x2*)op = o;
+          // statistics are taken on the rounded values the consumer will read
+          v[0] = bf_lo(o[0]); v[1] = bf_hi(o[0]); v[2] = bf_lo(o[1]); v[3] = bf_hi(o[1]);
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) {
+              float w = d.accumulate ? bf2f(op[r]) + v[r] : v[r];
+              op[r] = (bf16r)f2bf(w);
+              v[r] = bf2f(op[r]);
+            }
+        }
+      }
+      if (stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st1[i][r] += v[r];
+          st2[i][r] += hasx ? v[r] * xv[r] : v[r] * v[r];
+        }
+      }
+    }
+  }
+  if (stats) {
+    // reduce over the 16 pixel lanes of each quad-row; the wave's pixels are one image
+    const int srow = (px0 + wn * (BPX / WN)) / A.stats_rows;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = st1[i][r], q = st2[i][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        const int co = co0 + wm * (BCO / WM) + 16 * i + 4 * lq + r;
+        if (l16 == 0 && co < K) {
+          float* sp = d.stats + ((size_t)srow * K + co) * 2;
+          sp[0] = a;
+          sp[1] = q;
+        }
+      }
+    }
+  }
+}
+
+__global__ void splitk_reduce(const fmd_conv_desc d, int M) {
+  const int K = d.K;
+  const int HWo = d.Ho * d.Wo;
+  const size_t total = (size_t)M * K;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int p = (int)(idx / K);
+    const int c = (int)(idx - (size_t)p * K);
+    const int n = p / HWo;
+    float v = 0.f;
+    for (int s = 0; s < d.splits; ++s) v += d.ws[(size_t)s * total + idx];
+    if (d.bias) v += d.bias[c];
+    if (d.bias2) v += d.bias2[c];
+    if (d.bias_nc) v += d.bias_nc[(size_t)n * K + c];
+    if (d.resid) v += bf2f(((const bf16r*)d.resid)[idx]);
+    if (d.ep_a) {
+      const int C0e = d.ep_C0;
+      const float x = (c < C0e) ? bf2f(((const bf16r*)d.ep_x0)[(size_t)p * C0e + c])
+                                : bf2f(((const bf16r*)d.ep_x1)[(size_t)p * (K - C0e) + (c - C0e)]);
+      v *= silu_grad(d.ep_a[(size_t)n * K + c] * x + d.ep_b[(size_t)n * K + c]);
+    }
+    if (d.out_f32) {
+      float* o = (float*)d.out + idx;
+      *o = d.accumulate ? *o + v : v;
+    } else {
+      bf16r* o = (bf16r*)d.out + idx;
+      *o = (bf16r)f2bf(d.accumulate ? bf2f(*o) + v : v);
+    }
+  }
+}
+
+template <int BCO, int BPX, int WM, int WN, int BK>
+int launch(const fmd_conv_desc* d, hipStream_t s) {
+  KArgs A;
+  A.d = *d;
+  A.M = d->N * d->Ho * d->Wo;
+  A.T = d->ks * d->ks;
+  A.C = d->C0 + d->C1;
+  A.nk1 = ((A.C + BK - 1) / BK) * A.T;
+  A.nk = A.nk1 + (d->src2 ? (d->C2 + d->C3 + BK - 1) / BK : 0);
+  const int splits = d->splits > 1 ? d->splits : 1;
+  A.per_split = (A.nk + splits - 1) / splits;
+  A.ntp = (A.M + BPX - 1) / BPX;
+  A.ntc = (d->K + BCO - 1) / BCO;
+  A.stats_rows = 64;
+  if (d->stats) {
+    // every wave's pixel range must be one image and full
+    const int wrows = BPX / WN;
+    if (wrows != 64 || (d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
+  }
+  dim3 grid(A.ntp * A.ntc, splits);
+  hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK>), grid, dim3(256), 0, s, A);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int C = d->C0 + d->C1;
+  if ((d->C0 % 8) || (d->C1 % 8) || (d->C2 % 8) || (d->C3 % 8) || d->ks < 1 || d->N < 1) return -1;
+  if (d->C3 && !d->src3) return -6;
+  if (d->C1 && !d->src1) return -2;
+  if (d->src2 && !d->wgt2) return -3;
+  if (d->pro_a && !d->pro_b) return -4;
+  if (d->splits > 1 && (!d->ws || d->stats)) return -5;
+  (void)C;
+  int rc;
+  if (d->K <= 16)
+    rc = launch<16, 256, 1, 4, 64>(d, s);
+  else if (d->K <= 64)
+    rc = launch<64, 128, 2, 2, 64>(d, s);
+  else
+    rc = launch<128, 128, 2, 2, 64>(d, s);
+  if (rc) return rc;
+  if (d->splits > 1) {
+    const int M = d->N * d->Ho * d->Wo;
+    const size_t total = (size_t)M * d->K;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, s, *d, M);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}

@@ -1,0 +1,295 @@
+// GroupNorm (+ResBlock scale/shift) as folded per-(n,c) affines, forward and
+// backward, for gfx950.
+//
+// Forward: producers emit per-channel partial sums (conv epilogue slab or
+// fmd_channel_stats); fmd_gn_prep reduces them per (n, group) in fp64, and
+// folds mean/rstd, gamma/beta and the time-embedding scale/shift of
+// ResBlockND (src/nn/blocks/residual.py:106-117) into a[n][c], b[n][c] so the
+// consuming conv prologue computes silu(a*x + b).
+// Backward: with S1 = sum dz, S2 = sum dz*x per (n,c) (conv data-gradient
+// epilogue), dx = P*dz + Q*x + R exactly (P, Q, R per (n,c)); gamma/beta and
+// scale/shift gradients come from the same sums.
+//
+// Replaces nn.GroupNorm (src/nn/ops/normalization.py:11-19,
+// src/nn/blocks/attention.py:97,210) and its autograd.
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+// x [N][HW][C] bf16 -> slab [N*splits][C][2]; mode 0: (sum x, sum x^2);
+// mode 1: (sum dz, sum dz*x) with dz = x, and the second tensor y = the forward input.
+__global__ void channel_stats_kernel(const bf16r* __restrict__ x, const bf16r* __restrict__ y0,
+                                     const bf16r* __restrict__ y1, int C0, int N, int HW, int C, int rows,
+                                     float* __restrict__ out) {
+  // block: (n*splits + split, channel block of 64); 256 threads = 8 chunks x 32 pixel lanes
+  const int nsplit = HW / rows;
+  const int row = blockIdx.x;           // n*nsplit + split
+  const int n = row / nsplit, sp = row - n * nsplit;
+  const int cblk = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  const int ch = t & 7, pl = t >> 3;
+  const int c = cblk + ch * 8;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  if (c < C) {
+    const size_t base = (size_t)n * HW + (size_t)sp * rows;
+    for (int p = pl; p < rows; p += 32) {
+      const size_t pix = base + p;
+      const u32x4 v = *(const u32x4*)(x + pix * C + c);
+      float xv[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { xv[2 * e] = bf_lo(v[e]); xv[2 * e + 1] = bf_hi(v[e]); }
+      if (y0) {
+        const u32x4 w = (c < C0) ? *(const u32x4*)(y0 + pix * C0 + c) : *(const u32x4*)(y1 + pix * (C - C0) + (c - C0));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[2 * e] += xv[2 * e];
+          s1[2 * e + 1] += xv[2 * e + 1];
+          s2[2 * e] += xv[2 * e] * bf_lo(w[e]);
+          s2[2 * e + 1] += xv[2 * e + 1] * bf_hi(w[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += xv[e]; s2[e] += xv[e] * xv[e]; }
+      }
+    }
+  }
+  __shared__ float red[32][8][2][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[pl][ch][0][e] = s1[e]; red[pl][ch][1][e] = s2[e]; }
+  __syncthreads();
+  if (t < 128) {
+    const int cc = t >> 1, k = t & 1;   // 64 channels x 2 sums
+    const int chh = cc >> 3, e = cc & 7;
+    float a = 0.f;
+    for (int i = 0; i < 32; ++i) a += red[i][chh][k][e];
+    if (cblk + cc < C) out[((size_t)row * C + cblk + cc) * 2 + k] = a;
+  }
+}
+
+// one block per (n, group)
+__global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const float* __restrict__ st1, int rows1,
+                               int N, int HW, int C0, int C1, int G, float eps, const float* __restrict__ gamma,
+                               const float* __restrict__ beta, const float* __restrict__ emb, int emb_stride,
+                               int emb_mode, float* __restrict__ a, float* __restrict__ b,
+                               float* __restrict__ mr) {
+  const int n = blockIdx.x / G, g = blockIdx.x - (blockIdx.x / G) * G;
+  const int C = C0 + C1;
+  const int Cg = C / G;
+  const int c_begin = g * Cg;
+  const int E0 = HW / rows0;
+  const int E1 = C1 ? HW / rows1 : 0;
+  double s1 = 0.0, s2 = 0.0;
+  for (int idx = threadIdx.x;; idx += blockDim.x) {
+    // enumerate (channel in group, entry)
+    const int maxE = E0 > E1 ? E0 : E1;
+    if (idx >= Cg * maxE) break;
+    const int cl = idx / maxE, e = idx - cl * maxE;
+    const int c = c_begin + cl;
+    if (c < C0) {
+      if (e < E0) {
+        const float* p = st0 + (((size_t)n * E0 + e) * C0 + c) * 2;
+        s1 += p[0]; s2 += p[1];
+      }
+    } else {
+      if (e < E1) {
+        const float* p = st1 + (((size_t)n * E1 + e) * C1 + (c - C0)) * 2;
+        s1 += p[0]; s2 += p[1];
+      }
+    }
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1; r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) { r1[threadIdx.x] += r1[threadIdx.x + o]; r2[threadIdx.x] += r2[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  const double cnt = (double)Cg * HW;
+  const double mean = r1[0] / cnt;
+  double var = r2[0] / cnt - mean * mean;
+  if (var < 0) var = 0;
+  const float meanf = (float)mean;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (threadIdx.x == 0 && mr) { mr[((size_t)n * G + g) * 2] = meanf; mr[((size_t)n * G + g) * 2 + 1] = rstd; }
+  for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
+    const int c = c_begin + cl;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    float av = rstd * gm;
+    float bv = bt - meanf * av;
+    if (emb_mode == 1) {
+      const float s = 1.f + emb[(size_t)n * emb_stride + c];
+      const float sh = emb[(size_t)n * emb_stride + C + c];
+      av *= s;
+      bv = bv * s + sh;
+    }
+    a[(size_t)n * C + c] = av;
+    b[(size_t)n * C + c] = bv;
+  }
+}
+
+// one block per group; loops over n so gamma/beta grads are complete per block
+__global__ void gn_bwd_prep_kernel(const float* __restrict__ s12, int rows, int N, int HW, int C, int G,
+                                   const float* __restrict__ mr, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, const float* __restrict__ emb, int emb_stride,
+                                   int emb_mode, float* __restrict__ P, float* __restrict__ Q, float* __restrict__ R,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ demb,
+                                   int demb_stride, const float* __restrict__ fst, int frows) {
+  const int g = blockIdx.x;
+  const int Cg = C / G;
+  const int E = HW / rows;
+  __shared__ double sh1[1024], sh2[1024];   // per-channel S1, S2 (Cg <= 1024)
+  __shared__ double red[2][256];
+  double dg_acc[4] = {0, 0, 0, 0}, db_acc[4] = {0, 0, 0, 0};   // channels threadIdx.x + 256*k
+  for (int n = 0; n < N; ++n) {
+    const float mean = mr[((size_t)n * G + g) * 2], rstd = mr[((size_t)n * G + g) * 2 + 1];
+    double a1 = 0.0, a2 = 0.0;
+    for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
+      const int c = g * Cg + cl;
+      double S1 = 0.0, S2 = 0.0;
+      for (int e = 0; e < E; ++e) {
+        const float* p = s12 + (((size_t)n * E + e) * C + c) * 2;
+        S1 += p[0]; S2 += p[1];
+      }
+      sh1[cl] = S1; sh2[cl] = S2;
+      const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
+      const double gp = (double)(gamma ? gamma[c] : 1.f) * s;
+      const double dzxh = (double)rstd * (S2 - (double)mean * S1);
+      a1 += gp * S1;
+      a2 += gp * dzxh;
+    }
+    red[0][threadIdx.x] = a1; red[1][threadIdx.x] = a2;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) { red[0][threadIdx.x] += red[0][threadIdx.x + o]; red[1][threadIdx.x] += red[1][threadIdx.x + o]; }
+      __syncthreads();
+    }
+    const double cnt = (double)Cg * HW;
+    const double A1 = red[0][0] / cnt, A2 = red[1][0] / cnt;
+    const double r = rstd;
+    for (int cl = threadIdx.x, k = 0; cl < Cg; cl += blockDim.x, ++k) {
+      const int c = g * Cg + cl;
+      const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
+      const double gm = gamma ? gamma[c] : 1.f;
+      const double bt = beta ? beta[c] : 0.f;
+      const double gp = gm * s;
+      const double S1 = sh1[cl], S2 = sh2[cl];
+      const double dzxh = r * (S2 - (double)mean * S1);
+      P[(size_t)n * C + c] = (float)(r * gp);
+      Q[(size_t)n * C + c] = (float)(-r * r * A2);
+      R[(size_t)n * C + c] = (float)(r * r * A2 * mean - r * A1);
+      if (k < 4) { dg_acc[k] += s * dzxh; db_acc[k] += s * S1; }
+      if (emb_mode == 1 && demb) {
+        demb[(size_t)n * demb_stride + c] = (float)(gm * dzxh + bt * S1);
+        demb[(size_t)n * demb_stride + C + c] = (float)S1;
+      }
+      if (emb_mode == 2 && demb) {
+        // sum_hw dx = P*S1 + Q*sum_hw x + R*HW, sum_hw x from the forward statistics
+        const int FE = HW / frows;
+        double sx = 0.0;
+        for (int e = 0; e < FE; ++e) sx += fst[(((size_t)n * FE + e) * C + c) * 2];
+        demb[(size_t)n * demb_stride + c] =
+            (float)(r * gp * S1 + (-r * r * A2) * sx + (r * r * A2 * mean - r * A1) * (double)HW);
+      }
+    }
+    __syncthreads();
+  }
+  for (int cl = threadIdx.x, k = 0; cl < Cg && k < 4; cl += blockDim.x, ++k) {
+    const int c = g * Cg + cl;
+    if (dgamma) dgamma[c] += (float)dg_acc[k];
+    if (dbeta) dbeta[c] += (float)db_acc[k];
+  }
+}
+
+// dx = P*dz + Q*x + R (+ extra), split into two destinations at C0
+__global__ void gn_bwd_apply_kernel(const bf16r* __restrict__ dz, const bf16r* __restrict__ x0,
+                                    const bf16r* __restrict__ x1, int C0, int C1, long long M, int HW,
+                                    const float* __restrict__ P, const float* __restrict__ Q,
+                                    const float* __restrict__ R, const bf16r* __restrict__ extra,
+                                    bf16r* __restrict__ dx0, int acc0, bf16r* __restrict__ dx1, int acc1) {
+  const int C = C0 + C1;
+  const int CH = C / 8;
+  const long long total = M * CH;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long p = i / CH;
+    const int c = (int)(i - p * CH) * 8;
+    const int n = (int)(p / HW);
+    const u32x4 vz = *(const u32x4*)(dz + p * C + c);
+    const bool first = c < C0;
+    const u32x4 vx = first ? *(const u32x4*)(x0 + p * C0 + c) : *(const u32x4*)(x1 + p * C1 + (c - C0));
+    u32x4 ve = {0u, 0u, 0u, 0u};
+    if (extra) ve = *(const u32x4*)(extra + p * C + c);
+    const float* pp = P + (size_t)n * C + c;
+    const float* qq = Q + (size_t)n * C + c;
+    const float* rr = R + (size_t)n * C + c;
+    bf16r* dst = first ? dx0 + p * C0 + c : dx1 + p * C1 + (c - C0);
+    const int acc = first ? acc0 : acc1;
+    u32x4 old = {0u, 0u, 0u, 0u};
+    if (acc) old = *(const u32x4*)dst;
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float lo = pp[2 * e] * bf_lo(vz[e]) + qq[2 * e] * bf_lo(vx[e]) + rr[2 * e];
+      float hi = pp[2 * e + 1] * bf_hi(vz[e]) + qq[2 * e + 1] * bf_hi(vx[e]) + rr[2 * e + 1];
+      if (extra) { lo += bf_lo(ve[e]); hi += bf_hi(ve[e]); }
+      if (acc) { lo += bf_lo(old[e]); hi += bf_hi(old[e]); }
+      o[e] = pack2(lo, hi);
+    }
+    *(u32x4*)dst = o;
+  }
+}
+
+inline int grid_for(long long work, int per_block = 256, int cap = 8192) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int fmd_channel_stats(const void* x, const void* y0, const void* y1, int32_t C0, int32_t N, int32_t HW,
+                                  int32_t C, int32_t rows, float* out, fmd_stream_t stream) {
+  if (C % 8 || HW % rows) return -1;
+  dim3 grid(N * (HW / rows), (C + 63) / 64);
+  hipLaunchKernelGGL(channel_stats_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16r*)x,
+                     (const bf16r*)y0, (const bf16r*)y1, C0, N, HW, C, rows, out);
+  return (int)hipGetLastError();
+}
+
+
+extern "C" int fmd_gn_prep(const float* st0, int32_t rows0, const float* st1, int32_t rows1, int32_t N, int32_t HW,
+                           int32_t C0, int32_t C1, int32_t G, float eps, const float* gamma, const float* beta,
+                           const float* emb, int32_t emb_stride, int32_t emb_mode, float* a, float* b,
+                           float* mean_rstd, fmd_stream_t s) {
+  if ((C0 + C1) % G || HW % rows0 || (C1 && HW % rows1)) return -1;
+  hipLaunchKernelGGL(gn_prep_kernel, dim3(N * G), dim3(256), 0, (hipStream_t)s, st0, rows0, st1, rows1, N, HW, C0,
+                     C1, G, eps, gamma, beta, emb, emb_stride, emb_mode, a, b, mean_rstd);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_t HW, int32_t C, int32_t G,
+                               const float* mean_rstd, const float* gamma, const float* beta, const float* emb,
+                               int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R, float* dgamma,
+                               float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st, int32_t fwd_rows,
+                               fmd_stream_t s) {
+  if (C % G || HW % rows || C / G > 1024) return -1;
+  if (emb_mode == 2 && (!fwd_st || HW % fwd_rows)) return -2;
+  hipLaunchKernelGGL(gn_bwd_prep_kernel, dim3(G), dim3(256), 0, (hipStream_t)s, s12, rows, N, HW, C, G, mean_rstd,
+                     gamma, beta, emb, emb_stride, emb_mode, P, Q, R, dgamma, dbeta, demb, demb_stride, fwd_st,
+                     fwd_rows);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,
+                                int32_t HW, const float* P, const float* Q, const float* R, const void* extra,
+                                void* dx0, int32_t acc0, void* dx1, int32_t acc1, fmd_stream_t s) {
+  if ((C0 % 8) || (C1 % 8)) return -1;
+  const long long work = M * (long long)((C0 + C1) / 8);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)s, (const bf16r*)dz,
+                     (const bf16r*)x0, (const bf16r*)x1, C0, C1, (long long)M, HW, P, Q, R, (const bf16r*)extra,
+                     (bf16r*)dx0, acc0, (bf16r*)dx1, acc1);
+  return (int)hipGetLastError();
+}

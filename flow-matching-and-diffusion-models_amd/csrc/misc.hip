@@ -1,0 +1,506 @@
+// Small wavefront kernels around the UNet hot path (gfx950): weight layout
+// preparation, NCHW<->NHWC staging, sinusoidal timestep features and the
+// time-embedding / ResBlock emb_layers linears, the FM / DDPM train-step
+// input preparation and MSE loss, the FlowMatchEuler / DDPM / DDIM step
+// updates, and a flat fused AdamW.
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+inline int grid_for(long long work, int per_block = 256, int cap = 16384) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+#define GRID_STRIDE(i, total) \
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (total); i += (long long)gridDim.x * blockDim.x)
+
+// mode 0: forward  out[k][tap][c] (rows k >= K and channels c >= C zero; Kpad x T x Cpad)
+// mode 1: data-grad out[c][tap][k] (Cpad rows, Kpad inner)
+// mode 2: data-grad of nearest-x2 upsample + 3x3 conv: 4x4 effective taps, out[c][16][k]
+__global__ void prep_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode, int Kpad, int Cpad,
+                                    bf16r* __restrict__ out) {
+  const int T = ks * ks;
+  if (mode == 0) {
+    const long long total = (long long)Kpad * T * Cpad;
+    GRID_STRIDE(i, total) {
+      const int c = (int)(i % Cpad);
+      const long long r = i / Cpad;
+      const int tap = (int)(r % T);
+      const int k = (int)(r / T);
+      float v = (k < K && c < C) ? w[((size_t)k * C + c) * T + tap] : 0.f;
+      out[i] = (bf16r)f2bf(v);
+    }
+  } else if (mode == 1) {
+    const long long total = (long long)Cpad * T * Kpad;
+    GRID_STRIDE(i, total) {
+      const int k = (int)(i % Kpad);
+      const long long r = i / Kpad;
+      const int tap = (int)(r % T);
+      const int c = (int)(r / T);
+      float v = (k < K && c < C) ? w[((size_t)k * C + c) * T + tap] : 0.f;
+      out[i] = (bf16r)f2bf(v);
+    }
+  } else {
+    // 1-D effective taps over dY rows 2i-1 .. 2i+2:  r0: W2, r1: W1+W2, r2: W0+W1, r3: W0
+    const long long total = (long long)Cpad * 16 * Kpad;
+    GRID_STRIDE(i, total) {
+      const int k = (int)(i % Kpad);
+      const long long r = i / Kpad;
+      const int tap = (int)(r % 16);
+      const int c = (int)(r / 16);
+      const int ry = tap >> 2, rx = tap & 3;
+      float v = 0.f;
+      if (k < K && c < C) {
+        const int ylo = (ry == 0) ? 2 : (ry == 1 ? 1 : 0), yhi = (ry == 3) ? 0 : (ry == 2 ? 1 : 2);
+        const int xlo = (rx == 0) ? 2 : (rx == 1 ? 1 : 0), xhi = (rx == 3) ? 0 : (rx == 2 ? 1 : 2);
+        for (int ky = ylo; ky <= yhi; ++ky)
+          for (int kx = xlo; kx <= xhi; ++kx) v += w[((size_t)k * C + c) * 9 + ky * 3 + kx];
+      }
+      out[i] = (bf16r)f2bf(v);
+    }
+  }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW, int Cpad, bf16r* __restrict__ y) {
+  const long long total = (long long)N * HW * Cpad;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % Cpad);
+    const long long p = i / Cpad;
+    const int n = (int)(p / HW), hw = (int)(p % HW);
+    y[i] = (bf16r)f2bf(c < C ? x[((size_t)n * C + c) * HW + hw] : 0.f);
+  }
+}
+
+__global__ void nhwc_to_nchw_kernel(const void* __restrict__ y, int src_f32, int N, int C, int HW, int Cs,
+                                    float* __restrict__ x) {
+  const long long total = (long long)N * C * HW;
+  GRID_STRIDE(i, total) {
+    const int hw = (int)(i % HW);
+    const long long r = i / HW;
+    const int c = (int)(r % C), n = (int)(r / C);
+    const size_t src = ((size_t)n * HW + hw) * Cs + c;
+    x[i] = src_f32 ? ((const float*)y)[src] : bf2f(((const bf16r*)y)[src]);
+  }
+}
+
+// timestep_embedding (src/nn/ops/time_embedding.py:4-32), fp32 like the reference
+// t_scale / t_trunc: the FM trainer's integer timesteps (t * (N-1)).long() (flow_matching_lib.py:153)
+__global__ void temb_kernel(const float* __restrict__ t, int N, int dim, int flip, int shift, float neg_log_period,
+                            float t_scale, int t_trunc, float* __restrict__ out) {
+  const int half = dim / 2;
+  const long long total = (long long)N * dim;
+  GRID_STRIDE(i, total) {
+    const int j = (int)(i % dim), n = (int)(i / dim);
+    float v = 0.f;
+    if (j < 2 * half) {
+      int jj = j;
+      if (flip) jj = (j < half) ? j + half : j - half;   // [cos, sin]
+      const int f = jj < half ? jj : jj - half;
+      const float e = (neg_log_period * (float)f) / (float)max(half - shift, 1);
+      float tv = t[n] * t_scale;
+      if (t_trunc) tv = (float)(long long)tv;
+      const float arg = tv * expf(e);
+      v = jj < half ? sinf(arg) : cosf(arg);
+    }
+    out[i] = v;
+  }
+}
+
+// y[b][o] = sum_i f(x[b][i]) w[o][i] + bias[o]; one wave per output row, B <= 32
+__global__ void linear_kernel(const float* __restrict__ x, int B, int I, const float* __restrict__ w,
+                              const float* __restrict__ bias, int O, int in_silu, float* __restrict__ y, int ys) {
+  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wid >= O) return;
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+  for (int i = lane; i < I; i += 64) {
+    const float wv = w[(size_t)wid * I + i];
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      if (b < B) {
+        float xv = x[(size_t)b * I + i];
+        if (in_silu) xv = siluf_(xv);
+        acc[b] += wv * xv;
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 32; ++b) {
+    if (b < B) {
+      const float s = wave_sum(acc[b]);
+      if (lane == 0) y[(size_t)b * ys + wid] = s + (bias ? bias[wid] : 0.f);
+    }
+  }
+}
+
+// dw[o][i] += sum_b dy[b][o] f(x[b][i]);  db[o] += sum_b dy[b][o]
+__global__ void linear_dw_kernel(const float* __restrict__ x, int B, int I, int O, int in_silu,
+                                 const float* __restrict__ dy, int dys, float* __restrict__ dw,
+                                 float* __restrict__ db) {
+  const long long total = (long long)O * I;
+  GRID_STRIDE(idx, total) {
+    const int i = (int)(idx % I), o = (int)(idx / I);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      float xv = x[(size_t)b * I + i];
+      if (in_silu) xv = siluf_(xv);
+      s += dy[(size_t)b * dys + o] * xv;
+    }
+    dw[idx] += s;
+    if (db && i == 0) {
+      float t = 0.f;
+      for (int b = 0; b < B; ++b) t += dy[(size_t)b * dys + o];
+      db[o] += t;
+    }
+  }
+}
+
+// dx[b][i] (+)= f'(x) * sum_o dy[b][o] w[o][i]
+__global__ void linear_dx_kernel(const float* __restrict__ x, int B, int I, const float* __restrict__ w, int O,
+                                 int in_silu, const float* __restrict__ dy, int dys, float* __restrict__ dx, int acc) {
+  const long long total = (long long)B * I;
+  GRID_STRIDE(idx, total) {
+    const int i = (int)(idx % I), b = (int)(idx / I);
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s += dy[(size_t)b * dys + o] * w[(size_t)o * I + i];
+    if (in_silu) s *= silu_grad(x[idx]);
+    dx[idx] = acc ? dx[idx] + s : s;
+  }
+}
+
+__global__ void silu_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dx,
+                                long long n) {
+  GRID_STRIDE(i, n) dx[i] = dy[i] * silu_grad(x[i]);
+}
+
+// model input: ch [0,Cx) = ca[n]*x0 + cb[n]*noise (or noise if ca == NULL), [Cx,Cx+Cc) = cond, rest 0
+__global__ void noise_prepare_kernel(const float* __restrict__ x0, const float* __restrict__ noise,
+                                     const float* __restrict__ ca, const float* __restrict__ cb,
+                                     const float* __restrict__ cond, int N, int HW, int Cx, int Cc, int Cpad,
+                                     bf16r* __restrict__ inp) {
+  const long long total = (long long)N * HW * Cpad;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % Cpad);
+    const long long p = i / Cpad;
+    const int n = (int)(p / HW), hw = (int)(p % HW);
+    float v = 0.f;
+    if (c < Cx) {
+      const size_t s = ((size_t)n * Cx + c) * HW + hw;
+      v = ca ? (cb ? ca[n] * x0[s] + cb[n] * noise[s] : (1.0f - ca[n]) * x0[s] + ca[n] * noise[s]) : noise[s];
+    } else if (c < Cx + Cc) {
+      v = cond[((size_t)n * Cc + (c - Cx)) * HW + hw];
+    }
+    inp[i] = (bf16r)f2bf(v);
+  }
+}
+
+// partial sums of (pred - target)^2; dpred = scale * 2 (pred - target) / numel (bf16, NHWC, Kpad channels)
+__global__ void mse_kernel(const float* __restrict__ pred, int Kpad, const float* __restrict__ ta,
+                           const float* __restrict__ tb, float tb_sign, int N, int Cx, int HW, float inv_numel,
+                           float grad_scale, float* __restrict__ partial, bf16r* __restrict__ dpred) {
+  const long long total = (long long)N * HW * Kpad;
+  float s = 0.f;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % Kpad);
+    const long long p = i / Kpad;
+    float g = 0.f;
+    if (c < Cx) {
+      const int n = (int)(p / HW), hw = (int)(p % HW);
+      const size_t ti = ((size_t)n * Cx + c) * HW + hw;
+      float target = ta[ti];
+      if (tb) target = target + tb_sign * tb[ti];
+      const float dlt = pred[i] - target;
+      s += dlt * dlt;
+      g = grad_scale * 2.f * dlt * inv_numel;
+    }
+    if (dpred) dpred[i] = (bf16r)f2bf(g);
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void sum_partials_kernel(const float* __restrict__ partial, int n, float scale, float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(red[0] * scale);
+}
+
+// torch.optim.AdamW (foreach=False arithmetic), flat fp32 buffers
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long long n, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2_sqrt) {
+  GRID_STRIDE(i, n) {
+    float pv = p[i];
+    const float gv = g[i];
+    pv = pv * (1.f - lr * wd);
+    float mv = m[i];
+    mv = mv + (gv - mv) * (1.f - b1);
+    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
+    m[i] = mv;
+    v[i] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pv = pv - (lr / bc1) * (mv / denom);
+    p[i] = pv;
+  }
+}
+
+// Same update with the step count read from device memory and the LR of
+// get_cosine_schedule_with_warmup (flow_matching_lib.py:76-79) computed on device,
+// so a captured train-step graph replays with the right schedule.
+__global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                   float* __restrict__ v, long long n, const int* __restrict__ step_ctr,
+                                   float base_lr, int warmup, int total, float b1, float b2, float eps, float wd,
+                                   float grad_scale) {
+  const int step = step_ctr[0] + 1;          // optimizer.step() count, 1-based
+  const int s = step - 1;                    // lr_scheduler.step() calls so far
+  double lam;
+  if (s < warmup) {
+    lam = (double)s / (double)(warmup > 1 ? warmup : 1);
+  } else {
+    const double prog = (double)(s - warmup) / (double)((total - warmup) > 1 ? (total - warmup) : 1);
+    lam = 0.5 * (1.0 + cos(3.14159265358979323846 * 2.0 * 0.5 * prog));
+    if (lam < 0) lam = 0;
+  }
+  const float lr = (float)(base_lr * lam);
+  const float bc1 = (float)(1.0 - pow((double)b1, step));
+  const float bc2s = sqrtf((float)(1.0 - pow((double)b2, step)));
+  GRID_STRIDE(i, n) {
+    float pv = p[i];
+    const float gv = g[i] * grad_scale;
+    pv = pv * (1.f - lr * wd);
+    float mv = m[i];
+    mv = mv + (gv - mv) * (1.f - b1);
+    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
+    m[i] = mv;
+    v[i] = vv;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pv = pv - (lr / bc1) * (mv / denom);
+    p[i] = pv;
+  }
+}
+
+// FlowMatchEuler: x += (sigma[i+1] - sigma[i]) * v   (fp32), then write the next model input
+__global__ void flow_euler_kernel(float* __restrict__ x, const float* __restrict__ vout, int Kpad,
+                                  const float* __restrict__ sigmas, const int* __restrict__ index, int N, int Cx,
+                                  int HW, const float* __restrict__ cond, int Cc, int Cpad, bf16r* __restrict__ next) {
+  const int idx = index[0];
+  const float ds = sigmas[idx + 1] - sigmas[idx];
+  const long long total = (long long)N * HW;
+  GRID_STRIDE(p, total) {
+    const int n = (int)(p / HW), hw = (int)(p % HW);
+    for (int c = 0; c < Cx; ++c) {
+      const size_t xi = ((size_t)n * Cx + c) * HW + hw;
+      const float nv = x[xi] + ds * vout[p * Kpad + c];
+      x[xi] = nv;
+      if (next) next[p * Cpad + c] = (bf16r)f2bf(nv);
+    }
+    if (next) {
+      for (int c = 0; c < Cc; ++c) next[p * Cpad + Cx + c] = (bf16r)f2bf(cond[((size_t)n * Cc + c) * HW + hw]);
+      for (int c = Cx + Cc; c < Cpad; ++c) next[p * Cpad + c] = 0;
+    }
+  }
+}
+
+// DDPM / DDIM (eps-prediction): coef table row idx = [sqrt_b, sqrt_a, c_x0, c_xt, std, clip, c_eps]
+//   x0 = clip((x - sqrt_b*eps)/sqrt_a);  prev = c_x0*x0 + c_xt*x + c_eps*eps + std*z
+__global__ void ddpm_step_kernel(float* __restrict__ x, const float* __restrict__ eps, int Kpad,
+                                 const float* __restrict__ coef, const int* __restrict__ index,
+                                 const float* __restrict__ noise, int N, int Cx, int HW, const float* __restrict__ cond,
+                                 int Cc, int Cpad, bf16r* __restrict__ next) {
+  const int idx = index[0];
+  const float* cf = coef + idx * 7;
+  const float sqrt_b = cf[0], sqrt_a = cf[1], cx0 = cf[2], cxt = cf[3], sd = cf[4], clip = cf[5], ceps = cf[6];
+  const long long total = (long long)N * HW;
+  GRID_STRIDE(p, total) {
+    const int n = (int)(p / HW), hw = (int)(p % HW);
+    for (int c = 0; c < Cx; ++c) {
+      const size_t xi = ((size_t)n * Cx + c) * HW + hw;
+      const float e = eps[p * Kpad + c];
+      const float xv = x[xi];
+      float x0 = (xv - sqrt_b * e) / sqrt_a;
+      if (clip > 0.f) x0 = fminf(fmaxf(x0, -clip), clip);
+      float pv = cx0 * x0 + cxt * xv;
+      if (ceps != 0.f) pv = pv + ceps * e;
+      if (noise && sd > 0.f) pv = pv + sd * noise[(size_t)idx * N * Cx * HW + xi];
+      x[xi] = pv;
+      if (next) next[p * Cpad + c] = (bf16r)f2bf(pv);
+    }
+    if (next) {
+      for (int c = 0; c < Cc; ++c) next[p * Cpad + Cx + c] = (bf16r)f2bf(cond[((size_t)n * Cc + c) * HW + hw]);
+      for (int c = Cx + Cc; c < Cpad; ++c) next[p * Cpad + c] = 0;
+    }
+  }
+}
+
+__global__ void fill_from_table_kernel(const float* __restrict__ table, const int* __restrict__ index, float* out,
+                                       int N) {
+  const int i = threadIdx.x;
+  if (i < N) out[i] = table[index[0]];
+}
+
+__global__ void counter_add_kernel(int* c, int v) {
+  if (threadIdx.x == 0) c[0] += v;
+}
+
+__global__ void sum_pool2_kernel(const bf16r* __restrict__ src, int N, int H, int W, int C, bf16r* __restrict__ dst,
+                                 int acc) {
+  // dst[n][y][x][c] (+)= sum of the 2x2 block of src[n][2y..][2x..][c]   (dst is H x W, src 2H x 2W)
+  const long long total = (long long)N * H * W * C;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int x = (int)(r % W); r /= W;
+    const int y = (int)(r % H);
+    const int n = (int)(r / H);
+    float s = 0.f;
+    for (int dy = 0; dy < 2; ++dy)
+      for (int dx = 0; dx < 2; ++dx) s += bf2f(src[(((size_t)n * 2 * H + 2 * y + dy) * 2 * W + 2 * x + dx) * C + c]);
+    if (acc) s += bf2f(dst[i]);
+    dst[i] = (bf16r)f2bf(s);
+  }
+}
+
+__global__ void add_bf16_kernel(const bf16r* __restrict__ a, bf16r* __restrict__ dst, long long n) {
+  GRID_STRIDE(i, n) dst[i] = (bf16r)f2bf(bf2f(dst[i]) + bf2f(a[i]));
+}
+
+}  // namespace
+
+#define LAUNCH(kernel, grid, ...)                                                   \
+  do {                                                                              \
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(256), 0, (hipStream_t)s, __VA_ARGS__); \
+    return (int)hipGetLastError();                                                  \
+  } while (0)
+
+extern "C" {
+
+int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t Kpad, int32_t Cpad,
+                      void* out, fmd_stream_t s) {
+  const long long total = (long long)Kpad * Cpad * (mode == 2 ? 16 : ks * ks);
+  LAUNCH(prep_weights_kernel, grid_for(total), w, K, C, ks, mode, Kpad, Cpad, (bf16r*)out);
+}
+
+
+int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s) {
+  LAUNCH(nchw_to_nhwc_kernel, grid_for((long long)N * HW * Cpad), x, N, C, HW, Cpad, (bf16r*)y);
+}
+
+int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
+                      fmd_stream_t s) {
+  LAUNCH(nhwc_to_nchw_kernel, grid_for((long long)N * HW * C), y, src_f32, N, C, HW, Cs, x);
+}
+
+
+int fmd_timestep_embedding(const float* t, int32_t N, int32_t dim, int32_t flip, int32_t shift, float max_period,
+                           float t_scale, int32_t t_trunc, float* out, fmd_stream_t s) {
+  const float nlp = -(float)log((double)max_period);
+  LAUNCH(temb_kernel, grid_for((long long)N * dim), t, N, dim, flip, shift, nlp, t_scale, t_trunc, out);
+}
+
+int fmd_linear(const float* x, int32_t B, int32_t I, const float* w, const float* b, int32_t O, int32_t in_silu,
+               float* y, int32_t y_stride, fmd_stream_t s) {
+  if (B > 32) return -1;
+  LAUNCH(linear_kernel, (O + 3) / 4, x, B, I, w, b, O, in_silu, y, y_stride);
+}
+
+int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t O, int32_t in_silu,
+                   const float* dy, int32_t dy_stride, float* dx, int32_t dx_acc, float* dw, float* db,
+                   fmd_stream_t s) {
+  if (dw) {
+    hipLaunchKernelGGL(linear_dw_kernel, dim3(grid_for((long long)O * I)), dim3(256), 0, (hipStream_t)s, x, B, I, O,
+                       in_silu, dy, dy_stride, dw, db);
+    int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  if (dx) {
+    hipLaunchKernelGGL(linear_dx_kernel, dim3(grid_for((long long)B * I)), dim3(256), 0, (hipStream_t)s, x, B, I, w,
+                       O, in_silu, dy, dy_stride, dx, dx_acc);
+    return (int)hipGetLastError();
+  }
+  return 0;
+}
+
+int fmd_silu_bwd_f32(const float* x, const float* dy, float* dx, int64_t n, fmd_stream_t s) {
+  LAUNCH(silu_bwd_kernel, grid_for(n), x, dy, dx, (long long)n);
+}
+
+int fmd_noise_prepare(const float* x0, const float* noise, const float* ca, const float* cb, const float* cond,
+                      int32_t N, int32_t HW, int32_t Cx, int32_t Cc, int32_t Cpad, void* inp, fmd_stream_t s) {
+  LAUNCH(noise_prepare_kernel, grid_for((long long)N * HW * Cpad), x0, noise, ca, cb, cond, N, HW, Cx, Cc, Cpad,
+         (bf16r*)inp);
+}
+
+int fmd_mse(const float* pred, int32_t Kpad, const float* ta, const float* tb, float tb_sign, int32_t N, int32_t Cx,
+            int32_t HW, float grad_scale, float* partial, int32_t max_blocks, float* loss, void* dpred,
+            fmd_stream_t s) {
+  const long long total = (long long)N * HW * Kpad;
+  int blocks = grid_for(total, 256, max_blocks);
+  const float inv = 1.f / (float)((long long)N * Cx * HW);
+  hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)s, pred, Kpad, ta, tb, tb_sign, N, Cx, HW,
+                     inv, grad_scale, partial, (bf16r*)dpred);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, partial, blocks, inv, loss);
+  return (int)hipGetLastError();
+}
+
+int fmd_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+              float wd, float bc1, float bc2, fmd_stream_t s) {
+  LAUNCH(adamw_kernel, grid_for(n, 256, 8192), p, g, m, v, (long long)n, lr, beta1, beta2, eps, wd, bc1, sqrtf(bc2));
+}
+
+int fmd_adamw_sched(float* p, const float* g, float* m, float* v, int64_t n, const int32_t* step_ctr, float base_lr,
+                    int32_t warmup, int32_t total, float beta1, float beta2, float eps, float wd, float grad_scale,
+                    fmd_stream_t s) {
+  LAUNCH(adamw_sched_kernel, grid_for(n, 256, 8192), p, g, m, v, (long long)n, step_ctr, base_lr, warmup, total,
+         beta1, beta2, eps, wd, grad_scale);
+}
+
+int fmd_flow_euler(float* x, const float* v, int32_t Kpad, const float* sigmas, const int32_t* index, int32_t N,
+                   int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad, void* next, fmd_stream_t s) {
+  LAUNCH(flow_euler_kernel, grid_for((long long)N * HW), x, v, Kpad, sigmas, index, N, Cx, HW, cond, Cc, Cpad,
+         (bf16r*)next);
+}
+
+int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, const int32_t* index,
+                  const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
+                  void* next, fmd_stream_t s) {
+  LAUNCH(ddpm_step_kernel, grid_for((long long)N * HW), x, eps, Kpad, coef, index, noise, N, Cx, HW, cond, Cc, Cpad,
+         (bf16r*)next);
+}
+
+int fmd_fill_from_table(const float* table, const int32_t* index, float* out, int32_t N, fmd_stream_t s) {
+  if (N > 256) return -1;
+  LAUNCH(fill_from_table_kernel, 1, table, index, out, N);
+}
+
+int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s) { LAUNCH(counter_add_kernel, 1, c, v); }
+
+int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc,
+                  fmd_stream_t s) {
+  LAUNCH(sum_pool2_kernel, grid_for((long long)N * H * W * C), (const bf16r*)src, N, H, W, C, (bf16r*)dst, acc);
+}
+
+int fmd_add_bf16(const void* a, void* dst, int64_t n, fmd_stream_t s) {
+  LAUNCH(add_bf16_kernel, grid_for(n), (const bf16r*)a, (bf16r*)dst, (long long)n);
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+"""ctypes binding of the C ABI in ``include/fmdiff.h`` (libfmdiff_hip.so).
+
+There is deliberately no fallback: if the library is missing the import of
+any GPU op raises, so a GPU run can never silently use another path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libfmdiff_hip.so")
+
+p = C.c_void_p
+i32 = C.c_int32
+i64 = C.c_int64
+f32 = C.c_float
+
+
+class ConvDesc(C.Structure):
+    """Mirror of ``fmd_conv_desc``."""
+    _fields_ = [
+        ("N", i32), ("Hs", i32), ("Ws", i32), ("C0", i32), ("C1", i32), ("Ho", i32), ("Wo", i32), ("K", i32),
+        ("ks", i32), ("stride", i32), ("pad", i32), ("upsample", i32), ("transposed", i32),
+        ("src0", p), ("src1", p), ("pro_a", p), ("pro_b", p), ("pro_silu", i32), ("wgt", p),
+        ("src2", p), ("src3", p), ("C2", i32), ("C3", i32), ("wgt2", p),
+        ("bias", p), ("bias2", p), ("bias_nc", p), ("resid", p), ("out", p), ("out_f32", i32), ("accumulate", i32),
+        ("stats", p), ("ep_x0", p), ("ep_x1", p), ("ep_C0", i32), ("ep_a", p), ("ep_b", p),
+        ("ws", p), ("splits", i32),
+    ]
+
+
+class WgradDesc(C.Structure):
+    """Mirror of ``fmd_wgrad_desc``."""
+    _fields_ = [
+        ("N", i32), ("Hs", i32), ("Ws", i32), ("C0", i32), ("C1", i32), ("Ho", i32), ("Wo", i32), ("K", i32),
+        ("ks", i32), ("stride", i32), ("pad", i32), ("upsample", i32),
+        ("src0", p), ("src1", p), ("pro_a", p), ("pro_b", p), ("pro_silu", i32), ("dy", p), ("ldy", i32), ("dw", p), ("db", p),
+        ("accumulate", i32), ("ws", p), ("splits", i32),
+    ]
+
+
+# name -> argtypes (restype is int32 unless listed in _RESTYPE)
+SIGNATURES = {
+    "fmd_conv": [C.POINTER(ConvDesc), p],
+    "fmd_wgrad": [C.POINTER(WgradDesc), p],
+    "fmd_wgrad_workspace": [C.POINTER(WgradDesc)],
+    "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
+    "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p],
+    "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
+    "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
+    "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
+    "fmd_nhwc_to_nchw": [p, i32, i32, i32, i32, i32, p, p],
+    "fmd_sum_pool2": [p, i32, i32, i32, i32, p, i32, p],
+    "fmd_add_bf16": [p, p, i64, p],
+    "fmd_timestep_embedding": [p, i32, i32, i32, i32, f32, f32, i32, p, p],
+    "fmd_adamw_sched": [p, p, p, p, i64, p, f32, i32, i32, f32, f32, f32, f32, f32, p],
+    "fmd_linear": [p, i32, i32, p, p, i32, i32, p, i32, p],
+    "fmd_linear_bwd": [p, i32, i32, p, i32, i32, p, i32, p, i32, p, p, p],
+    "fmd_silu_bwd_f32": [p, p, p, i64, p],
+    "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
+    "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_noise_prepare": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_mse": [p, i32, p, p, f32, i32, i32, i32, f32, p, i32, p, p, p],
+    "fmd_adamw": [p, p, p, p, i64, f32, f32, f32, f32, f32, f32, f32, p],
+    "fmd_flow_euler": [p, p, i32, p, p, i32, i32, i32, p, i32, i32, p, p],
+    "fmd_ddpm_step": [p, p, i32, p, p, p, i32, i32, i32, p, i32, i32, p, p],
+    "fmd_fill_from_table": [p, p, p, i32, p],
+    "fmd_counter_add": [p, i32, p],
+}
+_RESTYPE = {"fmd_wgrad_workspace": i64}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library; raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"fmdiff HIP library not found at {LIB_PATH}; run __graft_entry__.build() "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, i32)
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)

@@ -1,0 +1,23 @@
+"""``ConvND`` envelope (reference ``src/nn/ops/convolution.py:8-54``); the parameter lives under ``.conv``."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch.nn as nn
+
+from ..params import Conv, SizeArg
+
+
+class ConvND(nn.Module):
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, kernel_size: SizeArg = 3,
+                 stride: SizeArg = 1, padding: Optional[SizeArg] = None, dilation: SizeArg = 1, groups: int = 1,
+                 bias: bool = True):
+        super().__init__()
+        if spatial_dims not in (1, 2, 3):
+            raise ValueError("spatial_dims must be 1, 2 or 3")
+        if padding is None:
+            padding = kernel_size // 2 if isinstance(kernel_size, int) else tuple(k // 2 for k in kernel_size)
+        self.conv = Conv(spatial_dims, in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias)
+
+    def forward(self, x):
+        return self.conv(x)

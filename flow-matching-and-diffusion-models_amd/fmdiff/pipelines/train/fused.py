@@ -1,0 +1,204 @@
+"""Device-resident FM / DDPM train step and FM-Euler sampler over the fused HIP engine.
+
+One train step is the body of ``src/pipelines/train/flow_matching_lib.py:150-182``
+(FM) or ``src/pipelines/train/diffusion_lib.py:153-185`` (DDPM) for one batch:
+
+    noise ~ N(0,1), t ~ U[0,1) (FM) | timesteps ~ randint (DDPM)
+    model input = cat([x_t, ldct]),  pred = UNet(input, timesteps)
+    loss = mse(pred, noise - x0) (FM) | mse(pred, noise) (DDPM), backward
+    [data-parallel: gradient all-reduce (mean) over RCCL]   <- added: the reference has none
+    AdamW + cosine-with-warmup LR
+
+Every stage is a HIP kernel on the current stream, nothing synchronises with
+the host, so the whole step can be captured once into a hipGraph
+(``torch.cuda.graph``) and replayed.  The LR schedule and Adam step count live
+in device memory for that reason.  Parameters, gradients and Adam moments are
+single flat fp32 buffers (the model's Parameters become views into them), so
+the optimizer is one launch and the gradient all-reduce is over contiguous
+buckets.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ...runtime import ops
+from ...runtime.engine import get_engine
+
+
+class FlatParams:
+    """Re-point every parameter (and its .grad) into one flat fp32 buffer."""
+
+    def __init__(self, model: torch.nn.Module):
+        params = [p for p in model.parameters()]
+        dev = params[0].device
+        total = sum(p.numel() for p in params)
+        self.data = torch.empty(total, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.slices = []
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                self.data[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.data[off:off + n].view_as(p)
+                p.grad = self.grad[off:off + n].view_as(p)
+                self.slices.append((off, n))
+                off += n
+        self.numel = total
+
+
+class FusedTrainStep:
+    def __init__(self, model, *, objective: str = "flow_matching", lr: float = 1e-4, weight_decay: float = 0.0,
+                 warmup: int = 500, total_steps: int = 10 ** 9, num_train_timesteps: int = 1000,
+                 grad_accum: int = 1, betas=(0.9, 0.999), eps: float = 1e-8, ddpm_scheduler=None,
+                 process_group=None, allreduce_buckets: int = 4):
+        self.model = model
+        self.eng = get_engine(model)
+        self.flat = FlatParams(model)
+        dev = self.flat.data.device
+        self.m = torch.zeros_like(self.flat.data)
+        self.v = torch.zeros_like(self.flat.data)
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.partial = torch.empty(4096, dtype=torch.float32, device=dev)
+        self.objective = objective
+        self.hp = dict(lr=lr, wd=weight_decay, warmup=warmup, total=total_steps, betas=betas, eps=eps)
+        self.N_train = num_train_timesteps
+        self.grad_accum = max(1, int(grad_accum))
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.buckets = allreduce_buckets
+        if objective == "ddpm":
+            if ddpm_scheduler is None:
+                raise ValueError("ddpm objective needs its DDPMScheduler (alphas_cumprod)")
+            self.acp = ddpm_scheduler.alphas_cumprod.to(dev, torch.float32)
+        self._graph = None
+        self._static = None
+
+    # ---------------------------------------------------------------- body
+    def _chunk(self, clean, ldct, noise, t_or_ts):
+        N, Cx = clean.shape[:2]
+        Cc = ldct.shape[1] if ldct is not None else 0
+        Cp = max(8, -(-(Cx + Cc) // 8) * 8)
+        if self.objective == "flow_matching":
+            inp = ops.noise_prepare(clean, noise, t_or_ts, None, ldct, Cp)        # (1-t) x0 + t eps
+            out, ctx = self.eng.forward(inp, t_or_ts, save=True, t_scale=float(self.N_train - 1), t_trunc=True)
+            ta, tb, sign = noise, clean, -1.0                                      # target eps - x0
+        else:
+            sel = self.acp[t_or_ts]
+            ca, cb = sel.sqrt(), (1 - sel).sqrt()
+            inp = ops.noise_prepare(clean, noise, ca, cb, ldct, Cp)               # add_noise
+            out, ctx = self.eng.forward(inp, t_or_ts, save=True)
+            ta, tb, sign = noise, None, 0.0                                        # target eps
+        dpred = torch.empty(out.shape, device=out.device, dtype=torch.bfloat16)
+        ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
+        self.eng.backward(ctx, dpred)
+        return self.loss
+
+    def _allreduce(self):
+        if self.world <= 1:
+            return
+        g = self.flat.grad
+        n = g.numel()
+        per = -(-n // self.buckets)
+        for i in range(self.buckets):
+            sl = g[i * per:min(n, (i + 1) * per)]
+            if sl.numel():
+                dist.all_reduce(sl, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def step(self, clean, ldct, noise=None, t=None):
+        """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss."""
+        self.eng.invalidate_weights()            # bf16 kernel weights re-derived from the updated masters
+        self.flat.grad.zero_()
+        N = clean.shape[0]
+        chunk = -(-N // self.grad_accum)
+        loss = None
+        for c0 in range(0, N, chunk):
+            cl = clean[c0:c0 + chunk]
+            ld = ldct[c0:c0 + chunk] if ldct is not None else None
+            nz = noise[c0:c0 + chunk] if noise is not None else torch.randn_like(cl)
+            if self.objective == "flow_matching":
+                tt = t[c0:c0 + chunk] if t is not None else torch.rand(cl.shape[0], device=cl.device)
+            else:
+                tt = t[c0:c0 + chunk] if t is not None else torch.randint(0, self.N_train, (cl.shape[0],),
+                                                                           device=cl.device)
+            loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt)
+        self._allreduce()
+        b1, b2 = self.hp["betas"]
+        ops.adamw_sched(self.flat.data, self.flat.grad, self.m, self.v, self.step_ctr, self.hp["lr"], self.hp["warmup"],
+                        self.hp["total"], b1, b2, self.hp["eps"], self.hp["wd"], 1.0 / self.world)
+        ops.counter_add(self.step_ctr)
+        return loss
+
+    # ---------------------------------------------------------- hipGraph
+    def capture(self, clean, ldct, warmup_iters: int = 2):
+        """Capture one full step (RNG, forward, loss, backward, [all-reduce], AdamW) into a hipGraph."""
+        self._static = (clean.clone(), ldct.clone() if ldct is not None else None)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup_iters):
+                self.step(*self._static)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_loss = self.step(*self._static)
+        self._graph = g
+
+    def replay(self, clean=None, ldct=None):
+        if clean is not None:
+            self._static[0].copy_(clean)
+        if ldct is not None:
+            self._static[1].copy_(ldct)
+        self._graph.replay()
+        return self._graph_loss
+
+
+class FusedFlowSampler:
+    """FlowMatchEuler sampling loop (``src/pipelines/utils.py:163-220``) with one replayable step."""
+
+    def __init__(self, model, num_inference_steps: int = 50, num_train_timesteps: int = 1000):
+        from ..schedulers import FlowMatchEulerDiscreteScheduler
+        self.eng = get_engine(model)
+        self.sched = FlowMatchEulerDiscreteScheduler(num_train_timesteps)
+        self.sched.set_timesteps(num_inference_steps)
+        self.S = num_inference_steps
+        self._graph = None
+
+    def _prepare(self, init, cond):
+        dev = init.device
+        self.ts = self.sched.timesteps.to(dev)
+        self.sig = self.sched.sigmas.to(dev)
+        self.idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.x = init.float().clone()
+        self.cond = cond.float().contiguous() if cond is not None else None
+        Cx = init.shape[1]
+        Cc = cond.shape[1] if cond is not None else 0
+        self.inp = ops.noise_prepare(None, self.x, None, None, self.cond, max(8, -(-(Cx + Cc) // 8) * 8))
+        self.tbuf = torch.empty(init.shape[0], device=dev, dtype=torch.float32)
+
+    def _one(self):
+        ops.fill_from_table(self.ts, self.idx, self.tbuf)
+        out, _ = self.eng.forward(self.inp, self.tbuf, save=False)
+        ops.flow_euler(self.x, out, self.sig, self.idx, self.cond, self.inp)
+        ops.counter_add(self.idx)
+
+    @torch.no_grad()
+    def sample(self, init: torch.Tensor, cond: Optional[torch.Tensor] = None, use_graph: bool = True):
+        self._prepare(init, cond)
+        if not use_graph:
+            for _ in range(self.S):
+                self._one()
+            return self.x
+        self.eng.invalidate_weights()
+        self._one()   # step 0 eagerly: re-derives the bf16 weights and warms the allocator
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):   # capture records, does not execute: the counter stays at 1
+            self._one()
+        for _ in range(self.S - 1):
+            g.replay()
+        self._graph = g
+        return self.x

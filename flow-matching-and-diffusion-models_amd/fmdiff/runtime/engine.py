@@ -1,0 +1,524 @@
+"""Fused HIP execution of EfficientUNetND / UNetDiffusersND (forward + hand-scheduled backward).
+
+The engine walks the model's module tree (same order as the reference's
+``_run_network``: ``src/models/unet/unet.py:310-326`` and
+``src/models/unet/unet_diffusers_nd.py:172-191``) and issues the fused kernels
+of ``csrc/``:
+
+* a ResBlockND (``src/nn/blocks/residual.py:84-120``) is two implicit-GEMM
+  convs: GN1+SiLU live in conv1's gather, the time-embedding add lives in
+  conv1's epilogue, GN2 (+scale/shift)+SiLU in conv2's gather, the identity /
+  1x1 skip and residual add in conv2's epilogue; both convs emit the channel
+  statistics the next GroupNorm needs;
+* the decoder ``torch.cat([h, skip])`` is a two-source gather, never copied;
+* UpsampleND's nearest-x2 is a gather mode of the following conv;
+* attention blocks: GN folded into the qkv 1x1-conv gather, head split
+  (incl. the raw reshape) inside the attention kernel, residual in the
+  projection epilogue.
+
+The backward pass is written out (no autograd tape of primitive ops): each
+layer pushes one closure that issues weight-gradient GEMMs (activations
+recomputed in their gather prologue), data-gradient convs (with the SiLU'
+multiply and the GroupNorm-backward sums in the epilogue) and the exact
+GroupNorm backward ``dx = P*dz + Q*x + R``.  Parameter gradients are
+accumulated straight into ``param.grad`` (fp32, reference layout).
+"""
+from __future__ import annotations
+
+import math
+import weakref
+from typing import List, Optional
+
+import torch
+
+from . import ops
+from ..nn.blocks.attention import DiffusersAttentionND, SpatialCrossAttention, SpatialSelfAttention
+from ..nn.blocks.residual import ResBlockND
+from ..nn.ops.convolution import ConvND
+from ..nn.ops.upsampling import DownsampleND, UpsampleND
+from ..nn.params import Conv, Identity
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+CPAD = 8      # NHWC channel padding of the model input / output (16-byte rows)
+
+
+class Act:
+    """One NHWC bf16 activation, its per-channel statistics and its gradient."""
+    __slots__ = ("t", "stats", "grad", "need_grad")
+
+    def __init__(self, t: torch.Tensor, stats: Optional[ops.Stats] = None, need_grad: bool = True):
+        self.t = t
+        self.stats = stats
+        self.grad = None
+        self.need_grad = need_grad
+
+    @property
+    def C(self):
+        return self.t.shape[-1]
+
+
+def _stats(a: Optional[Act]):
+    if a is None:
+        return None
+    if a.stats is None:
+        a.stats = ops.channel_stats(a.t)
+    return a.stats
+
+
+def _gdest(a: Optional[Act]):
+    """(buffer, accumulate) for writing a's gradient."""
+    if a is None:
+        return None, 0
+    if a.grad is None:
+        a.grad = torch.empty_like(a.t)
+        return a.grad, 0
+    return a.grad, 1
+
+
+class WeightCache:
+    """bf16 kernel-layout copies of the fp32 master weights, rebuilt when a weight changes."""
+
+    def __init__(self):
+        self._c = {}
+        self._force = set()
+
+    def invalidate(self):
+        self._force = set(self._c.keys())
+
+    def get(self, w: torch.Tensor, mode: int, Kpad=None, Cpad=None):
+        key = (id(w), mode, Kpad, Cpad)
+        ver = (w._version, w.data_ptr())
+        ent = self._c.get(key)
+        if ent is None or ent[0] != ver or key in self._force:
+            buf = ops.prep_weights(w.detach(), mode, Kpad, Cpad, out=None if ent is None else ent[1])
+            self._c[key] = (ver, buf)
+            self._force.discard(key)
+        return self._c[key][1]
+
+    def padded(self, v: torch.Tensor, n: int):
+        key = (id(v), "pad", n)
+        ver = (v._version, v.data_ptr())
+        ent = self._c.get(key)
+        if ent is None or ent[0] != ver or key in self._force:
+            buf = ent[1] if ent is not None else torch.zeros(n, device=v.device, dtype=F32)
+            buf[: v.numel()].copy_(v.detach().reshape(-1))
+            self._c[key] = (ver, buf)
+            self._force.discard(key)
+        return self._c[key][1]
+
+    def fused(self, ws, key_name):
+        """Concatenate several fp32 tensors along dim 0 (fused q/k/v projection)."""
+        key = (tuple(id(w) for w in ws), key_name)
+        ver = tuple((w._version, w.data_ptr()) for w in ws)
+        ent = self._c.get(key)
+        if ent is None or ent[0] != ver or key in self._force:
+            buf = ent[1] if ent is not None else torch.empty((sum(w.shape[0] for w in ws), *ws[0].shape[1:]),
+                                                             device=ws[0].device, dtype=F32)
+            o = 0
+            for w in ws:
+                buf[o:o + w.shape[0]].copy_(w.detach())
+                o += w.shape[0]
+            self._c[key] = (ver, buf)
+            self._force.discard(key)
+        return self._c[key][1]
+
+
+class Ctx:
+    __slots__ = ("emb", "demb", "tape", "N")
+
+    def __init__(self, emb, save, N):
+        self.emb = emb
+        self.demb = torch.zeros_like(emb) if save else None
+        self.tape: Optional[List] = [] if save else None
+        self.N = N
+
+
+def _check_conv(c: Conv, ks, stride, pad):
+    if c.dims != 2:
+        raise NotImplementedError("fmdiff engine runs spatial_dims=2 (1-D/3-D kernels: next)")
+    if c.kernel_size != (ks, ks) or c.stride != (stride, stride) or c.padding != (pad, pad):
+        raise NotImplementedError(f"unexpected conv geometry {c.kernel_size}/{c.stride}/{c.padding}")
+
+
+class UNetEngine:
+    def __init__(self, model):
+        from ..models.unet.unet import EfficientUNetND
+        from ..models.unet.unet_diffusers_nd import UNetDiffusersND
+        self._model = weakref.ref(model)
+        if isinstance(model, EfficientUNetND):
+            self.kind = "efficient"
+        elif isinstance(model, UNetDiffusersND):
+            self.kind = "diffusers"
+        else:
+            raise TypeError(type(model))
+        self.wc = WeightCache()
+
+    @property
+    def m(self):
+        return self._model()
+
+    def invalidate_weights(self):
+        self.wc.invalidate()
+
+    # ------------------------------------------------------------- layers
+    def conv_layer(self, conv: Conv, x: Act, ctx: Ctx, *, stride=1, upsample=False, cpad=None):
+        """Plain 3x3 conv (input conv, DownsampleND, UpsampleND)."""
+        _check_conv(conv, 3, stride, 1)
+        Cin = x.C
+        w = self.wc.get(conv.weight, 0, None, Cin)
+        out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
+                           bias=conv.bias, want_stats=True)
+        o = Act(out, st)
+        if ctx.tape is not None:
+            N, H, W, _ = x.t.shape
+
+            def bwd():
+                dy = o.grad
+                ops.wgrad(x.t, dy, self._wgrad_target(conv, Cin), ks=3, stride=stride, pad=1, upsample=upsample,
+                          db=conv.bias.grad if conv.bias is not None else None)
+                self._wgrad_finish(conv, Cin)
+                if not x.need_grad:
+                    return
+                if upsample:
+                    wd = self.wc.get(conv.weight, 2)
+                    g, acc = _gdest(x)
+                    ops.conv(dy, Cin, wd, ks=4, stride=2, pad=1, out_hw_=(H, W), out=g, accumulate=bool(acc))
+                else:
+                    wd = self.wc.get(conv.weight, 1)
+                    g, acc = _gdest(x)
+                    ops.conv(dy, Cin, wd, ks=3, stride=stride, pad=1, transposed=True, out_hw_=(H, W), out=g,
+                             accumulate=bool(acc))
+            ctx.tape.append(bwd)
+        return o
+
+    def _wgrad_target(self, conv: Conv, Cin: int):
+        """fp32 buffer the wgrad kernel writes: param.grad itself unless channels were padded."""
+        if conv.weight.shape[1] == Cin and conv.weight.shape[0] % 8 == 0:
+            return conv.weight.grad
+        self._pad_tmp = torch.zeros((max(8, -(-conv.weight.shape[0] // 8) * 8), Cin, *conv.weight.shape[2:]),
+                                    device=conv.weight.device, dtype=F32)
+        return self._pad_tmp
+
+    def _wgrad_finish(self, conv: Conv, Cin: int):
+        if conv.weight.shape[1] == Cin and conv.weight.shape[0] % 8 == 0:
+            return
+        K, C = conv.weight.shape[:2]
+        conv.weight.grad.add_(self._pad_tmp[:K, :C])
+        self._pad_tmp = None
+
+    def res_block(self, m: ResBlockND, xs: List[Act], ctx: Ctx):
+        x0 = xs[0]
+        x1 = xs[1] if len(xs) > 1 else None
+        N, H, W, C0 = x0.t.shape
+        C1 = x1.C if x1 is not None else 0
+        Cin, Cout, HW = C0 + C1, m.out_channels, H * W
+        if Cin != m.channels:
+            raise ValueError(f"ResBlockND expects {m.channels} channels, got {Cin}")
+        if m.dropout and m.training:
+            raise NotImplementedError("dropout > 0 in training is not on the fmdiff engine")
+        c1, c2 = m.conv1.conv, m.conv2.conv
+        _check_conv(c1, 3, 1, 1)
+        _check_conv(c2, 3, 1, 1)
+        g1, g2 = m.norm1, m.norm2
+        el = m.emb_layers
+        eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
+        ss = m.use_scale_shift_norm
+        add = (not ss) and m.add_embedding_to_hidden
+        a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
+        h, hst = ops.conv(x0.t, Cout, self.wc.get(c1.weight, 0), src1=x1.t if x1 else None, pro=(a1, b1, True),
+                          bias=c1.bias, bias_nc=eo if add else None, want_stats=True)
+        if ss:
+            a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
+                                      emb_stride=2 * Cout, emb_mode=1)
+        else:
+            a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias)
+        sk = m.skip_connection
+        kw = {}
+        if isinstance(sk, Identity):
+            if x1 is not None:
+                raise ValueError("identity skip with concatenated input")
+            kw["resid"] = x0.t
+        else:
+            _check_conv(sk.conv, 1, 1, 0)
+            kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=self.wc.get(sk.conv.weight, 0),
+                      bias2=sk.conv.bias)
+        out, ost = ops.conv(h, Cout, self.wc.get(c2.weight, 0), pro=(a2, b2, True), bias=c2.bias, want_stats=True,
+                            **kw)
+        o = Act(out, ost)
+        if ctx.tape is None:
+            return o
+
+        def bwd():
+            dy = o.grad
+            ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
+            if isinstance(sk, Identity):
+                extra = dy
+            else:
+                sc = sk.conv
+                ops.wgrad(x0.t, dy, sc.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0, db=sc.bias.grad)
+                extra, _ = ops.conv(dy, Cin, self.wc.get(sc.weight, 1), ks=1, pad=0, transposed=True,
+                                    out_hw_=(H, W))
+            dz2, s2 = ops.conv(dy, Cout, self.wc.get(c2.weight, 1), transposed=True, out_hw_=(H, W),
+                               ep=(h, None, a2, b2), want_stats=True)
+            demb = torch.empty_like(eo)
+            if ss:
+                P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
+                                             g2.bias.grad, emb=eo, emb_stride=2 * Cout, emb_mode=1, demb=demb,
+                                             demb_stride=2 * Cout)
+            elif add:
+                P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
+                                             g2.bias.grad, emb_mode=2, demb=demb, demb_stride=Cout, fwd=hst)
+            else:
+                P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
+                                             g2.bias.grad)
+            dh = torch.empty_like(h)
+            ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
+            del dz2
+            ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True), db=c1.bias.grad)
+            dz1, s1 = ops.conv(dh, Cin, self.wc.get(c1.weight, 1), transposed=True, out_hw_=(H, W),
+                               ep=(x0.t, x1.t if x1 else None, a1, b1), want_stats=True)
+            P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,
+                                         g1.bias.grad)
+            d0, acc0 = _gdest(x0)
+            d1, acc1 = _gdest(x1)
+            ops.gn_bwd_apply(dz1, x0.t, x1.t if x1 else None, P1, Q1, R1, extra, d0, acc0, d1, acc1)
+            if ss or add:
+                ops.linear_bwd(ctx.emb, el.weight, demb, el.weight.grad, el.bias.grad, dx=ctx.demb, dx_acc=True,
+                               in_silu=m.emb_activation_before_proj)
+        ctx.tape.append(bwd)
+        return o
+
+    def attention(self, m, x: Act, ctx: Ctx):
+        """SpatialSelfAttention (raw reshape) or DiffusersAttentionND (self-attention only)."""
+        N, H, W, Cc = x.t.shape
+        T = H * W
+        if isinstance(m, SpatialSelfAttention):
+            if m.use_linear:
+                raise NotImplementedError("LinearQKVAttention is not yet on the fmdiff engine")
+            norm, heads, dh, inner, raw = m.norm, m.heads, m.dim_head, m.inner_dim, 1
+            wq = m.qkv.weight
+            bq = m.qkv.bias
+            wo, bo = m.proj_out.weight, m.proj_out.bias
+            qparts = None
+        elif isinstance(m, DiffusersAttentionND):
+            if m.context_dim is not None:
+                raise NotImplementedError("cross-attention DiffusersAttentionND is not yet on the fmdiff engine")
+            norm, heads, dh, inner, raw = m.group_norm, m.heads, m.head_dim, m.channels, 0
+            qparts = (m.to_q, m.to_k, m.to_v)
+            wq = self.wc.fused([l.weight for l in qparts], "w")
+            bq = self.wc.fused([l.bias for l in qparts], "b")
+            wo, bo = m.to_out[0].weight, m.to_out[0].bias
+        else:
+            raise NotImplementedError(type(m).__name__)
+        a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
+        qkv, _ = ops.conv(x.t, 3 * inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
+        o, lse = ops.attention_fwd(qkv, T, heads, dh, raw)
+        o4 = o.view(N, H, W, inner)
+        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x.t, want_stats=True)
+        y = Act(out, st)
+        if ctx.tape is None:
+            return y
+
+        def bwd():
+            dy = y.grad
+            ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad)
+            do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
+            dqkv = ops.attention_bwd(qkv, o, do, lse, T, heads, dh, raw)
+            if qparts is None:
+                ops.wgrad(x.t, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
+            else:
+                for i, l in enumerate(qparts):
+                    ops.wgrad(x.t, dqkv, l.weight.grad, ks=1, pad=0, pro=(a, b, False), db=l.bias.grad,
+                              dy_offset=i * inner)
+            dz, s12 = ops.conv(dqkv, Cc, self.wc.get(wq, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W),
+                               ep=(x.t, None, None, None), want_stats=True)
+            P, Q, R = ops.gn_bwd_prep(s12, N, T, Cc, norm.num_groups, mr, norm.weight, norm.bias, norm.weight.grad,
+                                      norm.bias.grad)
+            g, acc = _gdest(x)
+            ops.gn_bwd_apply(dz, x.t, None, P, Q, R, dy, g, acc)
+        ctx.tape.append(bwd)
+        return y
+
+    def head(self, norm, conv: Conv, h: Act, ctx: Ctx):
+        """GroupNorm -> SiLU -> 3x3 conv to an fp32 NHWC output with CPAD channels."""
+        _check_conv(conv, 3, 1, 1)
+        N, H, W, Cc = h.t.shape
+        K = conv.out_channels
+        Kp = max(CPAD, -(-K // 8) * 8)
+        a, b, mr = ops.gn_prep(_stats(h), None, N, H * W, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
+        w = self.wc.get(conv.weight, 0, Kp, None)
+        bias = self.wc.padded(conv.bias, Kp)
+        out, _ = ops.conv(h.t, Kp, w, pro=(a, b, True), bias=bias, out_f32=True)
+        if ctx.tape is not None:
+            def bwd(dpred):
+                tmpw = torch.zeros((Kp, Cc, 3, 3), device=out.device, dtype=F32)
+                tmpb = torch.zeros((Kp,), device=out.device, dtype=F32)
+                ops.wgrad(h.t, dpred, tmpw, pro=(a, b, True), db=tmpb, accumulate=False)
+                conv.weight.grad.add_(tmpw[:K])
+                conv.bias.grad.add_(tmpb[:K])
+                dz, s12 = ops.conv(dpred, Cc, self.wc.get(conv.weight, 1, Kp, None), transposed=True,
+                                   out_hw_=(H, W), ep=(h.t, None, a, b), want_stats=True)
+                P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
+                                          norm.weight.grad, norm.bias.grad)
+                g, acc = _gdest(h)
+                ops.gn_bwd_apply(dz, h.t, None, P, Q, R, None, g, acc)
+            self._head_bwd = bwd
+        return out
+
+    def time_mlp(self, t, ctx_save, N, t_scale=1.0, t_trunc=False):
+        m = self.m
+        if self.kind == "efficient":
+            l1, l2 = m.time_embed[0], m.time_embed[2]
+            feats = ops.timestep_embedding(t, m.model_channels, False, 0, t_scale=t_scale, t_trunc=t_trunc)
+        else:
+            l1, l2 = m.time_embedding.linear_1, m.time_embedding.linear_2
+            feats = ops.timestep_embedding(t, m.time_proj_dim, m.flip_sin_to_cos, m.freq_shift, t_scale=t_scale,
+                                           t_trunc=t_trunc)
+        h1 = ops.linear(feats, l1.weight, l1.bias)
+        emb = ops.linear(h1, l2.weight, l2.bias, in_silu=True)
+        ctx = Ctx(emb, ctx_save, N)
+        if ctx.tape is not None:
+            def bwd():
+                dh1 = torch.empty_like(h1)
+                ops.linear_bwd(h1, l2.weight, ctx.demb, l2.weight.grad, l2.bias.grad, dx=dh1, in_silu=True)
+                ops.linear_bwd(feats, l1.weight, dh1, l1.weight.grad, l1.bias.grad)
+            ctx.tape.append(bwd)
+        return ctx
+
+    # ---------------------------------------------------------------- model
+    def forward(self, xin: torch.Tensor, t: torch.Tensor, save: bool, t_scale: float = 1.0, t_trunc: bool = False):
+        """xin: NHWC bf16 [N,H,W,CPAD] (channels past the model's in_channels are 0), t: [N] timesteps
+        (``t*t_scale``, truncated to integers if ``t_trunc``).
+
+        Returns (out fp32 NHWC [N,H,W,Kpad], ctx) -- ctx carries the backward tape when ``save``."""
+        m = self.m
+        N = xin.shape[0]
+        ctx = self.time_mlp(t, save, N, t_scale, t_trunc)
+        x = Act(xin, need_grad=False)
+        if self.kind == "efficient":
+            hs = []
+            h = x
+            for blk in m.input_blocks:
+                for layer in blk:
+                    h = self._apply(layer, h, ctx)
+                hs.append(h)
+            for layer in m.middle_block:
+                h = self._apply(layer, h, ctx)
+            for blk in m.output_blocks:
+                skip = hs.pop()
+                layers = list(blk)
+                h = self.res_block(layers[0], [h, skip], ctx)
+                for layer in layers[1:]:
+                    h = self._apply(layer, h, ctx)
+            out = self.head(m.out[0], m.out[2].conv, h, ctx)
+        else:
+            h = self.conv_layer(m.conv_in, x, ctx)
+            res = [h]
+            for blk in m.down_blocks:
+                for j, r in enumerate(blk.resnets):
+                    h = self.res_block(r, [h], ctx)
+                    if blk.attentions is not None:
+                        h = self.attention(blk.attentions[j], h, ctx)
+                    res.append(h)
+                if blk.downsamplers is not None:
+                    h = self._apply(blk.downsamplers[0], h, ctx)
+                    res.append(h)
+            if m.mid_block is not None:
+                h = self.res_block(m.mid_block.resnets[0], [h], ctx)
+                if m.mid_block.attentions is not None:
+                    h = self.attention(m.mid_block.attentions[0], h, ctx)
+                h = self.res_block(m.mid_block.resnets[1], [h], ctx)
+            for blk in m.up_blocks:
+                for j, r in enumerate(blk.resnets):
+                    h = self.res_block(r, [h, res.pop()], ctx)
+                    if blk.attentions is not None:
+                        h = self.attention(blk.attentions[j], h, ctx)
+                if blk.upsamplers is not None:
+                    h = self._apply(blk.upsamplers[0], h, ctx)
+            out = self.head(m.conv_norm_out, m.conv_out, h, ctx)
+        return out, ctx
+
+    def _apply(self, layer, h: Act, ctx: Ctx) -> Act:
+        if isinstance(layer, ResBlockND):
+            return self.res_block(layer, [h], ctx)
+        if isinstance(layer, ConvND):
+            return self.conv_layer(layer.conv, h, ctx)
+        if isinstance(layer, DownsampleND):
+            if not layer.use_conv:
+                raise NotImplementedError("average-pool DownsampleND is not yet on the fmdiff engine")
+            return self.conv_layer(layer.op.conv, h, ctx, stride=2)
+        if isinstance(layer, UpsampleND):
+            if not layer.use_conv:
+                raise NotImplementedError("conv-less UpsampleND is not yet on the fmdiff engine")
+            return self.conv_layer(layer.conv.conv, h, ctx, upsample=True)
+        if isinstance(layer, (SpatialSelfAttention, DiffusersAttentionND)):
+            return self.attention(layer, h, ctx)
+        if isinstance(layer, SpatialCrossAttention):
+            raise NotImplementedError("SpatialCrossAttention is not yet on the fmdiff engine")
+        raise NotImplementedError(type(layer).__name__)
+
+    def backward(self, ctx: Ctx, dpred: torch.Tensor):
+        """Run the written-out backward. ``dpred``: bf16 NHWC [N,H,W,Kpad] gradient of the output."""
+        self._head_bwd(dpred)
+        for fn in reversed(ctx.tape):
+            fn()
+        ctx.tape = None
+        self._head_bwd = None
+
+    # ----------------------------------------------------------- utilities
+    def stage_input(self, x: torch.Tensor, context: Optional[torch.Tensor]):
+        """NCHW fp32 (x, optional concat context) -> NHWC bf16 with CPAD-padded channels."""
+        Cin = x.shape[1] + (context.shape[1] if context is not None else 0)
+        Cp = max(CPAD, -(-Cin // 8) * 8)
+        return ops.noise_prepare(None, x.float().contiguous(), None, None,
+                                 context.float().contiguous() if context is not None else None, Cp)
+
+    def params(self):
+        return [p for p in self.m.parameters()]
+
+    def ensure_grads(self):
+        for p in self.m.parameters():
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+
+
+def get_engine(model) -> UNetEngine:
+    eng = getattr(model, "_fmd_engine", None)
+    if eng is None:
+        eng = UNetEngine(model)
+        object.__setattr__(model, "_fmd_engine", eng)
+    return eng
+
+
+class _UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, x, t, context, engine, *params):
+        xin = engine.stage_input(x, context)
+        out, ctx = engine.forward(xin, t, save=True)
+        fctx.engine = engine
+        fctx.ctx = ctx
+        fctx.kpad = out.shape[-1]
+        return ops.nhwc_to_nchw(out, engine.m_out_channels)
+
+    @staticmethod
+    def backward(fctx, gout):
+        eng = fctx.engine
+        eng.ensure_grads()
+        dpred = ops.nchw_to_nhwc(gout.contiguous(), fctx.kpad)
+        eng.backward(fctx.ctx, dpred)
+        fctx.ctx = None
+        return (None, None, None, None) + tuple(None for _ in eng.params())
+
+
+def unet_apply(model, x: torch.Tensor, t: torch.Tensor, context: Optional[torch.Tensor]):
+    """Module-level entry: NCHW fp32 in -> NCHW fp32 out, differentiable w.r.t. the parameters."""
+    ops._need_cuda(x, type(model).__name__)
+    eng = get_engine(model)
+    eng.m_out_channels = model.conv_out.out_channels if eng.kind == "diffusers" else int(model.out_channels)
+    params = eng.params()
+    if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        return _UNetFunction.apply(x, t, context, eng, *params)
+    xin = eng.stage_input(x, context)
+    out, _ = eng.forward(xin, t, save=False)
+    return ops.nhwc_to_nchw(out, eng.m_out_channels)

@@ -1,0 +1,338 @@
+"""Tensor-level launchers over the C ABI (device memory from PyTorch's allocator).
+
+Every function launches on the current HIP stream and returns new device
+tensors; none of them synchronises, so the whole train / sample step can be
+captured into a hipGraph.  Activations are NHWC bf16 ``[N, H, W, C]``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _lib
+from .._lib import ConvDesc, WgradDesc
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+NUM_CU = 256
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need_cuda(t: torch.Tensor, what: str):
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{what}: fmdiff HIP kernels need ROCm device tensors (got {t.device}); "
+                           "there is no CPU path")
+
+
+@dataclass
+class Stats:
+    """Per-channel partial sums of an activation: slab [N*HW/rows][C][2] (sum, sum of squares)."""
+    slab: torch.Tensor
+    rows: int
+
+
+def channel_stats(x: torch.Tensor, rows: Optional[int] = None, y: Tuple = None) -> Stats:
+    """(sum x, sum x^2) per (n, channel, row-block), or (sum x, sum x*y) when ``y=(y0, y1, C0)`` is given."""
+    N, H, W, Cc = x.shape
+    HW = H * W
+    if rows is None:
+        rows = HW
+        while rows > 1024 and rows % 2 == 0:
+            rows //= 2
+    slab = torch.empty((N * HW // rows, Cc, 2), device=x.device, dtype=F32)
+    y0, y1, C0 = (None, None, Cc) if y is None else y
+    _lib.call("fmd_channel_stats", _p(x), _p(y0), _p(y1), C0, N, HW, Cc, rows, _p(slab), stream())
+    return Stats(slab, rows)
+
+
+def gn_prep(st0: Stats, st1: Optional[Stats], N: int, HW: int, C0: int, C1: int, groups: int, eps: float,
+            gamma, beta, emb=None, emb_stride=0, emb_mode=0):
+    """Fold GroupNorm (+ scale/shift) into a[n][c], b[n][c]; returns (a, b, mean_rstd)."""
+    dev = st0.slab.device
+    Ct = C0 + C1
+    a = torch.empty((N, Ct), device=dev, dtype=F32)
+    b = torch.empty((N, Ct), device=dev, dtype=F32)
+    mr = torch.empty((N, groups, 2), device=dev, dtype=F32)
+    _lib.call("fmd_gn_prep", _p(st0.slab), st0.rows, _p(st1.slab) if st1 else None, st1.rows if st1 else 1,
+              N, HW, C0, C1, groups, float(eps), _p(gamma), _p(beta), _p(emb), emb_stride, emb_mode,
+              _p(a), _p(b), _p(mr), stream())
+    return a, b, mr
+
+
+def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, beta, dgamma, dbeta,
+                emb=None, emb_stride=0, emb_mode=0, demb=None, demb_stride=0, fwd: Optional[Stats] = None):
+    dev = s12.slab.device
+    P = torch.empty((N, Ct), device=dev, dtype=F32)
+    Q = torch.empty((N, Ct), device=dev, dtype=F32)
+    R = torch.empty((N, Ct), device=dev, dtype=F32)
+    _lib.call("fmd_gn_bwd_prep", _p(s12.slab), s12.rows, N, HW, Ct, groups, _p(mr), _p(gamma), _p(beta), _p(emb),
+              emb_stride, emb_mode, _p(P), _p(Q), _p(R), _p(dgamma), _p(dbeta), _p(demb), demb_stride,
+              _p(fwd.slab) if fwd else None, fwd.rows if fwd else 1, stream())
+    return P, Q, R
+
+
+def gn_bwd_apply(dz, x0, x1, P, Q, R, extra, dx0, acc0, dx1=None, acc1=0):
+    N, H, W, Ct = dz.shape
+    C0 = x0.shape[-1]
+    C1 = x1.shape[-1] if x1 is not None else 0
+    _lib.call("fmd_gn_bwd_apply", _p(dz), _p(x0), _p(x1), C0, C1, N * H * W, H * W, _p(P), _p(Q), _p(R),
+              _p(extra), _p(dx0), int(acc0), _p(dx1), int(acc1), stream())
+
+
+def out_hw(Hs, ks, stride, pad, upsample):
+    Hin = Hs * (2 if upsample else 1)
+    return (Hin + 2 * pad - ks) // stride + 1
+
+
+def _choose_splits(M, K, nk, bpx=128, bco=128):
+    tiles = -(-M // bpx) * -(-K // bco)
+    if tiles >= NUM_CU or nk < 8:
+        return 1
+    return max(1, min(nk // 4, -(-2 * NUM_CU // tiles), 32))
+
+
+def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, transposed=False, out_hw_=None,
+         pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
+         out_f32=False,
+         accumulate=False, want_stats=False, ep=None, splits=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+    """Implicit-GEMM conv (see csrc/conv.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``."""
+    _need_cuda(src0, "conv")
+    N, Hs, Ws, C0 = src0.shape
+    C1 = src1.shape[-1] if src1 is not None else 0
+    if out_hw_ is not None:
+        Ho, Wo = out_hw_
+    else:
+        Ho, Wo = out_hw(Hs, ks, stride, pad, upsample), out_hw(Ws, ks, stride, pad, upsample)
+    M = N * Ho * Wo
+    dev = src0.device
+    if out is None:
+        out = torch.empty((N, Ho, Wo, K), device=dev, dtype=F32 if out_f32 else BF16)
+    d = ConvDesc()
+    d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, Hs, Ws, C0, C1, Ho, Wo, K
+    d.ks, d.stride, d.pad, d.upsample, d.transposed = ks, stride, pad, int(upsample), int(transposed)
+    d.src0, d.src1 = _p(src0), _p(src1)
+    if pro is not None:
+        d.pro_a, d.pro_b, d.pro_silu = _p(pro[0]), _p(pro[1]), int(pro[2])
+    d.wgt = _p(wgt)
+    if src2 is not None:
+        d.src2, d.src3, d.C2, d.C3, d.wgt2 = _p(src2), _p(src3), src2.shape[-1], (src3.shape[-1] if src3 is not None else 0), _p(wgt2)
+    d.bias, d.bias2, d.bias_nc, d.resid, d.out = _p(bias), _p(bias2), _p(bias_nc), _p(resid), _p(out)
+    d.out_f32, d.accumulate = int(out_f32), int(accumulate)
+    if ep is not None:
+        x0, x1, ea, eb = ep
+        d.ep_x0, d.ep_x1, d.ep_C0, d.ep_a, d.ep_b = _p(x0), _p(x1), x0.shape[-1], _p(ea), _p(eb)
+        if x1 is None and x0.shape[-1] != K:
+            raise ValueError("epilogue tensor channels must match the conv output channels")
+    T = ks * ks
+    nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
+    bco = 16 if K <= 16 else (64 if K <= 64 else 128)
+    bpx = 256 if K <= 16 else 128
+    if splits is None:
+        splits = _choose_splits(M, K, nk, bpx, bco)
+    ws = None
+    if splits > 1:
+        ws = torch.empty((splits, M, K), device=dev, dtype=F32)
+        d.ws, d.splits = _p(ws), splits
+    else:
+        d.splits = 1
+    st = None
+    fused_stats = want_stats and splits == 1 and (Ho * Wo) % 64 == 0 and M % bpx == 0
+    if fused_stats:
+        slab = torch.empty((M // 64, K, 2), device=dev, dtype=F32)
+        d.stats = _p(slab)
+        st = Stats(slab, 64)
+    _lib.call("fmd_conv", C.byref(d), stream())
+    if want_stats and not fused_stats:
+        if ep is not None:
+            st = channel_stats(out, y=(ep[0], ep[1], ep[0].shape[-1]))
+        else:
+            st = channel_stats(out)
+    return out, st
+
+
+def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro=None, db=None, accumulate=True,
+          splits=None, dy_offset=0):
+    """dW (+)= conv weight gradient in the reference [K][C][kh][kw] fp32 layout (and db).
+
+    ``dy_offset``: use channels [dy_offset, dy_offset + dw.shape[0]) of a wider dY (fused q/k/v)."""
+    N, Hs, Ws, C0 = src0.shape
+    C1 = src1.shape[-1] if src1 is not None else 0
+    _, Ho, Wo, ldy = dy.shape
+    K = dw.shape[0]
+    M = N * Ho * Wo
+    Ct = C0 + C1
+    d = WgradDesc()
+    d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, Hs, Ws, C0, C1, Ho, Wo, K
+    d.ks, d.stride, d.pad, d.upsample = ks, stride, pad, int(upsample)
+    d.src0, d.src1 = _p(src0), _p(src1)
+    if pro is not None:
+        d.pro_a, d.pro_b, d.pro_silu = _p(pro[0]), _p(pro[1]), int(pro[2])
+    d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
+    if splits is None:
+        tiles = -(-K // 128) * -(-Ct // 128) * ks * ks
+        steps = -(-M // 32)
+        splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), 256))
+    d.splits = splits
+    ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
+    d.ws = _p(ws)
+    _lib.call("fmd_wgrad", C.byref(d), stream())
+
+
+def prep_weights(w: torch.Tensor, mode: int, Kpad: Optional[int] = None, Cpad: Optional[int] = None, out=None):
+    """fp32 [K][C][kh][kw] -> bf16 kernel layout (mode 0 fwd [Kpad][T][Cpad]; 1 dgrad [Cpad][T][Kpad]; 2 up-dgrad)."""
+    K, Cc = w.shape[0], w.shape[1]
+    ks = w.shape[2] if w.dim() == 4 else 1
+    Kpad = Kpad or K
+    Cpad = Cpad or Cc
+    T = 16 if mode == 2 else ks * ks
+    shape = (Kpad, T, Cpad) if mode == 0 else (Cpad, T, Kpad)
+    if out is None:
+        out = torch.empty(shape, device=w.device, dtype=BF16)
+    _lib.call("fmd_prep_weights", _p(w.contiguous()), K, Cc, ks, mode, Kpad, Cpad, _p(out), stream())
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, Cpad: Optional[int] = None) -> torch.Tensor:
+    _need_cuda(x, "nchw_to_nhwc")
+    x = x.contiguous().float()
+    N, Cc = x.shape[:2]
+    HW = x[0, 0].numel()
+    Cpad = Cpad or Cc
+    y = torch.empty((N, *x.shape[2:], Cpad), device=x.device, dtype=BF16)
+    _lib.call("fmd_nchw_to_nhwc", _p(x), N, Cc, HW, Cpad, _p(y), stream())
+    return y
+
+
+def nhwc_to_nchw(y: torch.Tensor, Cc: int) -> torch.Tensor:
+    N = y.shape[0]
+    sp = y.shape[1:-1]
+    Cs = y.shape[-1]
+    x = torch.empty((N, Cc, *sp), device=y.device, dtype=F32)
+    _lib.call("fmd_nhwc_to_nchw", _p(y), int(y.dtype == F32), N, Cc, x[0, 0].numel(), Cs, _p(x), stream())
+    return x
+
+
+def timestep_embedding(t: torch.Tensor, dim: int, flip: bool, shift: int = 0, max_period: float = 10000.0,
+                       t_scale: float = 1.0, t_trunc: bool = False):
+    if t.dtype != F32:
+        t = t.float()
+    t = t.contiguous()
+    out = torch.empty((t.shape[0], dim), device=t.device, dtype=F32)
+    _lib.call("fmd_timestep_embedding", _p(t), t.shape[0], dim, int(flip), shift, float(max_period), float(t_scale),
+              int(t_trunc), _p(out), stream())
+    return out
+
+
+def linear(x, w, b, in_silu=False, out=None, out_stride=None):
+    B, I = x.shape
+    O = w.shape[0]
+    if out is None:
+        out = torch.empty((B, O), device=x.device, dtype=F32)
+    _lib.call("fmd_linear", _p(x), B, I, _p(w), _p(b), O, int(in_silu), _p(out), out_stride or O, stream())
+    return out
+
+
+def linear_bwd(x, w, dy, dw, db, dx=None, dx_acc=False, in_silu=False, dy_stride=None):
+    B, I = x.shape
+    O = w.shape[0]
+    _lib.call("fmd_linear_bwd", _p(x), B, I, _p(w), O, int(in_silu), _p(dy), dy_stride or dy.shape[-1], _p(dx),
+              int(dx_acc), _p(dw), _p(db), stream())
+
+
+def silu_bwd(x, dy):
+    dx = torch.empty_like(x)
+    _lib.call("fmd_silu_bwd_f32", _p(x), _p(dy), _p(dx), x.numel(), stream())
+    return dx
+
+
+def attention_fwd(qkv, T, heads, dh, raw):
+    B = qkv.shape[0]
+    o = torch.empty((B, T, heads * dh), device=qkv.device, dtype=BF16)
+    lse = torch.empty((B, heads, T), device=qkv.device, dtype=F32)
+    _lib.call("fmd_attention_fwd", _p(qkv), B, T, heads, dh, int(raw), _p(o), _p(lse), stream())
+    return o, lse
+
+
+def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
+    B = qkv.shape[0]
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty_like(lse)
+    _lib.call("fmd_attention_bwd", _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), B, T, heads, dh, int(raw),
+              _p(dqkv), stream())
+    return dqkv
+
+
+def sum_pool2(src, dst, acc):
+    N, H, W, Cc = dst.shape
+    _lib.call("fmd_sum_pool2", _p(src), N, H, W, Cc, _p(dst), int(acc), stream())
+
+
+def add_(dst, a):
+    _lib.call("fmd_add_bf16", _p(a), _p(dst), dst.numel(), stream())
+
+
+def noise_prepare(x0, noise, ca, cb, cond, Cpad, out=None):
+    N, Cx = noise.shape[:2]
+    HW = noise[0, 0].numel()
+    Cc = cond.shape[1] if cond is not None else 0
+    if out is None:
+        out = torch.empty((N, *noise.shape[2:], Cpad), device=noise.device, dtype=BF16)
+    _lib.call("fmd_noise_prepare", _p(x0), _p(noise), _p(ca), _p(cb), _p(cond), N, HW, Cx, Cc, Cpad, _p(out),
+              stream())
+    return out
+
+
+def mse(pred_nhwc, ta, tb, tb_sign, grad_scale, loss, partial, dpred=None):
+    N = pred_nhwc.shape[0]
+    Kpad = pred_nhwc.shape[-1]
+    Cx = ta.shape[1]
+    HW = ta[0, 0].numel()
+    _lib.call("fmd_mse", _p(pred_nhwc), Kpad, _p(ta), _p(tb), float(tb_sign), N, Cx, HW, float(grad_scale),
+              _p(partial), partial.numel(), _p(loss), _p(dpred), stream())
+
+
+def adamw_sched(p, g, m, v, step_ctr, base_lr, warmup, total, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,
+                grad_scale=1.0):
+    _lib.call("fmd_adamw_sched", _p(p), _p(g), _p(m), _p(v), p.numel(), _p(step_ctr), float(base_lr), int(warmup),
+              int(total), float(beta1), float(beta2), float(eps), float(wd), float(grad_scale), stream())
+
+
+def counter_add(ctr, v=1):
+    _lib.call("fmd_counter_add", _p(ctr), int(v), stream())
+
+
+def fill_from_table(table, index, out):
+    _lib.call("fmd_fill_from_table", _p(table), _p(index), _p(out), out.numel(), stream())
+
+
+def flow_euler(x, v_nhwc, sigmas, index, cond, next_inp):
+    N, Cx = x.shape[:2]
+    HW = x[0, 0].numel()
+    Cc = cond.shape[1] if cond is not None else 0
+    _lib.call("fmd_flow_euler", _p(x), _p(v_nhwc), v_nhwc.shape[-1], _p(sigmas), _p(index), N, Cx, HW, _p(cond), Cc,
+              next_inp.shape[-1] if next_inp is not None else 0, _p(next_inp), stream())
+
+
+def ddpm_step(x, eps_nhwc, coef, index, noise, cond, next_inp):
+    N, Cx = x.shape[:2]
+    HW = x[0, 0].numel()
+    Cc = cond.shape[1] if cond is not None else 0
+    _lib.call("fmd_ddpm_step", _p(x), _p(eps_nhwc), eps_nhwc.shape[-1], _p(coef), _p(index), _p(noise), N, Cx, HW,
+              _p(cond), Cc, next_inp.shape[-1] if next_inp is not None else 0, _p(next_inp), stream())
+
+
+def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    _lib.call("fmd_adamw", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
+              float(wd), float(bc1), float(bc2), stream())

@@ -1,0 +1,182 @@
+/*
+ * fmdiff: MI355X-native (gfx950 / CDNA4) kernels for the flow-matching /
+ * diffusion UNet train + sample hot path.  C ABI, plain pointers and sizes.
+ *
+ * Ownership: every buffer (activations, weights, workspaces) is allocated by
+ * the caller (PyTorch's caching allocator) and passed in; the library
+ * allocates nothing.  Errors: every entry point returns 0 on success, a
+ * positive hipError_t, or a negative argument-validation code; no exception
+ * crosses the ABI.  Threading: kernels are stateless and launch on the
+ * caller's hipStream_t.
+ *
+ * Layouts: activations NHWC bf16 ("pixels x channels"); conv weights bf16
+ * [K][ks*ks][C] (forward) -- the fp32 master copy stays in the reference's
+ * [K][C][kh][kw] layout so state_dicts are drop-in.
+ *
+ * The reference has no native plugin API: its boundary is the Python module
+ * surface.  Each entry point names the reference op(s) it replaces.
+ */
+#ifndef FMDIFF_H
+#define FMDIFF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fmd_stream_t; /* hipStream_t */
+
+/* ------------------------------------------------------------------ conv
+ * Implicit-GEMM convolution on MFMA, replacing ConvND -> nn.Conv{2}d
+ * (src/nn/ops/convolution.py:8-54), the GroupNorm+SiLU(+scale/shift) that
+ * feeds it (src/nn/blocks/residual.py:95-117), nearest-x2 UpsampleND
+ * (src/nn/ops/upsampling.py:27), DownsampleND stride 2 (upsampling.py:49-56),
+ * the decoder torch.cat (src/models/unet/unet.py:322), the 1x1 skip conv and
+ * residual add (residual.py:120).  The same kernel computes data gradients
+ * (transposed gather) for the backward pass.
+ */
+typedef struct fmd_conv_desc {
+  int32_t N, Hs, Ws;        /* stored input dims */
+  int32_t C0, C1;           /* channels of src0 / src1 (virtual concat, C = C0 + C1) */
+  int32_t Ho, Wo, K;        /* output dims / output channels */
+  int32_t ks, stride, pad;  /* square kernel, stride, zero padding */
+  int32_t upsample;         /* 1: logical input = nearest-x2 of the stored input */
+  int32_t transposed;       /* 1: gather (o + pad - k) / stride  (data-gradient mode) */
+  const void* src0;         /* bf16 NHWC [N][Hs][Ws][C0] */
+  const void* src1;         /* bf16 NHWC [N][Hs][Ws][C1] or NULL */
+  const float* pro_a;       /* [N][C] prologue affine x*a+b (GroupNorm fused), or NULL */
+  const float* pro_b;
+  int32_t pro_silu;         /* apply SiLU after the affine */
+  const void* wgt;          /* bf16 [K][ks*ks][C] */
+  const void* src2;         /* optional 1x1 second GEMM over the concat (src2 | src3): */
+  const void* src3;         /*   bf16 [N][Ho][Wo][C2] and [N][Ho][Wo][C3] (ResBlock skip conv) */
+  int32_t C2, C3;
+  const void* wgt2;         /* bf16 [K][C2+C3] */
+  const float* bias;        /* [K] or NULL */
+  const float* bias2;       /* [K] or NULL (skip-conv bias, added too) */
+  const float* bias_nc;     /* [N][K] per-sample bias (time-embedding add) or NULL */
+  const void* resid;        /* bf16 [N][Ho][Wo][K] residual or NULL */
+  void* out;                /* bf16 (or fp32 if out_f32) [N][Ho][Wo][K] */
+  int32_t out_f32;
+  int32_t accumulate;       /* out += result */
+  float* stats;             /* slab [M/64][K][2] of per-64-pixel partial sums, or NULL */
+  const void* ep_x0;        /* data-gradient epilogue: x = forward GN input at (p, c); if ep_a: */
+                            /*   out *= silu'(ep_a*x+ep_b); stats become (sum out, sum out*x) */
+  const void* ep_x1;
+  int32_t ep_C0;
+  const float* ep_a;
+  const float* ep_b;
+  float* ws;                /* split-K workspace fp32 [splits][M][K] */
+  int32_t splits;
+} fmd_conv_desc;
+
+int fmd_conv(const fmd_conv_desc* d, fmd_stream_t s);
+
+/* Weight-gradient GEMM: dW[K][C][kh][kw] (+)= sum_p dY[p][K] x gather(src)[p][tap][C]
+ * with the same gather/prologue as the forward; db[K] (+)= sum_p dY[p][K].
+ * Replaces autograd of nn.Conv2d weight/bias (convolution.py:53). */
+typedef struct fmd_wgrad_desc {
+  int32_t N, Hs, Ws, C0, C1, Ho, Wo, K, ks, stride, pad, upsample;
+  const void* src0; const void* src1;
+  const float* pro_a; const float* pro_b; int32_t pro_silu;
+  const void* dy;           /* bf16 [N][Ho][Wo][ldy], first K channels used */
+  int32_t ldy;              /* dy row stride in elements (0 -> K) */
+  float* dw;                /* fp32 [K][C][ks][ks] (reference layout) */
+  float* db;                /* fp32 [K] or NULL */
+  int32_t accumulate;
+  float* ws;                /* fp32 workspace, size fmd_wgrad_workspace() floats */
+  int32_t splits;
+} fmd_wgrad_desc;
+
+int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t s);
+int64_t fmd_wgrad_workspace(const fmd_wgrad_desc* d);
+
+/* ------------------------------------------------------------- groupnorm
+ * nn.GroupNorm (src/nn/ops/normalization.py:11-19, attention.py:97) is never
+ * materialised: producers emit per-channel sums, fmd_gn_prep folds mean/rstd,
+ * gamma/beta and the ResBlock scale/shift into a per-(n,c) affine consumed by
+ * the conv prologue. */
+int fmd_channel_stats(const void* x, const void* y0, const void* y1, int32_t C0, int32_t N, int32_t HW, int32_t C,
+                      int32_t rows, float* out /* [N*HW/rows][C][2] */, fmd_stream_t s);
+int fmd_gn_prep(const float* st0, int32_t rows0, const float* st1, int32_t rows1, int32_t N, int32_t HW,
+                int32_t C0, int32_t C1, int32_t G, float eps, const float* gamma, const float* beta,
+                const float* emb, int32_t emb_stride, int32_t emb_mode /*0 none,1 scale-shift*/,
+                float* a, float* b, float* mean_rstd, fmd_stream_t s);
+/* emb_mode 0: plain GN; 1: scale/shift (demb = [dscale | dshift]); 2: embedding added to the GN
+ * input (demb[n][c] = sum_hw dx, from the forward channel sums fwd_st of x). */
+int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_t HW, int32_t C, int32_t G,
+                    const float* mean_rstd, const float* gamma, const float* beta, const float* emb,
+                    int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R,
+                    float* dgamma, float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st,
+                    int32_t fwd_rows, fmd_stream_t s);
+int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,
+                     int32_t HW, const float* P, const float* Q, const float* R, const void* extra,
+                     void* dx0, int32_t acc0, void* dx1, int32_t acc1, fmd_stream_t s);
+
+/* -------------------------------------------------- weights and layouts
+ * fp32 reference-layout conv weight -> bf16 kernel layout.  mode 0: [Kpad][T][Cpad]
+ * forward; mode 1: [Cpad][T][Kpad] data gradient (transposed gather); mode 2:
+ * [Cpad][16][Kpad] data gradient of nearest-x2 upsample + 3x3 conv (4x4 taps). */
+int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t Kpad, int32_t Cpad,
+                     void* out, fmd_stream_t s);
+int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s);
+int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
+                     fmd_stream_t s);
+int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc, fmd_stream_t s);
+int fmd_add_bf16(const void* a, void* dst, int64_t n, fmd_stream_t s);
+
+/* ------------------------------------------------------ time embedding
+ * timestep_embedding (src/nn/ops/time_embedding.py:4-32), the time MLP
+ * (src/models/unet/unet.py:117-121, src/models/unet/utils.py:9-24) and the
+ * ResBlock emb_layers (src/nn/blocks/residual.py:63-68,102-104). */
+/* t_eff = t*t_scale, truncated to an integer when t_trunc (the FM trainer's (t*(N-1)).long()) */
+int fmd_timestep_embedding(const float* t, int32_t N, int32_t dim, int32_t flip, int32_t shift, float max_period,
+                           float t_scale, int32_t t_trunc, float* out, fmd_stream_t s);
+int fmd_linear(const float* x, int32_t B, int32_t I, const float* w, const float* b, int32_t O, int32_t in_silu,
+               float* y, int32_t y_stride, fmd_stream_t s);
+int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t O, int32_t in_silu,
+                   const float* dy, int32_t dy_stride, float* dx, int32_t dx_acc, float* dw, float* db,
+                   fmd_stream_t s);
+int fmd_silu_bwd_f32(const float* x, const float* dy, float* dx, int64_t n, fmd_stream_t s);
+
+/* ----------------------------------------------------------- attention
+ * F.scaled_dot_product_attention inside SpatialSelfAttention (raw=1, raw
+ * reshape head split, src/nn/blocks/attention.py:111-115) and
+ * DiffusersAttentionND (raw=0, attention.py:262-268). qkv: bf16 [B][T][3*inner]. */
+int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw, void* o,
+                      float* lse, fmd_stream_t s);
+int fmd_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, int32_t B,
+                      int32_t T, int32_t heads, int32_t dh, int32_t raw, void* dqkv, fmd_stream_t s);
+
+/* ------------------------------------------ train step / sampler / optim
+ * FM input x_t = (1-t)x0 + t*eps and DDPM add_noise (flow_matching_lib.py:151-158,
+ * diffusion_lib.py:154-160) -> NHWC model input with the concatenated
+ * conditioning; MSE loss + gradient (flow_matching_lib.py:166-167); the
+ * FlowMatchEuler / DDPM step (diffusers, called at src/pipelines/utils.py:218);
+ * torch.optim.AdamW (flow_matching_lib.py:73,177). */
+/* x channels: ca&&cb: ca[n]*x0 + cb[n]*noise (DDPM add_noise); ca only: (1-ca[n])*x0 + ca[n]*noise
+ * (FM, ca = t); neither: noise (sampler input). */
+int fmd_noise_prepare(const float* x0, const float* noise, const float* ca, const float* cb, const float* cond,
+                      int32_t N, int32_t HW, int32_t Cx, int32_t Cc, int32_t Cpad, void* inp, fmd_stream_t s);
+int fmd_mse(const float* pred, int32_t Kpad, const float* ta, const float* tb, float tb_sign, int32_t N, int32_t Cx,
+            int32_t HW, float grad_scale, float* partial, int32_t max_blocks, float* loss, void* dpred,
+            fmd_stream_t s);
+int fmd_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+              float wd, float bc1, float bc2, fmd_stream_t s);
+/* AdamW with the step count on device and get_cosine_schedule_with_warmup's LR computed in-kernel
+ * (graph-replayable train step); g is scaled by grad_scale first. */
+int fmd_adamw_sched(float* p, const float* g, float* m, float* v, int64_t n, const int32_t* step_ctr, float base_lr,
+                    int32_t warmup, int32_t total, float beta1, float beta2, float eps, float wd, float grad_scale,
+                    fmd_stream_t s);
+int fmd_flow_euler(float* x, const float* v, int32_t Kpad, const float* sigmas, const int32_t* index, int32_t N,
+                   int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad, void* next, fmd_stream_t s);
+int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, const int32_t* index,
+                  const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
+                  void* next, fmd_stream_t s);
+int fmd_fill_from_table(const float* table, const int32_t* index, float* out, int32_t N, fmd_stream_t s);
+int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,261 @@
+"""Per-kernel numerics on the GPU: each HIP kernel vs a plain PyTorch fp32 reference of the same op.
+
+Inputs are bf16-rounded before the reference sees them, so the only expected
+differences are fp32 accumulation order and the final bf16 rounding of the
+kernel output (tolerance: 1.5e-2 x max|ref| for bf16 outputs, 1e-4 for fp32).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def ops():
+    from fmdiff.runtime import ops as O
+    return O
+
+
+def _close(got, ref, rel=1.5e-2):
+    ref = ref.float().cpu()
+    got = got.float().cpu()
+    err = (got - ref).abs().max().item()
+    scale = max(ref.abs().max().item(), 1e-6)
+    assert err <= rel * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _rand_nhwc(N, H, W, C, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(N, H, W, C, generator=g) * scale).to(torch.bfloat16)
+
+
+def _w(K, C, ks, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(K, C, ks, ks, generator=g) / math.sqrt(C * ks * ks)
+
+
+def _to_nchw(x):
+    return x.float().permute(0, 3, 1, 2).contiguous()
+
+
+def _bfw(w):
+    return w.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("case", [
+    dict(N=2, H=16, W=16, C=128, K=128, ks=3, stride=1),
+    dict(N=2, H=16, W=16, C=64, K=128, ks=3, stride=2),
+    dict(N=1, H=8, W=8, C=256, K=64, ks=1, stride=1),
+    dict(N=2, H=32, W=32, C=8, K=128, ks=3, stride=1),
+    dict(N=2, H=16, W=16, C=128, K=8, ks=3, stride=1),
+])
+def test_conv_forward(case):
+    O = ops()
+    N, H, W, C, K, ks, s = (case[k] for k in ("N", "H", "W", "C", "K", "ks", "stride"))
+    x = _rand_nhwc(N, H, W, C, 1)
+    w = _w(K, C, ks, 2)
+    b = torch.randn(K) * 0.1
+    pad = ks // 2
+    out, _ = O.conv(x.to(DEV), K, O.prep_weights(w.to(DEV), 0), ks=ks, stride=s, pad=pad, bias=b.to(DEV))
+    ref = F.conv2d(_to_nchw(x), _bfw(w), b, stride=s, padding=pad).permute(0, 2, 3, 1)
+    _close(out, ref)
+
+
+def test_conv_prologue_concat_upsample_skip_resid_stats():
+    O = ops()
+    N, H, W, C0, C1, K = 2, 8, 8, 64, 32, 128
+    x0, x1 = _rand_nhwc(N, H, W, C0, 3), _rand_nhwc(N, H, W, C1, 4)
+    a = torch.rand(N, C0 + C1) + 0.5
+    bb = torch.randn(N, C0 + C1) * 0.2
+    w = _w(K, C0 + C1, 3, 5)
+    bias = torch.randn(K) * 0.1
+    # upsample + concat + GN-affine/SiLU prologue, stats epilogue
+    out, st = O.conv(x0.to(DEV), K, O.prep_weights(w.to(DEV), 0), src1=x1.to(DEV), upsample=True,
+                     pro=(a.to(DEV), bb.to(DEV), True), bias=bias.to(DEV), want_stats=True)
+    xc = torch.cat([_to_nchw(x0), _to_nchw(x1)], 1)
+    z = F.silu(xc * a[:, :, None, None] + bb[:, :, None, None]).to(torch.bfloat16).float()
+    ref = F.conv2d(F.interpolate(z, scale_factor=2, mode="nearest"), _bfw(w), bias, padding=1).permute(0, 2, 3, 1)
+    _close(out, ref)
+    s = st.slab.cpu().view(N, -1, K, 2).sum(1)
+    o = out.float().cpu()
+    torch.testing.assert_close(s[..., 0], o.sum((1, 2)), rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(s[..., 1], (o * o).sum((1, 2)), rtol=2e-3, atol=2e-2)
+    # 1x1 skip second segment over the concat + residual-free epilogue
+    h = _rand_nhwc(N, H, W, K, 6)
+    w2 = _w(K, K, 3, 7)
+    ws = _w(K, C0 + C1, 1, 8)
+    bs = torch.randn(K) * 0.1
+    out2, _ = O.conv(h.to(DEV), K, O.prep_weights(w2.to(DEV), 0), src2=x0.to(DEV), src3=x1.to(DEV),
+                     wgt2=O.prep_weights(ws.to(DEV), 0), bias=bias.to(DEV), bias2=bs.to(DEV))
+    ref2 = (F.conv2d(_to_nchw(h), _bfw(w2), bias, padding=1)
+            + F.conv2d(torch.cat([_to_nchw(x0), _to_nchw(x1)], 1), _bfw(ws), bs)).permute(0, 2, 3, 1)
+    _close(out2, ref2)
+    # identity residual
+    out3, _ = O.conv(h.to(DEV), K, O.prep_weights(w2.to(DEV), 0), resid=h.to(DEV))
+    ref3 = (F.conv2d(_to_nchw(h), _bfw(w2), padding=1) + _to_nchw(h)).permute(0, 2, 3, 1)
+    _close(out3, ref3)
+
+
+def test_conv_splitk_matches():
+    O = ops()
+    x = _rand_nhwc(2, 8, 8, 512, 9)
+    w = _w(256, 512, 3, 10)
+    wp = O.prep_weights(w.to(DEV), 0)
+    a, _ = O.conv(x.to(DEV), 256, wp, splits=1)
+    b, _ = O.conv(x.to(DEV), 256, wp, splits=6)
+    _close(b, a.float(), rel=8e-3)
+
+
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1"])
+def test_conv_data_gradient(mode):
+    O = ops()
+    N, H, W, C, K = 2, 16, 16, 64, 128
+    ks, s, up = (1, 1, False) if mode == "1x1" else (3, 2 if mode == "s2" else 1, mode == "up")
+    pad = ks // 2
+    x = _to_nchw(_rand_nhwc(N, H, W, C, 11)).requires_grad_()
+    w = _w(K, C, ks, 12)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if up else x
+    y = F.conv2d(xin, _bfw(w), stride=s, padding=pad)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+    if up:
+        got, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 2), ks=4, stride=2, pad=1, out_hw_=(H, W))
+    else:
+        got, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 1), ks=ks, stride=s, pad=pad, transposed=True,
+                        out_hw_=(H, W))
+    _close(got, x.grad.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro"])
+def test_wgrad(mode):
+    O = ops()
+    N, H, W, C, K = 2, 16, 16, 64, 128
+    ks, s, up = (1, 1, False) if mode == "1x1" else (3, 2 if mode == "s2" else 1, mode == "up")
+    pad = ks // 2
+    xb = _rand_nhwc(N, H, W, C, 13)
+    x = _to_nchw(xb)
+    pro = None
+    if mode == "pro":
+        a = torch.rand(N, C) + 0.5
+        b = torch.randn(N, C) * 0.2
+        x = F.silu(x * a[:, :, None, None] + b[:, :, None, None]).to(torch.bfloat16).float()
+        pro = (a.to(DEV), b.to(DEV), True)
+    w = _w(K, C, ks, 14).requires_grad_()
+    bias = torch.zeros(K, requires_grad=True)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if up else x
+    y = F.conv2d(xin, w, bias, stride=s, padding=pad)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dw = torch.zeros(K, C, ks, ks, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    O.wgrad(xb.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV), dw, ks=ks, stride=s,
+            pad=pad, upsample=up, pro=pro, db=db)
+    torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
+    torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
+
+
+def test_groupnorm_forward_backward():
+    O = ops()
+    N, H, W, C, G = 2, 16, 16, 96, 32
+    xb = _rand_nhwc(N, H, W, C, 15, 2.0) .float().add(0.5).to(torch.bfloat16)
+    x = _to_nchw(xb).requires_grad_()
+    gamma = (torch.rand(C) + 0.5).requires_grad_()
+    beta = (torch.randn(C) * 0.1).requires_grad_()
+    emb = torch.randn(N, 2 * C) * 0.3
+    scale, shift = emb[:, :C], emb[:, C:]
+    z = F.group_norm(x, G, gamma, beta, 1e-5) * (1 + scale[:, :, None, None]) + shift[:, :, None, None]
+    dz = torch.randn_like(z).to(torch.bfloat16).float()
+    z.backward(dz)
+    st = O.channel_stats(xb.to(DEV))
+    a, b, mr = O.gn_prep(st, None, N, H * W, C, 0, G, 1e-5, gamma.detach().to(DEV), beta.detach().to(DEV),
+                         emb=emb.to(DEV), emb_stride=2 * C, emb_mode=1)
+    zk = xb.float().to(DEV) * a[:, None, None, :] + b[:, None, None, :]
+    _close(zk, z.detach().permute(0, 2, 3, 1), rel=1e-4)
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+    s12 = O.channel_stats(dzn, y=(xb.to(DEV), None, C))
+    dg = torch.zeros(C, device=DEV)
+    dbt = torch.zeros(C, device=DEV)
+    demb = torch.zeros(N, 2 * C, device=DEV)
+    P, Q, R = O.gn_bwd_prep(s12, N, H * W, C, G, mr, gamma.detach().to(DEV), beta.detach().to(DEV), dg, dbt,
+                            emb=emb.to(DEV), emb_stride=2 * C, emb_mode=1, demb=demb, demb_stride=2 * C)
+    dx = torch.empty_like(dzn)
+    O.gn_bwd_apply(dzn, xb.to(DEV), None, P, Q, R, None, dx, 0)
+    _close(dx, x.grad.permute(0, 2, 3, 1))
+    torch.testing.assert_close(dg.cpu(), gamma.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dbt.cpu(), beta.grad, rtol=1e-3, atol=1e-3)
+    ref_ds = (dz * F.group_norm(x.detach(), G, gamma.detach(), beta.detach(), 1e-5)).sum((2, 3))
+    torch.testing.assert_close(demb[:, :C].cpu(), ref_ds, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(demb[:, C:].cpu(), dz.sum((2, 3)), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32)])
+def test_attention(raw, T, heads, dh):
+    O = ops()
+    B = 2
+    inner = heads * dh
+    qkv = (torch.randn(B, T, 3 * inner) * 0.5).to(torch.bfloat16)
+    f = qkv.float().requires_grad_()
+    if raw:
+        flat = f.transpose(1, 2).reshape(B, heads, T, 3 * dh)   # (B, 3*inner, T) read raw
+        q, k, v = flat.chunk(3, dim=-1)
+    else:
+        q, k, v = (f[..., i * inner:(i + 1) * inner].view(B, T, heads, dh).transpose(1, 2) for i in range(3))
+    o = F.scaled_dot_product_attention(q, k, v)
+    if raw:
+        o_tok = o.reshape(B, inner, T).transpose(1, 2)          # raw reinterpretation as (inner, T)
+    else:
+        o_tok = o.transpose(1, 2).reshape(B, T, inner)
+    do = torch.randn_like(o_tok).to(torch.bfloat16).float()
+    o_tok.backward(do)
+    og, lse = O.attention_fwd(qkv.to(DEV), T, heads, dh, raw)
+    _close(og, o_tok.detach())
+    dq = O.attention_bwd(qkv.to(DEV), og, do.contiguous().to(torch.bfloat16).to(DEV), lse, T, heads, dh, raw)
+    _close(dq, f.grad, rel=2e-2)
+
+
+def test_time_embedding_and_linear():
+    O = ops()
+    from oracle.unet import timestep_embedding
+    t = torch.tensor([0.0, 1.0, 17.0, 999.0, 1000.0, 979.6122436523438])
+    for dim, flip, shift in [(128, False, 0), (128, True, 0), (33, False, 1)]:
+        got = O.timestep_embedding(t.to(DEV), dim, flip, shift)
+        torch.testing.assert_close(got.cpu(), timestep_embedding(t, dim, flip_sin_to_cos=flip, freq_shift=shift),
+                                   rtol=2e-5, atol=2e-4)
+    x = torch.randn(8, 128, requires_grad=True)
+    w = torch.randn(512, 128) * 0.05
+    b = torch.randn(512) * 0.1
+    for silu in (False, True):
+        y = F.linear(F.silu(x) if silu else x, w, b)
+        got = O.linear(x.detach().to(DEV), w.to(DEV), b.to(DEV), in_silu=silu)
+        torch.testing.assert_close(got.cpu(), y.detach(), rtol=1e-4, atol=1e-4)
+        dy = torch.randn_like(y)
+        x.grad = None
+        wr = w.clone().requires_grad_()
+        br = b.clone().requires_grad_()
+        F.linear(F.silu(x) if silu else x, wr, br).backward(dy)
+        dw = torch.zeros_like(w, device=DEV)
+        db = torch.zeros_like(b, device=DEV)
+        dx = torch.empty(8, 128, device=DEV)
+        O.linear_bwd(x.detach().to(DEV), w.to(DEV), dy.to(DEV), dw, db, dx=dx, in_silu=silu)
+        torch.testing.assert_close(dw.cpu(), wr.grad, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(db.cpu(), br.grad, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(dx.cpu(), x.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_adamw_matches_torch():
+    O = ops()
+    torch.manual_seed(0)
+    p0 = torch.randn(10000)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01, foreach=False)
+    p, m, v = p0.clone().to(DEV), torch.zeros(10000, device=DEV), torch.zeros(10000, device=DEV)
+    for step in range(1, 4):
+        g = torch.randn(10000)
+        ref.grad = g.clone()
+        opt.step()
+        O.adamw(p, g.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-7)
