@@ -62,19 +62,20 @@ def conv_roofline(dev, iters=20):
     a = torch.rand(N, C, device=dev) + 0.5
     b = torch.randn(N, C, device=dev) * 0.1
     bias = torch.zeros(K, device=dev)
+    wt = ops.tile_weights(w)
     out = torch.empty(N, H, W, K, device=dev, dtype=torch.bfloat16)
     for _ in range(3):
-        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True)
+        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(iters):
-        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True)
+        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2.0 * N * H * W * K * C * 9
-    return dict(kernel="conv_igemm<128,128,2,2,64> (GN+SiLU prologue, 3x3, 8x256x256x128->128)",
+    return dict(kernel="conv3x3_halo<false> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)",
                 ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
 
 
@@ -85,7 +86,8 @@ def cpu_baseline(iters=2):
     from oracle import spec as S
     from oracle import train_step as OT
     from oracle import unet as U
-    threads = os.cpu_count() or 1
+    # the GPU box gives one GPU a 16-CPU share (os.cpu_count() reports the whole host)
+    threads = min(os.cpu_count() or 1, int(os.environ.get("FMD_CPU_THREADS", "16")))
     torch.set_num_threads(threads)
     spec = S.derive_spec(LDCT_FM_UNET, "concatenate", 1)
     sd = {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, 0).items()}
@@ -105,6 +107,7 @@ def cpu_baseline(iters=2):
         sc.backward()
         OT.adamw_step(sd, 1e-4, i + 1, state)
         dt = time.perf_counter() - t0
+        log(f"[bench] cpu baseline iter {i}: {dt:.2f} s ({threads} threads)")
         if i:
             times.append(dt)
     times.sort()
@@ -209,6 +212,7 @@ def main():
             dist.destroy_process_group()
         return
     roof = conv_roofline(dev)
+    log(f"[bench] dominant conv: {roof['ms']:.3f} ms, {roof['tflops']:.1f} TFLOP/s")
     step_tflops = train_ips / world * TRAIN_GFLOP_PER_IMAGE / 1e3
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

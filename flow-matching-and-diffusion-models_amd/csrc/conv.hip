@@ -466,6 +466,10 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->splits > 1 && (!d->ws || d->stats)) return -5;
   (void)C;
   int rc;
+  if (d->splits <= 1 && d->K > 16 && !d->force_generic) {
+    rc = fmd_conv_halo(d, stream);   // 3x3 stride-1 problems with >= 128 16x16 tiles
+    if (rc != 1) return rc;
+  }
   if (d->K <= 16)
     rc = launch<16, 256, 1, 4, 64>(d, s);
   else if (d->K <= 64)

@@ -1,0 +1,411 @@
+// Halo-tiled 3x3 stride-1 convolution for gfx950 -- the UNet's dominant problem.
+//
+// Workgroup = 512 threads (8 waves) computing a 16x16-pixel x 128-output-channel
+// tile.  Per 64-channel chunk of the input, the (16+2)x(16+2) halo of the tile is
+// gathered ONCE (GroupNorm affine + SiLU applied once per element, zero padding,
+// optional nearest-x2 upsample = a 10x10 low-resolution halo, optional two-source
+// concat) into LDS, and all 9 taps read their shifted 16-pixel rows from that
+// single image: 9x less gather/transform work and ~7x less activation traffic
+// than a per-tap implicit GEMM.  Per tap, a 128x64 weight slice streams through
+// a double-buffered LDS tile (weights are pre-tiled in HBM by fmd_prep_weights
+// mode 4, so each slice is one contiguous 16 KiB block); the next chunk's halo
+// is gathered in 9 pieces behind the current chunk's MFMAs, one barrier per tap.
+//
+// LDS images are chunk-major ([16-byte k-chunk plane][row]): an MFMA fragment
+// read touches 16 consecutive rows of one plane = one 256-byte bank row, so
+// every ds_read_b128 is conflict-free for any row offset (tap shifts); planes
+// are padded to 338 rows so the 16-byte writes of one position's chunks land
+// in distinct banks.
+//
+// Same epilogue contract as csrc/conv.hip (bias, per-sample bias, residual,
+// second 1x1 GEMM over src2|src3, data-gradient SiLU' + GN-backward sums,
+// channel statistics).
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+constexpr int TH = 16, TW = 16;           // output tile
+constexpr int BCO = 128;                  // output channels per tile
+constexpr int BK = 64;                    // input channels per chunk
+constexpr int KC = BK / 8;                // 16-byte chunks per position
+constexpr int NT = 512;
+constexpr int HALO = (TH + 2) * (TW + 2); // 324 positions
+constexpr int HPAD = 338;                 // plane stride (rows): 338*16 B == 32 mod 128
+constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer
+constexpr int WBUF = KC * BCO * 8;        // bf16 elements per weight buffer (16 KiB)
+
+struct HArgs {
+  fmd_conv_desc d;
+  int C, C23;
+  int tiles_x, tiles_y, ntc;
+  int nchunk1, nchunk2;   // main / 1x1-segment chunks
+  int nsteps;
+  const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
+  const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
+};
+
+template <bool UP>
+__global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
+  constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
+  constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk
+  __shared__ __attribute__((aligned(16))) bf16r lds[2 * HBUF + 2 * WBUF];
+  bf16r* hbuf = lds;
+  bf16r* wbuf = lds + 2 * HBUF;
+
+  const fmd_conv_desc& d = A.d;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wco = wid >> 2, wpx = wid & 3;   // 2 x 4 waves: 64 couts x 4 pixel rows each
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  const int per_img = A.tiles_x * A.tiles_y;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tco = b % A.ntc;
+  const int tile = b / A.ntc;
+  const int n = tile / per_img;
+  const int tin = tile - n * per_img;
+  const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
+  const int co0 = tco * BCO;
+  const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;   // halo origin (stored-input coordinates)
+  const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
+
+  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
+  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
+  const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
+  const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
+  const bool pro = d.pro_a != nullptr;
+  const int nchunks = A.nchunk1 + A.nchunk2;
+
+  // ---- staging registers
+  u32x4 rw[2];           // two weight chunks per thread (16 KiB / 512 threads)
+  u32x4 rh[2];           // halo chunks per thread per step (main loop: <= 1, prologue / 1x1: <= 2)
+  int hidx[2];           // halo chunk index; -1 none; <= -2 zero chunk (-2 - index)
+  f32x4 ca[2][2], cb[2][2];  // GN affine coefficients of the staged chunks
+
+  auto wtile = [&](int s) -> const bf16r* {
+    if (s < A.nchunk1 * 9) {
+      const int chunk = s / 9, tap = s - (s / 9) * 9;
+      return A.wt + (((size_t)tco * A.nchunk1 + chunk) * 9 + tap) * WBUF;
+    }
+    return A.wt2 + ((size_t)tco * A.nchunk2 + (s - A.nchunk1 * 9)) * WBUF;
+  };
+  auto load_w = [&](int s) {
+    const bf16r* src = wtile(s);
+    rw[0] = *(const u32x4*)(src + tid * 8);
+    rw[1] = *(const u32x4*)(src + (tid + NT) * 8);
+  };
+  auto store_w = [&](int buf) {
+    *(u32x4*)(wbuf + buf * WBUF + tid * 8) = rw[0];
+    *(u32x4*)(wbuf + buf * WBUF + (tid + NT) * 8) = rw[1];
+  };
+
+  // halo chunk h of `chunk`: kc = h % KC (fastest: one position's 128 B are read by 8 lanes), pos = h / KC
+  auto load_h = [&](int chunk, int lo, int hi, int per) {
+    const bool seg2 = chunk >= A.nchunk1;
+    const int cbase = (seg2 ? chunk - A.nchunk1 : chunk) * BK;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int h = lo + tid + k * NT;
+      hidx[k] = -1;
+      rh[k] = u32x4{0u, 0u, 0u, 0u};
+      if (k >= per || h >= hi) continue;
+      const int kc = h & (KC - 1), pos = h >> 3;
+      const int c = cbase + kc * 8;
+      if (!seg2) {
+        const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
+        const int y = hy0 + py, x = hx0 + px;
+        if (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws && c < A.C) {
+          const size_t pix = ((size_t)n * d.Hs + y) * d.Ws + x;
+          rh[k] = *(const u32x4*)((c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0));
+          hidx[k] = h;
+          if (pro) {
+            const float* pa = d.pro_a + (size_t)n * A.C + c;
+            const float* pb = d.pro_b + (size_t)n * A.C + c;
+            ca[k][0] = *(const f32x4*)pa; ca[k][1] = *(const f32x4*)(pa + 4);
+            cb[k][0] = *(const f32x4*)pb; cb[k][1] = *(const f32x4*)(pb + 4);
+          }
+        } else {
+          hidx[k] = -2 - h;
+        }
+      } else {
+        const int py = pos / (TW + 2), px = pos - (pos / (TW + 2)) * (TW + 2);
+        const int y = ty0 - 1 + py, x = tx0 - 1 + px;
+        if (y >= 0 && y < d.Ho && x >= 0 && x < d.Wo && c < A.C23) {
+          const size_t pix = ((size_t)n * d.Ho + y) * d.Wo + x;
+          rh[k] = *(const u32x4*)((c < d.C2) ? s2 + pix * d.C2 + c : s3 + pix * d.C3 + (c - d.C2));
+          hidx[k] = h;
+        } else {
+          hidx[k] = -2 - h;
+        }
+      }
+    }
+  };
+  auto store_h = [&](int buf, bool transform) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int h = hidx[k];
+      if (h == -1) continue;
+      const bool valid = h >= 0;
+      if (!valid) h = -2 - h;
+      const int kc = h & (KC - 1), pos = h >> 3;
+      u32x4 v = rh[k];
+      if (valid && transform) {
+        const float av[8] = {ca[k][0][0], ca[k][0][1], ca[k][0][2], ca[k][0][3],
+                             ca[k][1][0], ca[k][1][1], ca[k][1][2], ca[k][1][3]};
+        const float bv[8] = {cb[k][0][0], cb[k][0][1], cb[k][0][2], cb[k][0][3],
+                             cb[k][1][0], cb[k][1][1], cb[k][1][2], cb[k][1][3]};
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = bf_lo(v[e]) * av[2 * e] + bv[2 * e];
+          float hi = bf_hi(v[e]) * av[2 * e + 1] + bv[2 * e + 1];
+          if (d.pro_silu) { lo = siluf_(lo); hi = siluf_(hi); }
+          o[e] = pack2(lo, hi);
+        }
+        v = o;
+      }
+      *(u32x4*)(hbuf + buf * HBUF + (kc * HPAD + pos) * 8) = v;
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int chunk, int tap, bool seg2, int wb_i) {
+    const bf16r* hb = hbuf + (chunk & 1) * HBUF;
+    const bf16r* wb = wbuf + wb_i * WBUF;
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int pl = ks * 4 + lq;   // 16-byte plane this lane reads
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(wb + (pl * BCO + wco * 64 + 16 * i + l16) * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int py = wpx * 4 + j;
+        int pos;
+        if (UP && !seg2) {
+          const int ly = ((ty0 + py + ky - 1) >> 1) - hy0;
+          const int lx = ((tx0 + l16 + kx - 1) >> 1) - hx0;
+          pos = ly * HROW + lx;
+        } else {
+          pos = (py + ky) * (TW + 2) + l16 + kx;
+        }
+        const bf16x8 bv = *(const bf16x8*)(hb + (pl * HPAD + pos) * 8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
+      }
+    }
+  };
+
+  // ---- prologue: full halo of chunk 0 + weights of step 0
+  {
+    const bool s2c = A.nchunk1 == 0;
+    const int tot = KC * (s2c ? HALO : HPOS);
+    for (int lo = 0; lo < tot; lo += 2 * NT) {
+      load_h(0, lo, tot, 2);
+      store_h(0, pro && !s2c);
+    }
+    load_w(0);
+    store_w(0);
+    __syncthreads();
+  }
+
+  for (int s = 0; s < A.nsteps; ++s) {
+    const bool seg2 = s >= A.nchunk1 * 9;
+    const int chunk = seg2 ? A.nchunk1 + (s - A.nchunk1 * 9) : s / 9;
+    const int tap = seg2 ? 4 : s - chunk * 9;
+    const int nt = seg2 ? 1 : 9;
+    const int t_in = seg2 ? 0 : tap;
+    const bool more = chunk + 1 < nchunks;
+    const bool nseg2 = chunk + 1 >= A.nchunk1;
+    if (more) {
+      const int tot = KC * (nseg2 ? HALO : HPOS);
+      const int lo = (int)((long)tot * t_in / nt), hi = (int)((long)tot * (t_in + 1) / nt);
+      load_h(chunk + 1, lo, hi, 2);
+    }
+    const bool wnext = s + 1 < A.nsteps;
+    if (wnext) load_w(s + 1);
+    compute(chunk, tap, seg2, s & 1);
+    if (wnext) store_w((s + 1) & 1);
+    if (more) store_h((chunk + 1) & 1, pro && !nseg2);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------ epilogue
+  const int K = d.K;
+  const int Ho = d.Ho, Wo = d.Wo;
+  const bool stats = d.stats != nullptr;
+  const bool dep = d.ep_a != nullptr;
+  const bool hasx = d.ep_x0 != nullptr;
+  float st1[4][4], st2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { st1[i][r] = 0.f; st2[i][r] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + wco * 64 + 16 * i + 4 * lq;
+    if (co >= K) continue;
+    const bool full = co + 3 < K;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) {
+      if (co + r < K) {
+        if (d.bias) bias[r] += d.bias[co + r];
+        if (d.bias2) bias[r] += d.bias2[co + r];
+        if (d.bias_nc) bias[r] += d.bias_nc[(size_t)n * K + co + r];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = ty0 + wpx * 4 + j, x = tx0 + l16;
+      const size_t p = ((size_t)n * Ho + y) * Wo + x;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[r];
+      if (d.resid) {
+        const bf16r* rp = (const bf16r*)d.resid + p * K + co;
+        if (full) {
+          const u32x2 rr = *(const u32x2*)rp;
+          v[0] += bf_lo(rr[0]); v[1] += bf_hi(rr[0]); v[2] += bf_lo(rr[1]); v[3] += bf_hi(rr[1]);
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) v[r] += bf2f(rp[r]);
+        }
+      }
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (hasx) {
+        const int C0e = d.ep_C0;
+        for (int r = 0; r < 4; ++r) {
+          const int c = co + r;
+          if (c >= K) continue;
+          const bf16r* xp = (c < C0e) ? (const bf16r*)d.ep_x0 + p * C0e + c
+                                      : (const bf16r*)d.ep_x1 + p * (K - C0e) + (c - C0e);
+          xv[r] = bf2f(*xp);
+          if (dep) v[r] *= silu_grad(d.ep_a[(size_t)n * K + c] * xv[r] + d.ep_b[(size_t)n * K + c]);
+        }
+      }
+      if (d.out_f32) {
+        float* op = (float*)d.out + p * K + co;
+        for (int r = 0; r < 4; ++r)
+          if (co + r < K) op[r] = d.accumulate ? op[r] + v[r] : v[r];
+      } else {
+        bf16r* op = (bf16r*)d.out + p * K + co;
+        if (full) {
+          if (d.accumulate) {
+            const u32x2 o = *(const u32x2*)op;
+            v[0] += bf_lo(o[0]); v[1] += bf_hi(o[0]); v[2] += bf_lo(o[1]); v[3] += bf_hi(o[1]);
+          }
+          u32x2 o;
+          o[0] = pack2(v[0], v[1]);
+          o[1] = pack2(v[2], v[3]);
+          *(u32x2*)op = o;
+          v[0] = bf_lo(o[0]); v[1] = bf_hi(o[0]); v[2] = bf_lo(o[1]); v[3] = bf_hi(o[1]);
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) {
+              const float w = d.accumulate ? bf2f(op[r]) + v[r] : v[r];
+              op[r] = (bf16r)f2bf(w);
+              v[r] = bf2f(op[r]);
+            }
+        }
+      }
+      if (stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st1[i][r] += v[r];
+          st2[i][r] += hasx ? v[r] * xv[r] : v[r] * v[r];
+        }
+      }
+    }
+  }
+  if (stats) {
+    // slab row = one wave's 64 pixels (4 rows x 16) of one image; any bijection works for GN
+    const int srow = tile * 4 + wpx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = st1[i][r], q = st2[i][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
+        if (l16 == 0 && co < K) {
+          float* sp = d.stats + ((size_t)srow * K + co) * 2;
+          sp[0] = a;
+          sp[1] = q;
+        }
+      }
+    }
+  }
+}
+
+// [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
+__global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, int C, int ntc, int nchunk,
+                                    bf16r* __restrict__ out) {
+  const long long total = (long long)ntc * nchunk * T * KC * BCO * 8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7);
+    long long r = i >> 3;
+    const int co = (int)(r % BCO); r /= BCO;
+    const int kc = (int)(r % KC); r /= KC;
+    const int tap = (int)(r % T); r /= T;
+    const int chunk = (int)(r % nchunk);
+    const int tc = (int)(r / nchunk);
+    const int k = tc * BCO + co, c = chunk * BK + kc * 8 + e;
+    out[i] = (k < K && c < C) ? w[((size_t)k * T + tap) * C + c] : (bf16r)0;
+  }
+}
+
+}  // namespace
+
+// Called by fmd_conv when the problem qualifies (3x3, stride 1, pad 1, forward gather,
+// output tile 16x16 inside one image, >= 128 tiles).  Returns 1 if not applicable.
+extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed || d->splits > 1) return 1;
+  if (d->Ho % TH || d->Wo % TW) return 1;
+  if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
+  if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
+  HArgs A;
+  A.d = *d;
+  A.C = d->C0 + d->C1;
+  A.C23 = d->src2 ? d->C2 + d->C3 : 0;
+  A.tiles_x = d->Wo / TW;
+  A.tiles_y = d->Ho / TH;
+  A.ntc = (d->K + BCO - 1) / BCO;
+  A.nchunk1 = (A.C + BK - 1) / BK;
+  A.nchunk2 = d->src2 ? (A.C23 + BK - 1) / BK : 0;
+  A.nsteps = A.nchunk1 * 9 + A.nchunk2;
+  A.wt = (const bf16r*)d->wgt_tiled;
+  A.wt2 = (const bf16r*)d->wgt2_tiled;
+  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  if (nwg < 128) return 1;   // too few tiles to fill the chip: the split-K implicit GEMM wins
+  if (d->upsample)
+    hipLaunchKernelGGL(conv3x3_halo<true>, dim3(nwg), dim3(NT), 0, (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(conv3x3_halo<false>, dim3(nwg), dim3(NT), 0, (hipStream_t)stream, A);
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C) {
+  return (int64_t)((K + BCO - 1) / BCO) * ((C + BK - 1) / BK) * T * KC * BCO * 8;
+}
+
+extern "C" int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* out,
+                                     fmd_stream_t stream) {
+  const int ntc = (K + BCO - 1) / BCO, nchunk = (C + BK - 1) / BK;
+  const long long total = (long long)ntc * nchunk * T * KC * BCO * 8;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(tile_weights_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const bf16r*)w, K, T,
+                     C, ntc, nchunk, (bf16r*)out);
+  return (int)hipGetLastError();
+}

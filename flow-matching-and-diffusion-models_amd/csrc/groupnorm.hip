@@ -130,77 +130,92 @@ __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const f
   }
 }
 
-// one block per group; loops over n so gamma/beta grads are complete per block
-__global__ void gn_bwd_prep_kernel(const float* __restrict__ s12, int rows, int N, int HW, int C, int G,
-                                   const float* __restrict__ mr, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, const float* __restrict__ emb, int emb_stride,
-                                   int emb_mode, float* __restrict__ P, float* __restrict__ Q, float* __restrict__ R,
-                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ demb,
-                                   int demb_stride, const float* __restrict__ fst, int frows) {
-  const int g = blockIdx.x;
+// one block per (n, group).  T = 256/Cg threads share each channel's slab entries
+// (E = HW/rows of them), so the big slabs of the high-resolution levels are
+// reduced in parallel; gamma/beta contributions go to a per-(n,c) scratch that
+// gn_bwd_gb_kernel folds over n (deterministic, no atomics).
+__global__ __launch_bounds__(256) void gn_bwd_prep_kernel(
+    const float* __restrict__ s12, int rows, int N, int HW, int C, int G, const float* __restrict__ mr,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ emb, int emb_stride,
+    int emb_mode, float* __restrict__ P, float* __restrict__ Q, float* __restrict__ R, float* __restrict__ gb,
+    float* __restrict__ demb, int demb_stride, const float* __restrict__ fst, int frows) {
+  const int n = blockIdx.x / G, g = blockIdx.x - (blockIdx.x / G) * G;
   const int Cg = C / G;
   const int E = HW / rows;
-  __shared__ double sh1[1024], sh2[1024];   // per-channel S1, S2 (Cg <= 1024)
+  const int FE = emb_mode == 2 ? HW / frows : 0;
+  __shared__ double sS1[256], sS2[256], sSx[256];
+  __shared__ double ch1[256], ch2[256], chx[256];
   __shared__ double red[2][256];
-  double dg_acc[4] = {0, 0, 0, 0}, db_acc[4] = {0, 0, 0, 0};   // channels threadIdx.x + 256*k
-  for (int n = 0; n < N; ++n) {
-    const float mean = mr[((size_t)n * G + g) * 2], rstd = mr[((size_t)n * G + g) * 2 + 1];
-    double a1 = 0.0, a2 = 0.0;
-    for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
-      const int c = g * Cg + cl;
-      double S1 = 0.0, S2 = 0.0;
-      for (int e = 0; e < E; ++e) {
-        const float* p = s12 + (((size_t)n * E + e) * C + c) * 2;
-        S1 += p[0]; S2 += p[1];
-      }
-      sh1[cl] = S1; sh2[cl] = S2;
-      const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
-      const double gp = (double)(gamma ? gamma[c] : 1.f) * s;
-      const double dzxh = (double)rstd * (S2 - (double)mean * S1);
-      a1 += gp * S1;
-      a2 += gp * dzxh;
+  const int tid = threadIdx.x;
+  const int T = 256 / Cg;                 // threads per channel (Cg <= 256)
+  const int cl = tid / T, sub = tid - (tid / T) * T;
+  double a = 0.0, q = 0.0, sx = 0.0;
+  if (cl < Cg) {
+    const int c = g * Cg + cl;
+    for (int e = sub; e < E; e += T) {
+      const float* p = s12 + (((size_t)n * E + e) * C + c) * 2;
+      a += p[0];
+      q += p[1];
     }
-    red[0][threadIdx.x] = a1; red[1][threadIdx.x] = a2;
+    for (int e = sub; e < FE; e += T) sx += fst[(((size_t)n * FE + e) * C + c) * 2];
+  }
+  sS1[tid] = a; sS2[tid] = q; sSx[tid] = sx;
+  __syncthreads();
+  if (tid < Cg) {
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int k = 0; k < T; ++k) { s1 += sS1[tid * T + k]; s2 += sS2[tid * T + k]; s3 += sSx[tid * T + k]; }
+    ch1[tid] = s1; ch2[tid] = s2; chx[tid] = s3;
+  }
+  __syncthreads();
+  const float mean = mr[((size_t)n * G + g) * 2], rstd = mr[((size_t)n * G + g) * 2 + 1];
+  double a1 = 0.0, a2 = 0.0;
+  if (tid < Cg) {
+    const int c = g * Cg + tid;
+    const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
+    const double gp = (double)(gamma ? gamma[c] : 1.f) * s;
+    a1 = gp * ch1[tid];
+    a2 = gp * (double)rstd * (ch2[tid] - (double)mean * ch1[tid]);
+  }
+  red[0][tid] = a1; red[1][tid] = a2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) { red[0][tid] += red[0][tid + o]; red[1][tid] += red[1][tid + o]; }
     __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) { red[0][threadIdx.x] += red[0][threadIdx.x + o]; red[1][threadIdx.x] += red[1][threadIdx.x + o]; }
-      __syncthreads();
-    }
+  }
+  if (tid < Cg) {
     const double cnt = (double)Cg * HW;
     const double A1 = red[0][0] / cnt, A2 = red[1][0] / cnt;
     const double r = rstd;
-    for (int cl = threadIdx.x, k = 0; cl < Cg; cl += blockDim.x, ++k) {
-      const int c = g * Cg + cl;
-      const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
-      const double gm = gamma ? gamma[c] : 1.f;
-      const double bt = beta ? beta[c] : 0.f;
-      const double gp = gm * s;
-      const double S1 = sh1[cl], S2 = sh2[cl];
-      const double dzxh = r * (S2 - (double)mean * S1);
-      P[(size_t)n * C + c] = (float)(r * gp);
-      Q[(size_t)n * C + c] = (float)(-r * r * A2);
-      R[(size_t)n * C + c] = (float)(r * r * A2 * mean - r * A1);
-      if (k < 4) { dg_acc[k] += s * dzxh; db_acc[k] += s * S1; }
-      if (emb_mode == 1 && demb) {
-        demb[(size_t)n * demb_stride + c] = (float)(gm * dzxh + bt * S1);
-        demb[(size_t)n * demb_stride + C + c] = (float)S1;
-      }
-      if (emb_mode == 2 && demb) {
-        // sum_hw dx = P*S1 + Q*sum_hw x + R*HW, sum_hw x from the forward statistics
-        const int FE = HW / frows;
-        double sx = 0.0;
-        for (int e = 0; e < FE; ++e) sx += fst[(((size_t)n * FE + e) * C + c) * 2];
-        demb[(size_t)n * demb_stride + c] =
-            (float)(r * gp * S1 + (-r * r * A2) * sx + (r * r * A2 * mean - r * A1) * (double)HW);
-      }
+    const int c = g * Cg + tid;
+    const double s = emb_mode == 1 ? 1.0 + (double)emb[(size_t)n * emb_stride + c] : 1.0;
+    const double gm = gamma ? gamma[c] : 1.f;
+    const double bt = beta ? beta[c] : 0.f;
+    const double gp = gm * s;
+    const double S1 = ch1[tid], S2 = ch2[tid];
+    const double dzxh = r * (S2 - (double)mean * S1);
+    const double Pv = r * gp, Qv = -r * r * A2, Rv = r * r * A2 * mean - r * A1;
+    P[(size_t)n * C + c] = (float)Pv;
+    Q[(size_t)n * C + c] = (float)Qv;
+    R[(size_t)n * C + c] = (float)Rv;
+    gb[((size_t)n * C + c) * 2] = (float)(s * dzxh);
+    gb[((size_t)n * C + c) * 2 + 1] = (float)(s * S1);
+    if (emb_mode == 1 && demb) {
+      demb[(size_t)n * demb_stride + c] = (float)(gm * dzxh + bt * S1);
+      demb[(size_t)n * demb_stride + C + c] = (float)S1;
     }
-    __syncthreads();
+    if (emb_mode == 2 && demb)   // sum_hw dx = P*S1 + Q*sum_hw x + R*HW (forward stats give sum_hw x)
+      demb[(size_t)n * demb_stride + c] = (float)(Pv * S1 + Qv * chx[tid] + Rv * (double)HW);
   }
-  for (int cl = threadIdx.x, k = 0; cl < Cg && k < 4; cl += blockDim.x, ++k) {
-    const int c = g * Cg + cl;
-    if (dgamma) dgamma[c] += (float)dg_acc[k];
-    if (dbeta) dbeta[c] += (float)db_acc[k];
-  }
+}
+
+__global__ void gn_bwd_gb_kernel(const float* __restrict__ gb, int N, int C, float* __restrict__ dgamma,
+                                 float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int n = 0; n < N; ++n) { a += gb[((size_t)n * C + c) * 2]; b += gb[((size_t)n * C + c) * 2 + 1]; }
+  if (dgamma) dgamma[c] += a;
+  if (dbeta) dbeta[c] += b;
 }
 
 // dx = P*dz + Q*x + R (+ extra), split into two destinations at C0
@@ -274,13 +289,20 @@ extern "C" int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_
                                const float* mean_rstd, const float* gamma, const float* beta, const float* emb,
                                int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R, float* dgamma,
                                float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st, int32_t fwd_rows,
-                               fmd_stream_t s) {
-  if (C % G || HW % rows || C / G > 1024) return -1;
+                               float* ws, fmd_stream_t s) {
+  if (C % G || HW % rows || C / G > 256 || !ws) return -1;
   if (emb_mode == 2 && (!fwd_st || HW % fwd_rows)) return -2;
-  hipLaunchKernelGGL(gn_bwd_prep_kernel, dim3(G), dim3(256), 0, (hipStream_t)s, s12, rows, N, HW, C, G, mean_rstd,
-                     gamma, beta, emb, emb_stride, emb_mode, P, Q, R, dgamma, dbeta, demb, demb_stride, fwd_st,
+  hipLaunchKernelGGL(gn_bwd_prep_kernel, dim3(N * G), dim3(256), 0, (hipStream_t)s, s12, rows, N, HW, C, G,
+                     mean_rstd, gamma, beta, emb, emb_stride, emb_mode, P, Q, R, ws, demb, demb_stride, fwd_st,
                      fwd_rows);
-  return (int)hipGetLastError();
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  if (dgamma || dbeta) {
+    hipLaunchKernelGGL(gn_bwd_gb_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)s, ws, N, C, dgamma,
+                       dbeta);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
 }
 
 extern "C" int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,

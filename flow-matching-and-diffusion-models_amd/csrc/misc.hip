@@ -33,14 +33,16 @@ __global__ void prep_weights_kernel(const float* __restrict__ w, int K, int C, i
       float v = (k < K && c < C) ? w[((size_t)k * C + c) * T + tap] : 0.f;
       out[i] = (bf16r)f2bf(v);
     }
-  } else if (mode == 1) {
+  } else if (mode == 1 || mode == 3) {
+    // mode 3: taps flipped (T-1-tap) -> the data gradient of a stride-1 conv as a forward gather
     const long long total = (long long)Cpad * T * Kpad;
     GRID_STRIDE(i, total) {
       const int k = (int)(i % Kpad);
       const long long r = i / Kpad;
       const int tap = (int)(r % T);
       const int c = (int)(r / T);
-      float v = (k < K && c < C) ? w[((size_t)k * C + c) * T + tap] : 0.f;
+      const int st = mode == 3 ? T - 1 - tap : tap;
+      float v = (k < K && c < C) ? w[((size_t)k * C + c) * T + st] : 0.f;
       out[i] = (bf16r)f2bf(v);
     }
   } else {
@@ -160,16 +162,39 @@ __global__ void linear_dw_kernel(const float* __restrict__ x, int B, int I, int 
   }
 }
 
-// dx[b][i] (+)= f'(x) * sum_o dy[b][o] w[o][i]
-__global__ void linear_dx_kernel(const float* __restrict__ x, int B, int I, const float* __restrict__ w, int O,
-                                 int in_silu, const float* __restrict__ dy, int dys, float* __restrict__ dx, int acc) {
-  const long long total = (long long)B * I;
-  GRID_STRIDE(idx, total) {
-    const int i = (int)(idx % I), b = (int)(idx / I);
-    float s = 0.f;
-    for (int o = 0; o < O; ++o) s += dy[(size_t)b * dys + o] * w[(size_t)o * I + i];
-    if (in_silu) s *= silu_grad(x[idx]);
-    dx[idx] = acc ? dx[idx] + s : s;
+// dx[b][i] += f'(x) * sum_o dy[b][o] w[o][i].  Grid (I/64, O/256): each wave sums 64 rows o
+// for 64 columns i and all b (<= 32), waves combine in LDS, blocks combine with fp32 atomics
+// (dx must be initialised by the caller).
+__global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ x, int B, int I,
+                                                        const float* __restrict__ w, int O, int in_silu,
+                                                        const float* __restrict__ dy, int dys,
+                                                        float* __restrict__ dx) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int o0 = blockIdx.y * 256 + wv * 64;
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+  if (i < I) {
+    for (int o = o0; o < min(O, o0 + 64); ++o) {
+      const float wv_ = w[(size_t)o * I + i];
+#pragma unroll
+      for (int b = 0; b < 32; ++b)
+        if (b < B) acc[b] += dy[(size_t)b * dys + o] * wv_;
+    }
+  }
+  __shared__ float red[4][32][64];
+#pragma unroll
+  for (int b = 0; b < 32; ++b)
+    if (b < B) red[wv][b][lane] = acc[b];
+  __syncthreads();
+  for (int k = threadIdx.x; k < B * 64; k += 256) {
+    const int b = k >> 6, l = k & 63;
+    const int ii = blockIdx.x * 64 + l;
+    if (ii >= I) continue;
+    float s = red[0][b][l] + red[1][b][l] + red[2][b][l] + red[3][b][l];
+    if (in_silu) s *= silu_grad(x[(size_t)b * I + ii]);
+    atomicAdd(dx + (size_t)b * I + ii, s);
   }
 }
 
@@ -431,8 +456,13 @@ int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t
     if (rc) return rc;
   }
   if (dx) {
-    hipLaunchKernelGGL(linear_dx_kernel, dim3(grid_for((long long)B * I)), dim3(256), 0, (hipStream_t)s, x, B, I, w,
-                       O, in_silu, dy, dy_stride, dx, dx_acc);
+    if (!dx_acc) {   // the kernel accumulates with atomics
+      int rc = (int)hipMemsetAsync(dx, 0, sizeof(float) * (size_t)B * I, (hipStream_t)s);
+      if (rc) return rc;
+    }
+    if (B > 32) return -1;
+    hipLaunchKernelGGL(linear_dx_kernel, dim3((I + 63) / 64, (O + 255) / 256), dim3(256), 0, (hipStream_t)s, x, B, I,
+                       w, O, in_silu, dy, dy_stride, dx);
     return (int)hipGetLastError();
   }
   return 0;

@@ -25,7 +25,7 @@ class ConvDesc(C.Structure):
         ("src2", p), ("src3", p), ("C2", i32), ("C3", i32), ("wgt2", p),
         ("bias", p), ("bias2", p), ("bias_nc", p), ("resid", p), ("out", p), ("out_f32", i32), ("accumulate", i32),
         ("stats", p), ("ep_x0", p), ("ep_x1", p), ("ep_C0", i32), ("ep_a", p), ("ep_b", p),
-        ("ws", p), ("splits", i32),
+        ("ws", p), ("splits", i32), ("force_generic", i32), ("wgt_tiled", p), ("wgt2_tiled", p),
     ]
 
 
@@ -42,11 +42,14 @@ class WgradDesc(C.Structure):
 # name -> argtypes (restype is int32 unless listed in _RESTYPE)
 SIGNATURES = {
     "fmd_conv": [C.POINTER(ConvDesc), p],
+    "fmd_conv_halo": [C.POINTER(ConvDesc), p],
     "fmd_wgrad": [C.POINTER(WgradDesc), p],
     "fmd_wgrad_workspace": [C.POINTER(WgradDesc)],
+    "fmd_halo_tiled_size": [i32, i32, i32],
+    "fmd_tile_weights_halo": [p, i32, i32, i32, p, p],
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
-    "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p],
+    "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
@@ -68,7 +71,7 @@ SIGNATURES = {
     "fmd_fill_from_table": [p, p, p, i32, p],
     "fmd_counter_add": [p, i32, p],
 }
-_RESTYPE = {"fmd_wgrad_workspace": i64}
+_RESTYPE = {"fmd_wgrad_workspace": i64, "fmd_halo_tiled_size": i64}
 
 _lib = None
 

@@ -22,9 +22,9 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
 from ...runtime import ops
+from ...runtime.dp import bucketed_allreduce, world_size
 from ...runtime.engine import get_engine
 
 
@@ -69,7 +69,7 @@ class FusedTrainStep:
         self.N_train = num_train_timesteps
         self.grad_accum = max(1, int(grad_accum))
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = world_size(process_group)
         self.buckets = allreduce_buckets
         if objective == "ddpm":
             if ddpm_scheduler is None:
@@ -99,15 +99,7 @@ class FusedTrainStep:
         return self.loss
 
     def _allreduce(self):
-        if self.world <= 1:
-            return
-        g = self.flat.grad
-        n = g.numel()
-        per = -(-n // self.buckets)
-        for i in range(self.buckets):
-            sl = g[i * per:min(n, (i + 1) * per)]
-            if sl.numel():
-                dist.all_reduce(sl, op=dist.ReduceOp.SUM, group=self.pg)
+        bucketed_allreduce(self.flat.grad, self.buckets, self.pg)
 
     def step(self, clean, ldct, noise=None, t=None):
         """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss."""

@@ -96,6 +96,18 @@ class WeightCache:
             self._force.discard(key)
         return self._c[key][1]
 
+    def tiled(self, w: torch.Tensor, mode: int, Kpad=None, Cpad=None):
+        """Halo-kernel tiling of ``get(w, mode, ...)`` (csrc/conv_halo.hip)."""
+        base = self.get(w, mode, Kpad, Cpad)
+        key = (id(w), "tiled", mode, Kpad, Cpad)
+        ver = (w._version, w.data_ptr())
+        ent = self._c.get(key)
+        if ent is None or ent[0] != ver or key in self._force:
+            buf = ops.tile_weights(base, out=None if ent is None else ent[1])
+            self._c[key] = (ver, buf)
+            self._force.discard(key)
+        return self._c[key][1]
+
     def padded(self, v: torch.Tensor, n: int):
         key = (id(v), "pad", n)
         ver = (v._version, v.data_ptr())
@@ -167,8 +179,9 @@ class UNetEngine:
         _check_conv(conv, 3, stride, 1)
         Cin = x.C
         w = self.wc.get(conv.weight, 0, None, Cin)
+        wt = self.wc.tiled(conv.weight, 0, None, Cin) if stride == 1 else None
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
-                           bias=conv.bias, want_stats=True)
+                           bias=conv.bias, want_stats=True, wgt_tiled=wt)
         o = Act(out, st)
         if ctx.tape is not None:
             N, H, W, _ = x.t.shape
@@ -185,12 +198,19 @@ class UNetEngine:
                     g, acc = _gdest(x)
                     ops.conv(dy, Cin, wd, ks=4, stride=2, pad=1, out_hw_=(H, W), out=g, accumulate=bool(acc))
                 else:
-                    wd = self.wc.get(conv.weight, 1)
                     g, acc = _gdest(x)
-                    ops.conv(dy, Cin, wd, ks=3, stride=stride, pad=1, transposed=True, out_hw_=(H, W), out=g,
-                             accumulate=bool(acc))
+                    self.dgrad3x3(conv.weight, dy, Cin, H, W, stride=stride, out=g, accumulate=bool(acc))
             ctx.tape.append(bwd)
         return o
+
+    def dgrad3x3(self, w, dy, Cin, H, W, *, stride=1, Kpad=None, **kw):
+        """Data gradient of a 3x3 pad-1 conv.  Stride 1 = forward gather with flipped taps (so it runs on
+        the halo-tiled kernel); stride 2 = transposed gather."""
+        if stride == 1:
+            return ops.conv(dy, Cin, self.wc.get(w, 3, Kpad, None), ks=3, stride=1, pad=1, out_hw_=(H, W),
+                            wgt_tiled=self.wc.tiled(w, 3, Kpad, None), **kw)
+        return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,
+                        out_hw_=(H, W), **kw)
 
     def _wgrad_target(self, conv: Conv, Cin: int):
         """fp32 buffer the wgrad kernel writes: param.grad itself unless channels were padded."""
@@ -227,7 +247,8 @@ class UNetEngine:
         add = (not ss) and m.add_embedding_to_hidden
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         h, hst = ops.conv(x0.t, Cout, self.wc.get(c1.weight, 0), src1=x1.t if x1 else None, pro=(a1, b1, True),
-                          bias=c1.bias, bias_nc=eo if add else None, want_stats=True)
+                          bias=c1.bias, bias_nc=eo if add else None, want_stats=True,
+                          wgt_tiled=self.wc.tiled(c1.weight, 0))
         if ss:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
                                       emb_stride=2 * Cout, emb_mode=1)
@@ -242,9 +263,9 @@ class UNetEngine:
         else:
             _check_conv(sk.conv, 1, 1, 0)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=self.wc.get(sk.conv.weight, 0),
-                      bias2=sk.conv.bias)
+                      wgt2_tiled=self.wc.tiled(sk.conv.weight, 0), bias2=sk.conv.bias)
         out, ost = ops.conv(h, Cout, self.wc.get(c2.weight, 0), pro=(a2, b2, True), bias=c2.bias, want_stats=True,
-                            **kw)
+                            wgt_tiled=self.wc.tiled(c2.weight, 0), **kw)
         o = Act(out, ost)
         if ctx.tape is None:
             return o
@@ -259,8 +280,7 @@ class UNetEngine:
                 ops.wgrad(x0.t, dy, sc.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0, db=sc.bias.grad)
                 extra, _ = ops.conv(dy, Cin, self.wc.get(sc.weight, 1), ks=1, pad=0, transposed=True,
                                     out_hw_=(H, W))
-            dz2, s2 = ops.conv(dy, Cout, self.wc.get(c2.weight, 1), transposed=True, out_hw_=(H, W),
-                               ep=(h, None, a2, b2), want_stats=True)
+            dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, H, W, ep=(h, None, a2, b2), want_stats=True)
             demb = torch.empty_like(eo)
             if ss:
                 P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
@@ -276,8 +296,8 @@ class UNetEngine:
             ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
             del dz2
             ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True), db=c1.bias.grad)
-            dz1, s1 = ops.conv(dh, Cin, self.wc.get(c1.weight, 1), transposed=True, out_hw_=(H, W),
-                               ep=(x0.t, x1.t if x1 else None, a1, b1), want_stats=True)
+            dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, H, W, ep=(x0.t, x1.t if x1 else None, a1, b1),
+                                    want_stats=True)
             P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,
                                          g1.bias.grad)
             d0, acc0 = _gdest(x0)
@@ -357,8 +377,8 @@ class UNetEngine:
                 ops.wgrad(h.t, dpred, tmpw, pro=(a, b, True), db=tmpb, accumulate=False)
                 conv.weight.grad.add_(tmpw[:K])
                 conv.bias.grad.add_(tmpb[:K])
-                dz, s12 = ops.conv(dpred, Cc, self.wc.get(conv.weight, 1, Kp, None), transposed=True,
-                                   out_hw_=(H, W), ep=(h.t, None, a, b), want_stats=True)
+                dz, s12 = self.dgrad3x3(conv.weight, dpred, Cc, H, W, Kpad=Kp, ep=(h.t, None, a, b),
+                                        want_stats=True)
                 P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
                                           norm.weight.grad, norm.bias.grad)
                 g, acc = _gdest(h)

@@ -75,9 +75,10 @@ def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, be
     P = torch.empty((N, Ct), device=dev, dtype=F32)
     Q = torch.empty((N, Ct), device=dev, dtype=F32)
     R = torch.empty((N, Ct), device=dev, dtype=F32)
+    ws = torch.empty((N, Ct, 2), device=dev, dtype=F32)
     _lib.call("fmd_gn_bwd_prep", _p(s12.slab), s12.rows, N, HW, Ct, groups, _p(mr), _p(gamma), _p(beta), _p(emb),
               emb_stride, emb_mode, _p(P), _p(Q), _p(R), _p(dgamma), _p(dbeta), _p(demb), demb_stride,
-              _p(fwd.slab) if fwd else None, fwd.rows if fwd else 1, stream())
+              _p(fwd.slab) if fwd else None, fwd.rows if fwd else 1, _p(ws), stream())
     return P, Q, R
 
 
@@ -104,8 +105,9 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
 def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, transposed=False, out_hw_=None,
          pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
          out_f32=False,
-         accumulate=False, want_stats=False, ep=None, splits=None) -> Tuple[torch.Tensor, Optional[Stats]]:
-    """Implicit-GEMM conv (see csrc/conv.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``."""
+         accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
+         wgt2_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+    """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``."""
     _need_cuda(src0, "conv")
     N, Hs, Ws, C0 = src0.shape
     C1 = src1.shape[-1] if src1 is not None else 0
@@ -137,6 +139,18 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
     bpx = 256 if K <= 16 else 128
+    halo = (not force_generic and K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed
+            and Ho % 16 == 0 and Wo % 16 == 0 and N * (Ho // 16) * (Wo // 16) * -(-K // 128) >= 128
+            and (Ho == 2 * Hs if upsample else Ho == Hs))
+    d.force_generic = int(force_generic)
+    if halo:
+        splits = 1
+        bpx = 256
+        if wgt_tiled is None:
+            wgt_tiled = tile_weights(wgt)
+        if src2 is not None and wgt2_tiled is None:
+            wgt2_tiled = tile_weights(wgt2)
+        d.wgt_tiled, d.wgt2_tiled = _p(wgt_tiled), _p(wgt2_tiled)
     if splits is None:
         splits = _choose_splits(M, K, nk, bpx, bco)
     ws = None
@@ -199,6 +213,16 @@ def prep_weights(w: torch.Tensor, mode: int, Kpad: Optional[int] = None, Cpad: O
     if out is None:
         out = torch.empty(shape, device=w.device, dtype=BF16)
     _lib.call("fmd_prep_weights", _p(w.contiguous()), K, Cc, ks, mode, Kpad, Cpad, _p(out), stream())
+    return out
+
+
+def tile_weights(wk: torch.Tensor, out=None):
+    """bf16 kernel-layout weights [rows][T][cols] -> halo-kernel tiles (csrc/conv_halo.hip)."""
+    R, T, Cc = wk.shape
+    n = int(_lib.lib().fmd_halo_tiled_size(R, T, Cc))
+    if out is None:
+        out = torch.empty((n,), device=wk.device, dtype=BF16)
+    _lib.call("fmd_tile_weights_halo", _p(wk), R, T, Cc, _p(out), stream())
     return out
 
 

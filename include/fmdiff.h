@@ -68,9 +68,19 @@ typedef struct fmd_conv_desc {
   const float* ep_b;
   float* ws;                /* split-K workspace fp32 [splits][M][K] */
   int32_t splits;
+  int32_t force_generic;    /* 1: never take the halo-tiled 3x3 path (testing) */
+  const void* wgt_tiled;    /* wgt re-tiled by fmd_tile_weights_halo (enables the halo path) */
+  const void* wgt2_tiled;   /* wgt2 re-tiled likewise (T = 1) */
 } fmd_conv_desc;
 
+/* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the
+ * halo-tiled kernel (csrc/conv_halo.hip), everything else to the implicit GEMM (csrc/conv.hip). */
 int fmd_conv(const fmd_conv_desc* d, fmd_stream_t s);
+/* Halo-tiled 3x3 stride-1 conv; returns 1 (nothing launched) when the problem does not qualify. */
+int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t s);
+/* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, 64-channel chunk, tap) 16 KiB tiles. */
+int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);
+int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* out, fmd_stream_t s);
 
 /* Weight-gradient GEMM: dW[K][C][kh][kw] (+)= sum_p dY[p][K] x gather(src)[p][tap][C]
  * with the same gather/prologue as the forward; db[K] (+)= sum_p dY[p][K].
@@ -108,7 +118,7 @@ int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_t HW, int32
                     const float* mean_rstd, const float* gamma, const float* beta, const float* emb,
                     int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R,
                     float* dgamma, float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st,
-                    int32_t fwd_rows, fmd_stream_t s);
+                    int32_t fwd_rows, float* ws /* [N][C][2] scratch */, fmd_stream_t s);
 int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,
                      int32_t HW, const float* P, const float* Q, const float* R, const void* extra,
                      void* dx0, int32_t acc0, void* dx1, int32_t acc1, fmd_stream_t s);
