@@ -45,10 +45,12 @@ struct HArgs {
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
 };
 
-template <bool UP>
+// PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
+template <bool UP, int PRO>
 __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
   constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk
+  constexpr int LMAX = 4;                                  // staged 16-byte chunks per thread per step
   __shared__ __attribute__((aligned(16))) bf16r lds[2 * HBUF + 2 * WBUF];
   bf16r* hbuf = lds;
   bf16r* wbuf = lds + 2 * HBUF;
@@ -57,6 +59,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid >> 2, wpx = wid & 3;   // 2 x 4 waves: 64 couts x 4 pixel rows each
   const int l16 = lane & 15, lq = lane >> 4;
+  const int kc = tid & (KC - 1);             // every staged piece starts at a multiple of 8 chunks
 
   const int per_img = A.tiles_x * A.tiles_y;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -73,99 +76,97 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
   const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
   const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
-  const bool pro = d.pro_a != nullptr;
   const int nchunks = A.nchunk1 + A.nchunk2;
 
-  // ---- staging registers
-  u32x4 rw[2];           // two weight chunks per thread (16 KiB / 512 threads)
-  u32x4 rh[2];           // halo chunks per thread per step (main loop: <= 1, prologue / 1x1: <= 2)
-  int hidx[2];           // halo chunk index; -1 none; <= -2 zero chunk (-2 - index)
-  f32x4 ca[2][2], cb[2][2];  // GN affine coefficients of the staged chunks
-
-  auto wtile = [&](int s) -> const bf16r* {
+  // ---- weights: one contiguous 16 KiB tile per step, copied global -> LDS by the DMA path
+  auto load_w = [&](int s, int buf) {
+    const bf16r* src;
     if (s < A.nchunk1 * 9) {
-      const int chunk = s / 9, tap = s - (s / 9) * 9;
-      return A.wt + (((size_t)tco * A.nchunk1 + chunk) * 9 + tap) * WBUF;
+      const int chunk = s / 9, tap = s - chunk * 9;
+      src = A.wt + (((size_t)tco * A.nchunk1 + chunk) * 9 + tap) * WBUF;
+    } else {
+      src = A.wt2 + ((size_t)tco * A.nchunk2 + (s - A.nchunk1 * 9)) * WBUF;
     }
-    return A.wt2 + ((size_t)tco * A.nchunk2 + (s - A.nchunk1 * 9)) * WBUF;
-  };
-  auto load_w = [&](int s) {
-    const bf16r* src = wtile(s);
-    rw[0] = *(const u32x4*)(src + tid * 8);
-    rw[1] = *(const u32x4*)(src + (tid + NT) * 8);
-  };
-  auto store_w = [&](int buf) {
-    *(u32x4*)(wbuf + buf * WBUF + tid * 8) = rw[0];
-    *(u32x4*)(wbuf + buf * WBUF + (tid + NT) * 8) = rw[1];
+    bf16r* dst = wbuf + buf * WBUF + wid * 64 * 8;
+    __builtin_amdgcn_global_load_lds((const void*)(src + tid * 8), (__attribute__((address_space(3))) void*)dst,
+                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + (tid + NT) * 8),
+                                     (__attribute__((address_space(3))) void*)(dst + NT * 8), 16, 0, 0);
   };
 
-  // halo chunk h of `chunk`: kc = h % KC (fastest: one position's 128 B are read by 8 lanes), pos = h / KC
-  auto load_h = [&](int chunk, int lo, int hi, int per) {
-    const bool seg2 = chunk >= A.nchunk1;
-    const int cbase = (seg2 ? chunk - A.nchunk1 : chunk) * BK;
+  // ---- halo staging: branch-free loads (clamped addresses), masked LDS stores after the MFMAs
+  u32x4 rh[LMAX];
+  int hoff[LMAX];            // LDS element offset; -1: nothing to store; bit 30: store zeros (padding)
+  float ca[8], cb[8];        // GN affine of this thread's 8 channels of the chunk being staged
+
+  auto load_coef = [&](int chunk) {
+    if (PRO == 0 || chunk >= A.nchunk1) return;
+    const int c = min(chunk * BK + kc * 8, A.C - 8 < 0 ? 0 : A.C - 8);
+    const f32x4* pa = (const f32x4*)(d.pro_a + (size_t)n * A.C + c);
+    const f32x4* pb = (const f32x4*)(d.pro_b + (size_t)n * A.C + c);
+    const f32x4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int e = 0; e < 4; ++e) { ca[e] = a0[e]; ca[4 + e] = a1[e]; cb[e] = b0[e]; cb[4 + e] = b1[e]; }
+  };
+
+  // stage chunk-pieces [lo, hi) of `chunk`, cnt (wave-uniform) loads per thread
+  auto load_h = [&](int chunk, int lo, int hi, int cnt) {
+    const bool seg2 = chunk >= A.nchunk1;
+    const int c = (seg2 ? chunk - A.nchunk1 : chunk) * BK + kc * 8;
+#pragma unroll
+    for (int k = 0; k < LMAX; ++k) {
+      if (k >= cnt) break;
       const int h = lo + tid + k * NT;
-      hidx[k] = -1;
-      rh[k] = u32x4{0u, 0u, 0u, 0u};
-      if (k >= per || h >= hi) continue;
-      const int kc = h & (KC - 1), pos = h >> 3;
-      const int c = cbase + kc * 8;
+      const bool act = h < hi;
+      const int pos = (act ? h : lo) >> 3;
+      int lpos, y, x;
+      const bf16r* ptr;
+      bool valid;
       if (!seg2) {
         const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-        const int y = hy0 + py, x = hx0 + px;
-        if (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws && c < A.C) {
-          const size_t pix = ((size_t)n * d.Hs + y) * d.Ws + x;
-          rh[k] = *(const u32x4*)((c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0));
-          hidx[k] = h;
-          if (pro) {
-            const float* pa = d.pro_a + (size_t)n * A.C + c;
-            const float* pb = d.pro_b + (size_t)n * A.C + c;
-            ca[k][0] = *(const f32x4*)pa; ca[k][1] = *(const f32x4*)(pa + 4);
-            cb[k][0] = *(const f32x4*)pb; cb[k][1] = *(const f32x4*)(pb + 4);
-          }
-        } else {
-          hidx[k] = -2 - h;
-        }
-      } else {
-        const int py = pos / (TW + 2), px = pos - (pos / (TW + 2)) * (TW + 2);
-        const int y = ty0 - 1 + py, x = tx0 - 1 + px;
-        if (y >= 0 && y < d.Ho && x >= 0 && x < d.Wo && c < A.C23) {
-          const size_t pix = ((size_t)n * d.Ho + y) * d.Wo + x;
-          rh[k] = *(const u32x4*)((c < d.C2) ? s2 + pix * d.C2 + c : s3 + pix * d.C3 + (c - d.C2));
-          hidx[k] = h;
-        } else {
-          hidx[k] = -2 - h;
-        }
+        y = hy0 + py;
+        x = hx0 + px;
+        lpos = pos;
+        valid = y >= 0 && y < d.Hs && x >= 0 && x < d.Ws && c < A.C;
+        const size_t pix = ((size_t)n * d.Hs + (valid ? y : 0)) * d.Ws + (valid ? x : 0);
+        ptr = !valid ? s0 : (c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0);
+      } else {   // 1x1 segment: only the 16x16 interior, stored at its halo position
+        const int py = pos >> 4, px = pos & 15;
+        y = ty0 + py;
+        x = tx0 + px;
+        lpos = (py + 1) * (TW + 2) + px + 1;
+        valid = c < A.C23;
+        const size_t pix = ((size_t)n * d.Ho + y) * d.Wo + x;
+        ptr = !valid ? s2 : (c < d.C2) ? s2 + pix * d.C2 + c : s3 + pix * d.C3 + (c - d.C2);
       }
+      rh[k] = *(const u32x4*)ptr;
+      hoff[k] = act ? ((kc * HPAD + lpos) * 8) | (valid ? 0 : (1 << 30)) : -1;
     }
   };
-  auto store_h = [&](int buf, bool transform) {
+  auto store_h = [&](int buf, int cnt, bool transform) {
+    bf16r* hb = hbuf + buf * HBUF;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      int h = hidx[k];
-      if (h == -1) continue;
-      const bool valid = h >= 0;
-      if (!valid) h = -2 - h;
-      const int kc = h & (KC - 1), pos = h >> 3;
+    for (int k = 0; k < LMAX; ++k) {
+      if (k >= cnt) break;
       u32x4 v = rh[k];
-      if (valid && transform) {
-        const float av[8] = {ca[k][0][0], ca[k][0][1], ca[k][0][2], ca[k][0][3],
-                             ca[k][1][0], ca[k][1][1], ca[k][1][2], ca[k][1][3]};
-        const float bv[8] = {cb[k][0][0], cb[k][0][1], cb[k][0][2], cb[k][0][3],
-                             cb[k][1][0], cb[k][1][1], cb[k][1][2], cb[k][1][3]};
-        u32x4 o;
+      if (PRO != 0 && transform) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float lo = bf_lo(v[e]) * av[2 * e] + bv[2 * e];
-          float hi = bf_hi(v[e]) * av[2 * e + 1] + bv[2 * e + 1];
-          if (d.pro_silu) { lo = siluf_(lo); hi = siluf_(hi); }
-          o[e] = pack2(lo, hi);
+          float lo = bf_lo(v[e]) * ca[2 * e] + cb[2 * e];
+          float hi = bf_hi(v[e]) * ca[2 * e + 1] + cb[2 * e + 1];
+          if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
+          v[e] = pack2(lo, hi);
         }
-        v = o;
       }
-      *(u32x4*)(hbuf + buf * HBUF + (kc * HPAD + pos) * 8) = v;
+      const int o = hoff[k];
+      if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
+      if (o >= 0) *(u32x4*)(hb + (o & ~(1 << 30))) = v;
     }
+  };
+  // piece of the next chunk staged during one step of the current one (multiple of 8 chunks)
+  auto piece = [&](int next_chunk, int nt, int& tot) {
+    tot = KC * (next_chunk >= A.nchunk1 ? TH * TW : HPOS);
+    return ((tot + nt - 1) / nt + 7) & ~7;
   };
 
   f32x4 acc[4][4];
@@ -204,14 +205,14 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
 
   // ---- prologue: full halo of chunk 0 + weights of step 0
   {
-    const bool s2c = A.nchunk1 == 0;
-    const int tot = KC * (s2c ? HALO : HPOS);
-    for (int lo = 0; lo < tot; lo += 2 * NT) {
-      load_h(0, lo, tot, 2);
-      store_h(0, pro && !s2c);
+    int tot;
+    piece(0, 1, tot);
+    load_coef(0);
+    load_w(0, 0);
+    for (int lo = 0; lo < tot; lo += LMAX * NT) {
+      load_h(0, lo, tot, LMAX);
+      store_h(0, LMAX, A.nchunk1 > 0);
     }
-    load_w(0);
-    store_w(0);
     __syncthreads();
   }
 
@@ -222,17 +223,18 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
     const int nt = seg2 ? 1 : 9;
     const int t_in = seg2 ? 0 : tap;
     const bool more = chunk + 1 < nchunks;
-    const bool nseg2 = chunk + 1 >= A.nchunk1;
+    int cnt = 0;
     if (more) {
-      const int tot = KC * (nseg2 ? HALO : HPOS);
-      const int lo = (int)((long)tot * t_in / nt), hi = (int)((long)tot * (t_in + 1) / nt);
-      load_h(chunk + 1, lo, hi, 2);
+      int tot;
+      const int pc = piece(chunk + 1, nt, tot);
+      const int lo = t_in * pc, hi = min(tot, lo + pc);
+      cnt = lo < hi ? (hi - lo + NT - 1) / NT : 0;
+      if (t_in == 0) load_coef(chunk + 1);
+      load_h(chunk + 1, lo, hi, cnt);
     }
-    const bool wnext = s + 1 < A.nsteps;
-    if (wnext) load_w(s + 1);
+    if (s + 1 < A.nsteps) load_w(s + 1, (s + 1) & 1);
     compute(chunk, tap, seg2, s & 1);
-    if (wnext) store_w((s + 1) & 1);
-    if (more) store_h((chunk + 1) & 1, pro && !nseg2);
+    if (cnt) store_h((chunk + 1) & 1, cnt, chunk + 1 < A.nchunk1);
     __syncthreads();
   }
 
@@ -388,10 +390,18 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt2 = (const bf16r*)d->wgt2_tiled;
   const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;   // too few tiles to fill the chip: the split-K implicit GEMM wins
-  if (d->upsample)
-    hipLaunchKernelGGL(conv3x3_halo<true>, dim3(nwg), dim3(NT), 0, (hipStream_t)stream, A);
-  else
-    hipLaunchKernelGGL(conv3x3_halo<false>, dim3(nwg), dim3(NT), 0, (hipStream_t)stream, A);
+  const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
+  const dim3 g(nwg), blk(NT);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->upsample) {
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<true, 0>), g, blk, 0, st, A);
+  } else {
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<false, 0>), g, blk, 0, st, A);
+  }
   return (int)hipGetLastError();
 }
 

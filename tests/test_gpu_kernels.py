@@ -261,33 +261,40 @@ def test_adamw_matches_torch():
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("case", ["plain", "pro_concat_stats", "upsample", "skip_seg2", "dgrad_ep", "k64"])
+@pytest.mark.parametrize("case", ["plain", "pro_concat_stats", "upsample", "skip_seg2", "skip_wide", "dgrad_ep",
+                                  "k64", "k256_pro_nosilu"])
 def test_halo_conv_matches_generic(case):
-    """csrc/conv_halo.hip (16x16 tiles, halo staged once per chunk) vs the per-tap implicit GEMM."""
+    """csrc/conv_halo.hip (16x16 tiles, halo staged once per chunk) vs the per-tap implicit GEMM.
+
+    N=8 at 64x64 = 128 tiles: the smallest problem the halo path accepts (fmd_conv_halo), so every case runs it."""
     O = ops()
-    N, H, W = 2, 64, 64
+    N, H, W = 8, 64, 64
     C0, C1, K = 64, 0, 128
     if case == "pro_concat_stats":
         C1 = 96
     if case == "k64":
         K = 64
-        N = 8
+    if case == "k256_pro_nosilu":
+        C0, K = 192, 256
     Hs, Ws = (H // 2, W // 2) if case == "upsample" else (H, W)
     x0 = _rand_nhwc(N, Hs, Ws, C0, 21).to(DEV)
     x1 = _rand_nhwc(N, Hs, Ws, C1, 22).to(DEV) if C1 else None
     w = O.prep_weights(_w(K, C0 + C1, 3, 23).to(DEV), 0)
     kw = dict(bias=(torch.randn(K) * 0.1).to(DEV))
-    if case in ("pro_concat_stats", "upsample"):
-        kw["pro"] = ((torch.rand(N, C0 + C1) + 0.5).to(DEV), (torch.randn(N, C0 + C1) * 0.2).to(DEV), True)
-    if case == "skip_seg2":
-        s2 = _rand_nhwc(N, H, W, 96, 24).to(DEV)
-        s3 = _rand_nhwc(N, H, W, 32, 25).to(DEV)
-        kw.update(src2=s2, src3=s3, wgt2=O.prep_weights(_w(K, 128, 1, 26).to(DEV), 0),
+    if case in ("pro_concat_stats", "upsample", "skip_wide", "k256_pro_nosilu"):
+        kw["pro"] = ((torch.rand(N, C0 + C1) + 0.5).to(DEV), (torch.randn(N, C0 + C1) * 0.2).to(DEV),
+                     case != "k256_pro_nosilu")
+    if case in ("skip_seg2", "skip_wide"):
+        c2, c3 = (96, 32) if case == "skip_seg2" else (256, 128)
+        s2 = _rand_nhwc(N, H, W, c2, 24).to(DEV)
+        s3 = _rand_nhwc(N, H, W, c3, 25).to(DEV)
+        kw.update(src2=s2, src3=s3, wgt2=O.prep_weights(_w(K, c2 + c3, 1, 26).to(DEV), 0),
                   bias2=(torch.randn(K) * 0.1).to(DEV), resid=None)
     if case == "dgrad_ep":
         xe = _rand_nhwc(N, H, W, K, 27).to(DEV)
         kw["ep"] = (xe, None, (torch.rand(N, K) + 0.5).to(DEV), (torch.randn(N, K) * 0.2).to(DEV))
     want = case in ("pro_concat_stats", "dgrad_ep", "upsample")
+    assert O.halo_eligible(N, Hs, H, W, K, upsample=case == "upsample")
     a, sa = O.conv(x0, K, w, src1=x1, upsample=case == "upsample", want_stats=want, **kw)
     b, sb = O.conv(x0, K, w, src1=x1, upsample=case == "upsample", want_stats=want, force_generic=True, **kw)
     torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item())

@@ -1,0 +1,195 @@
+"""CPU tests of the host side: scheduler bookkeeping (bit-exact vs the oracle), the scheduler registry,
+the model factory's state_dict surface, and the data-parallel gradient exchange over gloo (world 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fmdiff.models.generators import DiffusionUNetFactory
+from fmdiff.pipelines import schedulers as FS
+from fmdiff.pipelines import utils as PU
+from fmdiff.runtime import dp
+from oracle import schedulers as OS
+from oracle import spec as S
+from oracle import train_step as OT
+from oracle import unet as U
+
+MODEL_CASES = ["ldct_fm_test", "mnist_ddpm_diffusers", "mnist_fm_compvis", "ldct_fm_b64", "ldct_fm_diffusers_b64"]
+
+
+# ------------------------------------------------------------------ schedulers (host tables)
+@pytest.mark.parametrize("n", [1, 2, 10, 50, 999, 1000])
+def test_flow_match_tables_bit_exact(n):
+    a, o = FS.FlowMatchEulerDiscreteScheduler(1000), OS.FlowMatchEuler(1000)
+    assert torch.equal(a.timesteps, o.timesteps) and torch.equal(a.sigmas, o.sigmas)
+    assert a.sigma_min == o.sigma_min == 0.0010000000474974513
+    a.set_timesteps(n)
+    o.set_timesteps(n)
+    assert a.timesteps.dtype == torch.float32
+    assert torch.equal(a.timesteps, o.timesteps) and torch.equal(a.sigmas, o.sigmas)
+    for t in a.timesteps[:3]:
+        assert a.index_for_timestep(t) == o.index_for_timestep(t)
+
+
+def test_flow_match_kat():
+    s = FS.FlowMatchEulerDiscreteScheduler(1000)
+    s.set_timesteps(50)
+    assert s.timesteps[:3].tolist() == [1000.0, 979.6122436523438, 959.2244873046875]
+    assert s.timesteps[-1].item() == 1.0 and s.sigmas[-1].item() == 0.0 and len(s.sigmas) == 51
+
+
+@pytest.mark.parametrize("spacing", ["leading", "linspace", "trailing"])
+@pytest.mark.parametrize("n", [1, 7, 50, 1000])
+def test_ddpm_ddim_tables_bit_exact(spacing, n):
+    kw = dict(beta_start=0.00085, beta_end=0.012, timestep_spacing=spacing)
+    a, o = FS.DDPMScheduler(1000, **kw), OS.DDPM(1000, **kw)
+    assert torch.equal(a.alphas_cumprod, o.alphas_cumprod)
+    a.set_timesteps(n)
+    o.set_timesteps(n)
+    assert a.timesteps.dtype == torch.int64 and torch.equal(a.timesteps, o.timesteps)
+    for t in a.timesteps[:4].tolist():
+        c = a.coefficients(t)
+        r = o.coefficients(t)
+        want = torch.stack([r["sqrt_b"], r["sqrt_a"], r["c_x0"], r["c_xt"],
+                            r["std"] if t > 0 else torch.tensor(0.0)]).float()
+        assert torch.equal(c[:5], want)
+
+
+def test_ddpm_leading_kat():
+    s = FS.DDPMScheduler(1000)
+    s.set_timesteps(50)
+    assert s.timesteps.tolist() == list(range(980, -1, -20))
+
+
+@pytest.mark.parametrize("sched", ["linear", "scaled_linear", "squaredcos_cap_v2"])
+def test_beta_schedules(sched):
+    a, o = FS.DDPMScheduler(1000, beta_schedule=sched), OS.DDPM(1000, beta_schedule=sched)
+    assert torch.equal(a.betas, o.betas)
+
+
+# ------------------------------------------------------------------ registry / loop host logic
+def test_build_scheduler_and_overrides():
+    s, n = PU.build_scheduler({"name": "flow_match_euler", "params": {"shift": 1.0, "bogus": 3}}, {})
+    assert isinstance(s, FS.FlowMatchEulerDiscreteScheduler) and n == 1000
+    s, n = PU.build_scheduler({}, {"scheduler": "DDIM", "num_train_timesteps": 500, "num_inference_steps": 20})
+    assert isinstance(s, FS.DDIMScheduler) and s.config.num_train_timesteps == 500 and n == 20
+    s, _ = PU.build_scheduler(None, None)
+    assert isinstance(s, FS.DDPMScheduler)
+    with pytest.raises(ValueError, match="Unknown scheduler"):
+        PU.build_scheduler({"name": "euler_a"}, {})
+    assert PU.resolve_scheduler_override(None) is None
+    assert PU.resolve_scheduler_override("  ") is None
+    assert PU.resolve_scheduler_override("flowmatch") == {"name": "flow_match_euler"}
+    assert PU.resolve_scheduler_override("dpmsolver++") == {
+        "name": "dpm_multistep", "params": {"solver_order": 2, "algorithm_type": "dpmsolver++"}}
+    with pytest.raises(ValueError, match="Unknown scheduler override"):
+        PU.resolve_scheduler_override("heun")
+    assert set(PU.SCHEDULER_REGISTRY) == {"ddpm", "ddim", "dpm_multistep", "dpm_sde", "unipc", "flow_match_euler",
+                                          "flowmatch"}
+
+
+def test_select_timesteps():
+    ts = torch.tensor([980, 960, 500, 20, 0])
+    assert PU.select_timesteps(ts, start_step=500).tolist() == [500, 20, 0]
+    assert PU.select_timesteps(ts, last_n_steps=2).tolist() == [20, 0]
+    assert PU.select_timesteps(ts, 960, 10).tolist() == [960, 500, 20, 0]
+    with pytest.raises(ValueError):
+        PU.select_timesteps(ts, start_step=-1)
+    with pytest.raises(ValueError):
+        PU.select_timesteps(ts, last_n_steps=0)
+    with pytest.raises(ValueError, match="No timesteps"):
+        PU.select_timesteps(torch.tensor([980, 960]), start_step=10)
+
+
+def test_align_and_normalize_conditioning():
+    c = torch.arange(2 * 1 * 2 * 2, dtype=torch.float32).view(2, 1, 2, 2)
+    assert PU._align_conditioning(c, 5).shape[0] == 5
+    assert torch.equal(PU._align_conditioning(c, 5)[2], c[0])
+    z = PU.normalize_latent_conditioning(c, "standardize")
+    assert torch.allclose(z.mean(dim=(2, 3)), torch.zeros(2, 1), atol=1e-6)
+    m = PU.normalize_latent_conditioning(c, "minmax")
+    assert m.amax().item() <= 1.0 and m.amin().item() >= 0.0
+    assert PU.normalize_latent_conditioning(c, "off") is c
+    with pytest.raises(ValueError):
+        PU.normalize_latent_conditioning(c, "zscore")
+
+
+# ------------------------------------------------------------------ factory surface
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_factory_state_dict_matches_reference_order(golden, name):
+    _, M = golden
+    m = M[name]
+    tr = m["training"]
+    spec = S.derive_spec(m["unet"], tr["conditioning"], tr["channels"] or 1)
+    model = DiffusionUNetFactory().build(m["unet"], tr["conditioning"], tr["channels"] or 1)
+    got = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
+    want = list(U.param_shapes(spec).items())
+    assert got == want
+
+
+# ------------------------------------------------------------------ data parallel (gloo, world 2)
+def test_bucket_bounds():
+    assert dp.bucket_bounds(10, 4) == [(0, 3), (3, 6), (6, 9), (9, 10)]
+    assert dp.bucket_bounds(3, 8) == [(0, 1), (1, 2), (2, 3)]
+    assert dp.bucket_bounds(0, 4) == []
+    b = dp.bucket_bounds(113_008_257, 4)
+    assert b[0][0] == 0 and b[-1][1] == 113_008_257 and all(x[1] == y[0] for x, y in zip(b, b[1:]))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, meta, tensors, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        spec = S.derive_spec(meta["unet"], meta["training"]["conditioning"], meta["training"]["channels"] or 1)
+        sd = {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, meta["seed"]).items()}
+        B = tensors["clean"].shape[0]
+        sl = slice(rank * B // world, (rank + 1) * B // world)        # DistributedSampler-style shard
+        _, sc = OT.fm_loss(sd, spec, tensors["clean"][sl], tensors["ldct"][sl], tensors["noise"][sl],
+                           tensors["t"][sl], meta["num_train_timesteps"])
+        sc.backward()
+        flat = torch.cat([p.grad.reshape(-1) for p in sd.values()])
+        dp.bucketed_allreduce(flat, buckets=3)
+        flat /= world                                                     # grad_scale folded into AdamW on GPU
+        if rank == 0:
+            q.put(flat)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_allreduce_equals_global_batch(golden):
+    """N-rank step with the bucketed all-reduce == one process on the concatenated batch."""
+    T, M = golden
+    meta = M["fm_step"]
+    tensors = {k: T[f"fm_step/{k}"] for k in ("clean", "ldct", "noise", "t")}
+    if tensors["clean"].shape[0] % 2:
+        pytest.skip("fixture batch not divisible by 2")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, meta, tensors, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    spec = S.derive_spec(meta["unet"], meta["training"]["conditioning"], meta["training"]["channels"] or 1)
+    sd = {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, meta["seed"]).items()}
+    _, sc = OT.fm_loss(sd, spec, tensors["clean"], tensors["ldct"], tensors["noise"], tensors["t"],
+                       meta["num_train_timesteps"])
+    sc.backward()
+    want = torch.cat([p.grad.reshape(-1) for p in sd.values()])
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-6)
