@@ -25,7 +25,8 @@ FMD_DEV unsigned int f2bf(float f) {
 }
 FMD_DEV unsigned int pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
 
-FMD_DEV float sigmoidf_(float z) { return 1.0f / (1.0f + __expf(-z)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp): no IEEE division sequence in the hot prologues
+FMD_DEV float sigmoidf_(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }
 FMD_DEV float siluf_(float z) { return z * sigmoidf_(z); }
 // d silu / dz
 FMD_DEV float silu_grad(float z) {

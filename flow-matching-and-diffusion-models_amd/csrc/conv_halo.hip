@@ -40,18 +40,25 @@ struct HArgs {
   int C, C23;
   int tiles_x, tiles_y, ntc;
   int nchunk1, nchunk2;   // main / 1x1-segment chunks
-  int nsteps;
+  int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
   const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
+  unsigned long long* trace;   // debug: s_memtime per phase for the first TRACE_WG workgroups, else null
 };
+
+constexpr int TRACE_WG = 16, TRACE_STEPS = 40, TRACE_PH = 4;
+static unsigned long long* g_trace = nullptr;
 
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
 template <bool UP, int PRO>
 __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
   constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk
-  constexpr int LMAX = 4;                                  // staged 16-byte chunks per thread per step
-  __shared__ __attribute__((aligned(16))) bf16r lds[2 * HBUF + 2 * WBUF];
+  constexpr int TOT1 = KC * HPOS;                          // 16-byte pieces of a main chunk
+  constexpr int PC1 = ((TOT1 + 3) / 4 + 7) & ~7;           // pieces staged per step (4 staging steps per chunk)
+  constexpr int LPT = (PC1 + NT - 1) / NT;                 // loads per thread per staging step (2 | 1)
+  constexpr int LPRO = (TOT1 + NT - 1) / NT;               // loads per thread for the prologue's full chunk
+  __shared__ __attribute__((aligned(16))) bf16r lds[2 * HBUF + 4 * WBUF];   // 2 halo + 2x2 weight tiles
   bf16r* hbuf = lds;
   bf16r* wbuf = lds + 2 * HBUF;
 
@@ -59,7 +66,8 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid >> 2, wpx = wid & 3;   // 2 x 4 waves: 64 couts x 4 pixel rows each
   const int l16 = lane & 15, lq = lane >> 4;
-  const int kc = tid & (KC - 1);             // every staged piece starts at a multiple of 8 chunks
+  const int kc = tid & (KC - 1);             // staged pieces start at multiples of 8: the 16-byte channel group is fixed
+  const int tp = tid >> 3;                   // position of this thread within a piece
 
   const int per_img = A.tiles_x * A.tiles_y;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -78,105 +86,95 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
   const int nchunks = A.nchunk1 + A.nchunk2;
 
+  // pixel index of every halo position of a main chunk (-1: zero padding); 32-bit offsets
+  // (N*H*W*C < 2^31 is checked on the host).  Written once, read by the stagers of every chunk.
+  __shared__ int pixtab[HPOS];
+  for (int pos = tid; pos < HPOS; pos += NT) {
+    const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
+    const int y = hy0 + py, x = hx0 + px;
+    pixtab[pos] = (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? (n * d.Hs + y) * d.Ws + x : -1;
+  }
+  __syncthreads();
+
   // ---- weights: one contiguous 16 KiB tile per step, copied global -> LDS by the DMA path
-  auto load_w = [&](int s, int buf) {
+  // slot = tap index over the whole reduction: 9 per 3x3 chunk, then 1 per 1x1 chunk; wtile = 0..3
+  auto load_w = [&](int slot, int wtile) {
     const bf16r* src;
-    if (s < A.nchunk1 * 9) {
-      const int chunk = s / 9, tap = s - chunk * 9;
-      src = A.wt + (((size_t)tco * A.nchunk1 + chunk) * 9 + tap) * WBUF;
+    if (slot < A.nchunk1 * 9) {
+      src = A.wt + ((size_t)tco * A.nchunk1 * 9 + slot) * WBUF;
     } else {
-      src = A.wt2 + ((size_t)tco * A.nchunk2 + (s - A.nchunk1 * 9)) * WBUF;
+      src = A.wt2 + ((size_t)tco * A.nchunk2 + (slot - A.nchunk1 * 9)) * WBUF;
     }
-    bf16r* dst = wbuf + buf * WBUF + wid * 64 * 8;
+    bf16r* dst = wbuf + wtile * WBUF + wid * 64 * 8;
     __builtin_amdgcn_global_load_lds((const void*)(src + tid * 8), (__attribute__((address_space(3))) void*)dst,
                                      16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(src + (tid + NT) * 8),
                                      (__attribute__((address_space(3))) void*)(dst + NT * 8), 16, 0, 0);
   };
 
-  // ---- halo staging: branch-free loads (clamped addresses), masked LDS stores after the MFMAs
+  // ---- halo staging through registers (the GN/SiLU transform happens between load and LDS store)
+  constexpr int LMAX = 9;
   u32x4 rh[LMAX];
-  int hoff[LMAX];            // LDS element offset; -1: nothing to store; bit 30: store zeros (padding)
+  int hoff[LMAX];            // LDS element offset; -1: no store; bit 30: store zeros (padding)
   float ca[8], cb[8];        // GN affine of this thread's 8 channels of the chunk being staged
+  const bf16r* cbase = s0;   // this thread's channel group of the chunk being staged
+  int cs = 0;                // its pixel stride
+  bool cok = false;
 
-  auto load_coef = [&](int chunk) {
-    if (PRO == 0 || chunk >= A.nchunk1) return;
-    const int c = min(chunk * BK + kc * 8, A.C - 8 < 0 ? 0 : A.C - 8);
-    const f32x4* pa = (const f32x4*)(d.pro_a + (size_t)n * A.C + c);
-    const f32x4* pb = (const f32x4*)(d.pro_b + (size_t)n * A.C + c);
-    const f32x4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+  auto setup = [&](int chunk) {
+    if (chunk < A.nchunk1) {
+      const int c = chunk * BK + kc * 8;
+      cok = c < A.C;
+      cbase = !cok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
+      cs = (c < d.C0) ? d.C0 : d.C1;
+      if (PRO != 0) {
+        const int cc = cok ? c : 0;
+        const f32x4* pa = (const f32x4*)(d.pro_a + (size_t)n * A.C + cc);
+        const f32x4* pb = (const f32x4*)(d.pro_b + (size_t)n * A.C + cc);
+        const f32x4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { ca[e] = a0[e]; ca[4 + e] = a1[e]; cb[e] = b0[e]; cb[4 + e] = b1[e]; }
-  };
-
-  // stage chunk-pieces [lo, hi) of `chunk`, cnt (wave-uniform) loads per thread
-  auto load_h = [&](int chunk, int lo, int hi, int cnt) {
-    const bool seg2 = chunk >= A.nchunk1;
-    const int c = (seg2 ? chunk - A.nchunk1 : chunk) * BK + kc * 8;
-#pragma unroll
-    for (int k = 0; k < LMAX; ++k) {
-      if (k >= cnt) break;
-      const int h = lo + tid + k * NT;
-      const bool act = h < hi;
-      const int pos = (act ? h : lo) >> 3;
-      int lpos, y, x;
-      const bf16r* ptr;
-      bool valid;
-      if (!seg2) {
-        const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-        y = hy0 + py;
-        x = hx0 + px;
-        lpos = pos;
-        valid = y >= 0 && y < d.Hs && x >= 0 && x < d.Ws && c < A.C;
-        const size_t pix = ((size_t)n * d.Hs + (valid ? y : 0)) * d.Ws + (valid ? x : 0);
-        ptr = !valid ? s0 : (c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0);
-      } else {   // 1x1 segment: only the 16x16 interior, stored at its halo position
-        const int py = pos >> 4, px = pos & 15;
-        y = ty0 + py;
-        x = tx0 + px;
-        lpos = (py + 1) * (TW + 2) + px + 1;
-        valid = c < A.C23;
-        const size_t pix = ((size_t)n * d.Ho + y) * d.Wo + x;
-        ptr = !valid ? s2 : (c < d.C2) ? s2 + pix * d.C2 + c : s3 + pix * d.C3 + (c - d.C2);
+        for (int e = 0; e < 4; ++e) { ca[e] = a0[e]; ca[4 + e] = a1[e]; cb[e] = b0[e]; cb[4 + e] = b1[e]; }
       }
-      rh[k] = *(const u32x4*)ptr;
-      hoff[k] = act ? ((kc * HPAD + lpos) * 8) | (valid ? 0 : (1 << 30)) : -1;
+    } else {
+      const int c = (chunk - A.nchunk1) * BK + kc * 8;
+      cok = c < A.C23;
+      cbase = !cok ? s2 : (c < d.C2) ? s2 + c : s3 + (c - d.C2);
+      cs = (c < d.C2) ? d.C2 : d.C3;
     }
   };
-  auto store_h = [&](int buf, int cnt, bool transform) {
-    bf16r* hb = hbuf + buf * HBUF;
-#pragma unroll
-    for (int k = 0; k < LMAX; ++k) {
-      if (k >= cnt) break;
-      u32x4 v = rh[k];
-      if (PRO != 0 && transform) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float lo = bf_lo(v[e]) * ca[2 * e] + cb[2 * e];
-          float hi = bf_hi(v[e]) * ca[2 * e + 1] + cb[2 * e + 1];
-          if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-          v[e] = pack2(lo, hi);
-        }
-      }
-      const int o = hoff[k];
-      if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
-      if (o >= 0) *(u32x4*)(hb + (o & ~(1 << 30))) = v;
-    }
+  auto load_main = [&](int k, int h, bool act) {   // h: piece index (multiple-of-8 base + tid)
+    const int pos = act ? h >> 3 : 0;
+    const int pix = pixtab[pos];
+    const bool valid = pix >= 0 && cok;
+    rh[k] = *(const u32x4*)(cbase + (valid ? pix : 0) * cs);
+    hoff[k] = !act ? -1 : ((kc * HPAD + pos) * 8) | (valid ? 0 : (1 << 30));
   };
-  // piece of the next chunk staged during one step of the current one (multiple of 8 chunks)
-  auto piece = [&](int next_chunk, int nt, int& tot) {
-    tot = KC * (next_chunk >= A.nchunk1 ? TH * TW : HPOS);
-    return ((tot + nt - 1) / nt + 7) & ~7;
+  auto load_seg2 = [&](int k, int p) {   // p: interior position 0..255
+    const int py = p >> 4, px = p & 15;
+    const int pix = (n * d.Ho + ty0 + py) * d.Wo + tx0 + px;
+    rh[k] = *(const u32x4*)(cbase + (cok ? pix : 0) * cs);
+    hoff[k] = ((kc * HPAD + (py + 1) * (TW + 2) + px + 1) * 8) | (cok ? 0 : (1 << 30));
+  };
+  auto store = [&](int buf, int k, bool transform) {
+    u32x4 v = rh[k];
+    if (PRO != 0 && transform) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = bf_lo(v[e]) * ca[2 * e] + cb[2 * e];
+        float hi = bf_hi(v[e]) * ca[2 * e + 1] + cb[2 * e + 1];
+        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
+        v[e] = pack2(lo, hi);
+      }
+    }
+    const int o = hoff[k];
+    if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
+    if (o >= 0) *(u32x4*)(hbuf + buf * HBUF + (o & ~(1 << 30))) = v;
   };
 
   f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int chunk, int tap, bool seg2, int wb_i) {
-    const bf16r* hb = hbuf + (chunk & 1) * HBUF;
+  auto compute = [&](int hb_i, int tap, bool seg2, int wb_i) {
+    const bf16r* hb = hbuf + hb_i * HBUF;
     const bf16r* wb = wbuf + wb_i * WBUF;
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
 #pragma unroll
@@ -203,41 +201,106 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
     }
   };
 
-  // ---- prologue: full halo of chunk 0 + weights of step 0
-  {
-    int tot;
-    piece(0, 1, tot);
-    load_coef(0);
-    load_w(0, 0);
-    for (int lo = 0; lo < tot; lo += LMAX * NT) {
-      load_h(0, lo, tot, LMAX);
-      store_h(0, LMAX, A.nchunk1 > 0);
-    }
-    __syncthreads();
-  }
+  const bool tr = A.trace != nullptr && blockIdx.x < TRACE_WG && lane == 0;
+  auto mark = [&](int step, int ph) {
+    if (tr && step < TRACE_STEPS)
+      A.trace[((blockIdx.x * 8 + wid) * TRACE_STEPS + step) * TRACE_PH + ph] = __builtin_amdgcn_s_memtime();
+  };
+  mark(0, 0);
+  // ---- prologue: the full halo of chunk 0 (always a 3x3 chunk) + the weights of step 0
+  setup(0);
+  load_w(0, 0);
+  if (A.nchunk1 * 9 > 1) load_w(1, 1);
+#pragma unroll
+  for (int k = 0; k < LPRO; ++k) load_main(k, tid + NT * k, tid + NT * k < TOT1);
+#pragma unroll
+  for (int k = 0; k < LPRO; ++k) store(0, k, true);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
 
-  for (int s = 0; s < A.nsteps; ++s) {
-    const bool seg2 = s >= A.nchunk1 * 9;
-    const int chunk = seg2 ? A.nchunk1 + (s - A.nchunk1 * 9) : s / 9;
-    const int tap = seg2 ? 4 : s - chunk * 9;
-    const int nt = seg2 ? 1 : 9;
-    const int t_in = seg2 ? 0 : tap;
-    const bool more = chunk + 1 < nchunks;
-    int cnt = 0;
+  // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8); the next chunk is staged in 4
+  //      pieces behind the MFMAs of steps 0-3.  Waves of the two cout halves share a SIMD pairwise:
+  //      wco 0 transforms its staged piece before its first tap, wco 1 after it, so one wave's
+  //      GroupNorm/SiLU VALU work overlaps the other's MFMAs.
+  const int T1 = A.nchunk1 * 9;
+  int wb = 0;   // weight double-buffer of the current step (tiles 2*wb, 2*wb+1)
+  int s = 0;
+  for (int chunk = 0; chunk < A.nchunk1; ++chunk) {
+    const int nx = chunk + 1;
+    const bool more = nx < nchunks, nseg2 = nx >= A.nchunk1;
+    if (more) setup(nx);
+#pragma unroll 1
+    for (int ps = 0; ps < 5; ++ps) {
+      const int slot = chunk * 9 + 2 * ps;
+      const bool two = ps < 4;
+      const bool st = more && ps < 4;
+      if (st) {
+        if (!nseg2) {
+#pragma unroll
+          for (int k = 0; k < LPT; ++k) {
+            const int hl = tid + NT * k;
+            load_main(k, ps * PC1 + hl, hl < PC1 && ps * PC1 + hl < TOT1);
+          }
+        } else {
+          load_seg2(0, ps * (NT / 8) + tp);
+        }
+      }
+      // weights of the next step: the next pair of this chunk, the first pair of the next chunk,
+      // or the first 1x1 slot
+      const int nslot = slot + (two ? 2 : 1);
+      if (nslot < A.nsteps_slots) {
+        load_w(nslot, 2 * (wb ^ 1));
+        const bool ntwo = nslot < T1 && (nslot - (nslot / 9) * 9) < 8;
+        if (ntwo) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
+      }
+      mark(s + 1, 0);
+      if (wco == 0) {
+        if (st) {
+#pragma unroll
+          for (int k = 0; k < (nseg2 ? 1 : LPT); ++k) store(nx & 1, k, !nseg2);
+        }
+        compute(chunk & 1, 2 * ps, false, 2 * wb);
+      } else {
+        compute(chunk & 1, 2 * ps, false, 2 * wb);
+        if (st) {
+#pragma unroll
+          for (int k = 0; k < (nseg2 ? 1 : LPT); ++k) store(nx & 1, k, !nseg2);
+        }
+      }
+      mark(s + 1, 1);
+      if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
+      mark(s + 1, 2);
+      __syncthreads();
+      mark(s + 1, 3);
+      wb ^= 1;
+      ++s;
+    }
+  }
+  // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, next chunk staged whole
+  for (int chunk = A.nchunk1; chunk < nchunks; ++chunk) {
+    const int nx = chunk + 1;
+    const bool more = nx < nchunks;
     if (more) {
-      int tot;
-      const int pc = piece(chunk + 1, nt, tot);
-      const int lo = t_in * pc, hi = min(tot, lo + pc);
-      cnt = lo < hi ? (hi - lo + NT - 1) / NT : 0;
-      if (t_in == 0) load_coef(chunk + 1);
-      load_h(chunk + 1, lo, hi, cnt);
+      setup(nx);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) load_seg2(k, tp + 64 * k);
     }
-    if (s + 1 < A.nsteps) load_w(s + 1, (s + 1) & 1);
-    compute(chunk, tap, seg2, s & 1);
-    if (cnt) store_h((chunk + 1) & 1, cnt, chunk + 1 < A.nchunk1);
+    const int slot = T1 + (chunk - A.nchunk1);
+    if (slot + 1 < A.nsteps_slots) load_w(slot + 1, 2 * (wb ^ 1));
+    compute(chunk & 1, 4, true, 2 * wb);
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) store(nx & 1, k, false);
+    }
     __syncthreads();
+    wb ^= 1;
+    ++s;
   }
 
+  mark(0, 1);
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
   const int Ho = d.Ho, Wo = d.Wo;
@@ -249,82 +312,165 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { st1[i][r] = 0.f; st2[i][r] = 0.f; }
+
+  if (co0 + BCO <= K && !d.out_f32 && !d.accumulate && !(d.resid && hasx)) {
+    // Fast path: the 256-pixel x 128-channel tile goes through LDS ([pixel][16-byte chunk ^ (pixel & 15)],
+    // conflict-free for the lanes' 8-byte reads), so every global access is a coalesced 16-byte one.
+    bf16r* tileb = lds;   // 64 KiB inside the (now idle) halo buffers
+    const bool side = d.resid != nullptr || hasx;
+    if (side) {
+      u32x4 sv[8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = co0 + wco * 64 + 16 * i + 4 * lq;
-    if (co >= K) continue;
-    const bool full = co + 3 < K;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < 4; ++r) {
-      if (co + r < K) {
-        if (d.bias) bias[r] += d.bias[co + r];
-        if (d.bias2) bias[r] += d.bias2[co + r];
-        if (d.bias_nc) bias[r] += d.bias_nc[(size_t)n * K + co + r];
+      for (int k = 0; k < 8; ++k) {
+        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
+        const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+        const int c = co0 + c16 * 8;
+        const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
+                           : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
+                                           : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
+        sv[k] = *(const u32x4*)src;
       }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
+        *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
+      }
+      __syncthreads();
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int y = ty0 + wpx * 4 + j, x = tx0 + l16;
-      const size_t p = ((size_t)n * Ho + y) * Wo + x;
-      float v[4];
+    for (int i = 0; i < 4; ++i) {
+      const int cl = wco * 64 + 16 * i + 4 * lq;   // channel within the tile (multiple of 4)
+      const int co = co0 + cl;
+      f32x4 bias = f32x4{0.f, 0.f, 0.f, 0.f}, ea = bias, eb = bias;
+      if (d.bias) bias += *(const f32x4*)(d.bias + co);
+      if (d.bias2) bias += *(const f32x4*)(d.bias2 + co);
+      if (d.bias_nc) bias += *(const f32x4*)(d.bias_nc + (size_t)n * K + co);
+      if (dep) {
+        ea = *(const f32x4*)(d.ep_a + (size_t)n * K + co);
+        eb = *(const f32x4*)(d.ep_b + (size_t)n * K + co);
+      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[r];
-      if (d.resid) {
-        const bf16r* rp = (const bf16r*)d.resid + p * K + co;
-        if (full) {
-          const u32x2 rr = *(const u32x2*)rp;
-          v[0] += bf_lo(rr[0]); v[1] += bf_hi(rr[0]); v[2] += bf_lo(rr[1]); v[3] += bf_hi(rr[1]);
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (co + r < K) v[r] += bf2f(rp[r]);
-        }
-      }
-      float xv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (hasx) {
-        const int C0e = d.ep_C0;
-        for (int r = 0; r < 4; ++r) {
-          const int c = co + r;
-          if (c >= K) continue;
-          const bf16r* xp = (c < C0e) ? (const bf16r*)d.ep_x0 + p * C0e + c
-                                      : (const bf16r*)d.ep_x1 + p * (K - C0e) + (c - C0e);
-          xv[r] = bf2f(*xp);
-          if (dep) v[r] *= silu_grad(d.ep_a[(size_t)n * K + c] * xv[r] + d.ep_b[(size_t)n * K + c]);
-        }
-      }
-      if (d.out_f32) {
-        float* op = (float*)d.out + p * K + co;
-        for (int r = 0; r < 4; ++r)
-          if (co + r < K) op[r] = d.accumulate ? op[r] + v[r] : v[r];
-      } else {
-        bf16r* op = (bf16r*)d.out + p * K + co;
-        if (full) {
-          if (d.accumulate) {
-            const u32x2 o = *(const u32x2*)op;
-            v[0] += bf_lo(o[0]); v[1] += bf_hi(o[0]); v[2] += bf_lo(o[1]); v[3] += bf_hi(o[1]);
-          }
-          u32x2 o;
-          o[0] = pack2(v[0], v[1]);
-          o[1] = pack2(v[2], v[3]);
-          *(u32x2*)op = o;
-          v[0] = bf_lo(o[0]); v[1] = bf_hi(o[0]); v[2] = bf_lo(o[1]); v[3] = bf_hi(o[1]);
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (co + r < K) {
-              const float w = d.accumulate ? bf2f(op[r]) + v[r] : v[r];
-              op[r] = (bf16r)f2bf(w);
-              v[r] = bf2f(op[r]);
+      for (int j = 0; j < 4; ++j) {
+        const int pi = (wpx * 4 + j) * 16 + l16;
+        bf16r* tp8 = tileb + pi * BCO + (((cl >> 3) ^ (pi & 15)) * 8) + (cl & 7);
+        float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[r];
+        if (side) {
+          const u32x2 sr = *(const u32x2*)tp8;
+          const float f[4] = {bf_lo(sr[0]), bf_hi(sr[0]), bf_lo(sr[1]), bf_hi(sr[1])};
+          if (d.resid) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += f[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              xv[r] = f[r];
+              if (dep) v[r] *= silu_grad(ea[r] * f[r] + eb[r]);
             }
+          }
+        }
+        u32x2 o;
+        o[0] = pack2(v[0], v[1]);
+        o[1] = pack2(v[2], v[3]);
+        *(u32x2*)tp8 = o;
+        if (stats) {
+          const float w[4] = {bf_lo(o[0]), bf_hi(o[0]), bf_lo(o[1]), bf_hi(o[1])};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            st1[i][r] += w[r];
+            st2[i][r] += hasx ? w[r] * xv[r] : w[r] * w[r];
+          }
         }
       }
-      if (stats) {
+    }
+    __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          st1[i][r] += v[r];
-          st2[i][r] += hasx ? v[r] * xv[r] : v[r] * v[r];
+    for (int k = 0; k < 8; ++k) {
+      const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
+      const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+      *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) =
+          *(const u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8));
+    }
+  } else {
+  #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wco * 64 + 16 * i + 4 * lq;
+      if (co >= K) continue;
+      const bool full = co + 3 < K;
+      float bias[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) {
+        if (co + r < K) {
+          if (d.bias) bias[r] += d.bias[co + r];
+          if (d.bias2) bias[r] += d.bias2[co + r];
+          if (d.bias_nc) bias[r] += d.bias_nc[(size_t)n * K + co + r];
+        }
+      }
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int y = ty0 + wpx * 4 + j, x = tx0 + l16;
+        const size_t p = ((size_t)n * Ho + y) * Wo + x;
+        float v[4];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[r];
+        if (d.resid) {
+          const bf16r* rp = (const bf16r*)d.resid + p * K + co;
+          if (full) {
+            const u32x2 rr = *(const u32x2*)rp;
+            v[0] += bf_lo(rr[0]); v[1] += bf_hi(rr[0]); v[2] += bf_lo(rr[1]); v[3] += bf_hi(rr[1]);
+          } else {
+            for (int r = 0; r < 4; ++r)
+              if (co + r < K) v[r] += bf2f(rp[r]);
+          }
+        }
+        float xv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (hasx) {
+          const int C0e = d.ep_C0;
+          for (int r = 0; r < 4; ++r) {
+            const int c = co + r;
+            if (c >= K) continue;
+            const bf16r* xp = (c < C0e) ? (const bf16r*)d.ep_x0 + p * C0e + c
+                                        : (const bf16r*)d.ep_x1 + p * (K - C0e) + (c - C0e);
+            xv[r] = bf2f(*xp);
+            if (dep) v[r] *= silu_grad(d.ep_a[(size_t)n * K + c] * xv[r] + d.ep_b[(size_t)n * K + c]);
+          }
+        }
+        if (d.out_f32) {
+          float* op = (float*)d.out + p * K + co;
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) op[r] = d.accumulate ? op[r] + v[r] : v[r];
+        } else {
+          bf16r* op = (bf16r*)d.out + p * K + co;
+          if (full) {
+            if (d.accumulate) {
+              const u32x2 o = *(const u32x2*)op;
+              v[0] += bf_lo(o[0]); v[1] += bf_hi(o[0]); v[2] += bf_lo(o[1]); v[3] += bf_hi(o[1]);
+            }
+            u32x2 o;
+            o[0] = pack2(v[0], v[1]);
+            o[1] = pack2(v[2], v[3]);
+            *(u32x2*)op = o;
+            v[0] = bf_lo(o[0]); v[1] = bf_hi(o[0]); v[2] = bf_lo(o[1]); v[3] = bf_hi(o[1]);
+          } else {
+            for (int r = 0; r < 4; ++r)
+              if (co + r < K) {
+                const float w = d.accumulate ? bf2f(op[r]) + v[r] : v[r];
+                op[r] = (bf16r)f2bf(w);
+                v[r] = bf2f(op[r]);
+              }
+          }
+        }
+        if (stats) {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            st1[i][r] += v[r];
+            st2[i][r] += hasx ? v[r] * xv[r] : v[r] * v[r];
+          }
         }
       }
     }
   }
+  mark(0, 2);
   if (stats) {
     // slab row = one wave's 64 pixels (4 rows x 16) of one image; any bijection works for GN
     const int srow = tile * 4 + wpx;
@@ -376,6 +522,8 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
+  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      (long long)d->N * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
   HArgs A;
   A.d = *d;
   A.C = d->C0 + d->C1;
@@ -385,9 +533,10 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.ntc = (d->K + BCO - 1) / BCO;
   A.nchunk1 = (A.C + BK - 1) / BK;
   A.nchunk2 = d->src2 ? (A.C23 + BK - 1) / BK : 0;
-  A.nsteps = A.nchunk1 * 9 + A.nchunk2;
+  A.nsteps_slots = A.nchunk1 * 9 + A.nchunk2;
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
+  A.trace = g_trace;
   const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;   // too few tiles to fill the chip: the split-K implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
@@ -403,6 +552,13 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
     else hipLaunchKernelGGL((conv3x3_halo<false, 0>), g, blk, 0, st, A);
   }
   return (int)hipGetLastError();
+}
+
+// Debug hook (not part of the public ABI): record per-phase s_memtime stamps of the next launches
+// into buf [TRACE_WG][8 waves][TRACE_STEPS][TRACE_PH] (u64); null disables.  tools/halo_trace.py.
+extern "C" int fmd_debug_halo_trace(void* buf) {
+  g_trace = (unsigned long long*)buf;
+  return 0;
 }
 
 extern "C" int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C) {

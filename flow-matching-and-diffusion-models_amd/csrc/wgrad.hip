@@ -280,9 +280,12 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   if (d->C1 && !d->src1) return -2;
   WArgs A = make_args(d);
   const int splits = d->splits > 1 ? d->splits : 1;
-  dim3 grid(A.ntc * A.nci * A.T, splits);
-  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, s, A);
-  int rc = (int)hipGetLastError();
+  int rc = d->force_generic ? 1 : fmd_wgrad_halo(d, stream);
+  if (rc == 1) {
+    dim3 grid(A.ntc * A.nci * A.T, splits);
+    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, s, A);
+    rc = (int)hipGetLastError();
+  }
   if (rc) return rc;
   const size_t per = (size_t)d->K * A.T * A.C;
   int blocks = (int)((per + 255) / 256);

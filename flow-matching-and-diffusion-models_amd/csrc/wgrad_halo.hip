@@ -1,0 +1,273 @@
+// Halo-tiled weight gradient for 3x3 stride-1 convolutions (gfx950) -- the UNet's
+// dominant backward problem.
+//
+// dW[co][ci][tap] = sum_p dY[p][co] * G(p + off(tap))[ci], G = SiLU(a*x + b) (the
+// forward's fused GroupNorm prologue, recomputed).  A workgroup owns 128 output
+// channels x 64 input channels x ALL 9 taps and streams 8x16-pixel tiles of its
+// split of the image batch: per tile the 128-pixel dY tile and the 10x18 halo of
+// G are staged ONCE into LDS, and every tap reads its shifted pixel rows from the
+// same halo image -- 9x less staging/transform work than one workgroup per tap.
+// Both operands are pixel-major in HBM, so the reduction (pixel) dimension is the
+// strided one: LDS images are chunk-major ([16-byte channel group][position],
+// plane stride == 16 banks mod 64) and MFMA fragments come from gfx950's
+// transposing ds_read_b64_tr_b16, which is bank-conflict-free on this layout.
+// Waves: 2 (64 couts) x 4 (16 cins); each holds 4 x 9 accumulator tiles.
+// Tiles are double-buffered: the loads of tile i+1 are in flight while tile i's
+// MFMAs run; one barrier per tile.  Partial sums go to a split-K slab reduced by
+// wgrad_reduce (csrc/wgrad.hip), which writes the reference [K][C][3][3] layout.
+//
+// Replaces: autograd of nn.Conv2d weight/bias (src/nn/ops/convolution.py:53) for
+// the ResBlock 3x3 convs (src/nn/blocks/residual.py:71-76).
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+constexpr int WTH = 8, WTW = 16;                 // pixel tile
+constexpr int WPIX = WTH * WTW;                  // 128 pixels = 4 MFMA k-steps
+constexpr int HR = WTW + 2;                      // halo row (18)
+constexpr int HPOSW = (WTH + 2) * HR;            // 180 halo positions
+constexpr int XPAD = 180;                        // x plane stride in positions (180*4 dwords = 16 mod 64 banks)
+constexpr int DPAD = 132;                        // dY plane stride (132*4 = 16 mod 64)
+constexpr int WCO = 128, WCI = 64;
+constexpr int XPL = WCI / 8, DPL = WCO / 8;      // 16-byte planes
+constexpr int XBUF = XPL * XPAD * 8;             // bf16 elements per x buffer
+constexpr int DBUF = DPL * DPAD * 8;             // per dY buffer
+constexpr int NT = 512;
+constexpr int XLD = (HPOSW * XPL + NT - 1) / NT; // x chunks per thread per tile (3)
+
+struct HWArgs {
+  fmd_wgrad_desc d;
+  int C, ldy;
+  int tiles_x, tiles_y, ntiles;    // pixel tiles over N x Ho x Wo
+  int ntc, nci, splits, per_split;
+};
+
+// PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU
+template <int PRO>
+__global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
+  __shared__ __attribute__((aligned(16))) bf16r lds[2 * XBUF + 2 * DBUF];
+  bf16r* xb = lds;
+  bf16r* db_ = lds + 2 * XBUF;
+  const fmd_wgrad_desc& d = A.d;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wco = wid >> 2, wci = wid & 3;
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int rq = l16 >> 2, rp = lane & 3;          // transposed-read row / column group
+
+  int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tci = b % A.nci; b /= A.nci;
+  const int tco = b % A.ntc; b /= A.ntc;
+  const int split = b;
+  const int co0 = tco * WCO, ci0 = tci * WCI;
+  const int t0 = split * A.per_split, t1 = min(A.ntiles, t0 + A.per_split);
+  const bool do_bias = d.db != nullptr && tci == 0;
+
+  const bf16r* __restrict__ dy = (const bf16r*)d.dy;
+  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
+  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
+
+  // this thread's staging slots: x channel group kx8 (fixed), dY channel group dc (fixed)
+  const int kx8 = tid & 7;
+  const int c = ci0 + kx8 * 8;
+  const bf16r* xsrc = (c < d.C0) ? s0 + c : s1 + (c - d.C0);
+  const int xcs = (c < d.C0) ? d.C0 : d.C1;
+  float pa[8], pb[8];
+
+  auto tile_org = [&](int t, int& n, int& ty0, int& tx0) {
+    const int per_img = A.tiles_x * A.tiles_y;
+    n = t / per_img;
+    const int r = t - n * per_img;
+    ty0 = (r / A.tiles_x) * WTH;
+    tx0 = (r - (r / A.tiles_x) * A.tiles_x) * WTW;
+  };
+
+  u32x4 rx[XLD];
+  int xo[XLD];                  // LDS offset, -1 none, bit 30 zero padding
+  int cur_n = -1;
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};   // bias partials of this lane's 4 couts (from the A fragments)
+
+  auto load_tile = [&](int t) {
+    int n, ty0, tx0;
+    tile_org(t, n, ty0, tx0);
+    if (PRO != 0 && n != cur_n) {     // GN affine of this thread's 8 channels for image n
+      const f32x4* a4 = (const f32x4*)(d.pro_a + (size_t)n * A.C + c);
+      const f32x4* b4 = (const f32x4*)(d.pro_b + (size_t)n * A.C + c);
+      const f32x4 a0 = a4[0], a1 = a4[1], b0 = b4[0], b1 = b4[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { pa[e] = a0[e]; pa[4 + e] = a1[e]; pb[e] = b0[e]; pb[4 + e] = b1[e]; }
+      cur_n = n;
+    }
+#pragma unroll
+    for (int k = 0; k < XLD; ++k) {
+      const int q = tid + NT * k;
+      const int pos = q >> 3;
+      const bool act = pos < HPOSW;
+      const int hy = act ? pos / HR : 0, hx = act ? pos - (pos / HR) * HR : 0;
+      const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+      const bool valid = act && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
+      const int pix = valid ? (n * d.Hs + y) * d.Ws + x : 0;
+      rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
+      xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
+    }
+  };
+  // dY needs no transform: gathered global -> LDS by DMA (lane = one pixel's 16-byte channel group)
+  auto dma_dy = [&](int t, int buf) {
+    int n, ty0, tx0;
+    tile_org(t, n, ty0, tx0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int idx = wid * 4 + j, plane = idx >> 1, half = idx & 1;
+      const int pos = half * 64 + lane;
+      const int pix = (n * d.Ho + ty0 + (pos >> 4)) * d.Wo + tx0 + (pos & 15);
+      __builtin_amdgcn_global_load_lds((const void*)(dy + (size_t)pix * A.ldy + co0 + plane * 8),
+                                       (__attribute__((address_space(3))) void*)(db_ + buf * DBUF +
+                                                                                 (plane * DPAD + half * 64) * 8),
+                                       16, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < XLD; ++k) {
+      u32x4 v = rx[k];
+      if (PRO != 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = bf_lo(v[e]) * pa[2 * e] + pb[2 * e];
+          float hi = bf_hi(v[e]) * pa[2 * e + 1] + pb[2 * e + 1];
+          if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
+          v[e] = pack2(lo, hi);
+        }
+      }
+      const int o = xo[k];
+      if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
+      if (o >= 0) *(u32x4*)(xb + buf * XBUF + (o & ~(1 << 30))) = v;
+    }
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const bf16r* xbb = xb + buf * XBUF;
+    const bf16r* dbb = db_ + buf * DBUF;
+#pragma unroll 1
+    for (int ks = 0; ks < WPIX / 32; ++ks) {
+      const int r0 = 2 * ks + (lq >> 1);          // tile row of this lane group's 8 pixels
+      const int px0 = 8 * (lq & 1);
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int plane = wco * 8 + 2 * i + (rp >> 1);
+        const bf16r* base = dbb + (plane * DPAD + r0 * WTW + px0 + rq) * 8 + (rp & 1) * 4;
+        const s16x4 lo = ds_read_tr16(base);
+        const s16x4 hi = ds_read_tr16(base + 4 * 8);
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        if (do_bias && ks == wci) {   // each wave sums one k-step's pixels: sum over waves = all pixels
+          float sacc = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sacc += bf2f((unsigned short)lo[e]) + bf2f((unsigned short)hi[e]);
+          dbs[i] += sacc;
+        }
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const int plane = wci * 2 + (rp >> 1);
+        const bf16r* base = xbb + (plane * XPAD + (r0 + ky) * HR + px0 + kx + rq) * 8 + (rp & 1) * 4;
+        const s16x4 lo = ds_read_tr16(base);
+        const s16x4 hi = ds_read_tr16(base + 4 * 8);
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][tap] = mfma16(af[i], bv, acc[i][tap]);
+      }
+    }
+  };
+
+  if (t0 < t1) {
+    dma_dy(t0, 0);
+    load_tile(t0);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int t = t0; t < t1; ++t) {
+      const bool more = t + 1 < t1;
+      if (more) {
+        load_tile(t + 1);
+        dma_dy(t + 1, buf ^ 1);
+      }
+      compute(buf);
+      if (more) store_tile(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout)
+  const size_t per = (size_t)d.K * 9 * A.C;
+  float* ws = d.ws + (size_t)split * per;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
+        const int ci = ci0 + wci * 16 + l16;
+        ws[((size_t)co * 9 + tap) * A.C + ci] = acc[i][tap][r];
+      }
+  if (do_bias) {
+    // lanes of the 4 pixel groups, then the 4 cin-waves (each summed one k-step) of a cout half
+    float* red = (float*)lds;    // [4 wci][128 co] floats; the tiles are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dbs[i] += __shfl_xor(dbs[i], 16, 64);
+      dbs[i] += __shfl_xor(dbs[i], 32, 64);
+    }
+    __syncthreads();
+    if (lq == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wci * WCO + wco * 64 + 16 * i + l16] = dbs[i];
+    }
+    __syncthreads();
+    if (tid < WCO) {
+      const float v = red[tid] + red[WCO + tid] + red[2 * WCO + tid] + red[3 * WCO + tid];
+      d.ws[(size_t)A.splits * per + (size_t)split * d.K + co0 + tid] = v;
+    }
+  }
+}
+
+}  // namespace
+
+// 3x3 / stride 1 / pad 1 / no upsample, K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
+// Returns 1 (nothing launched) when the problem does not qualify.  d->splits = pixel-tile splits.
+extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->upsample) return 1;
+  if (d->Ho != d->Hs || d->Wo != d->Ws || d->Ho % WTH || d->Wo % WTW) return 1;
+  const int C = d->C0 + d->C1;
+  if (d->K % WCO || C % WCI || (d->C0 % 8) || !d->ws) return 1;
+  const int ldy = d->ldy > 0 ? d->ldy : d->K;
+  if (ldy % 8) return 1;
+  if ((long long)d->N * d->Hs * d->Ws >= (1LL << 31) / 8) return 1;
+  HWArgs A;
+  A.d = *d;
+  A.C = C;
+  A.ldy = ldy;
+  A.tiles_x = d->Wo / WTW;
+  A.tiles_y = d->Ho / WTH;
+  A.ntiles = d->N * A.tiles_x * A.tiles_y;
+  A.ntc = d->K / WCO;
+  A.nci = C / WCI;
+  A.splits = d->splits > 1 ? d->splits : 1;
+  A.per_split = (A.ntiles + A.splits - 1) / A.splits;
+  const int nwg = A.ntc * A.nci * A.splits;
+  const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (pro == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(nwg), dim3(NT), 0, st, A);
+  else if (pro == 1) hipLaunchKernelGGL(wgrad_halo_kernel<1>, dim3(nwg), dim3(NT), 0, st, A);
+  else hipLaunchKernelGGL(wgrad_halo_kernel<0>, dim3(nwg), dim3(NT), 0, st, A);
+  return (int)hipGetLastError();
+}

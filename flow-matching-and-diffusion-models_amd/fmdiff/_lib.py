@@ -35,7 +35,7 @@ class WgradDesc(C.Structure):
         ("N", i32), ("Hs", i32), ("Ws", i32), ("C0", i32), ("C1", i32), ("Ho", i32), ("Wo", i32), ("K", i32),
         ("ks", i32), ("stride", i32), ("pad", i32), ("upsample", i32),
         ("src0", p), ("src1", p), ("pro_a", p), ("pro_b", p), ("pro_silu", i32), ("dy", p), ("ldy", i32), ("dw", p), ("db", p),
-        ("accumulate", i32), ("ws", p), ("splits", i32),
+        ("accumulate", i32), ("ws", p), ("splits", i32), ("force_generic", i32),
     ]
 
 
@@ -45,6 +45,7 @@ SIGNATURES = {
     "fmd_conv_halo": [C.POINTER(ConvDesc), p],
     "fmd_wgrad": [C.POINTER(WgradDesc), p],
     "fmd_wgrad_workspace": [C.POINTER(WgradDesc)],
+    "fmd_wgrad_halo": [C.POINTER(WgradDesc), p],
     "fmd_halo_tiled_size": [i32, i32, i32],
     "fmd_tile_weights_halo": [p, i32, i32, i32, p, p],
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],

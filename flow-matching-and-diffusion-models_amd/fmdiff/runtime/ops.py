@@ -180,8 +180,14 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     return out, st
 
 
+def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
+    """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip)."""
+    return (ks == 3 and stride == 1 and pad == 1 and not upsample and Ho == Hs and Wo == Ws and Ho % 8 == 0
+            and Wo % 16 == 0 and K % 128 == 0 and C % 64 == 0 and C0 % 8 == 0 and (ldy or K) % 8 == 0)
+
+
 def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro=None, db=None, accumulate=True,
-          splits=None, dy_offset=0):
+          splits=None, dy_offset=0, force_generic=False):
     """dW (+)= conv weight gradient in the reference [K][C][kh][kw] fp32 layout (and db).
 
     ``dy_offset``: use channels [dy_offset, dy_offset + dw.shape[0]) of a wider dY (fused q/k/v)."""
@@ -198,10 +204,18 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     if pro is not None:
         d.pro_a, d.pro_b, d.pro_silu = _p(pro[0]), _p(pro[1]), int(pro[2])
     d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
+    d.force_generic = int(force_generic)
     if splits is None:
-        tiles = -(-K // 128) * -(-Ct // 128) * ks * ks
-        steps = -(-M // 32)
-        splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), 256))
+        if not force_generic and wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample, ldy):
+            # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk, pixel-tile split);
+            # partial slabs capped at ~96 MB (their write + reduce read)
+            tiles = N * (Ho // 8) * (Wo // 16)
+            base = (K // 128) * (Ct // 64)
+            splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36)))
+        else:
+            tiles = -(-K // 128) * -(-Ct // 128) * ks * ks
+            steps = -(-M // 32)
+            splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), 256))
     d.splits = splits
     ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
     d.ws = _p(ws)

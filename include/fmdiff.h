@@ -95,10 +95,15 @@ typedef struct fmd_wgrad_desc {
   float* db;                /* fp32 [K] or NULL */
   int32_t accumulate;
   float* ws;                /* fp32 workspace, size fmd_wgrad_workspace() floats */
-  int32_t splits;
+  int32_t splits;           /* split-K over pixels (halo path: over 8x16-pixel tiles) */
+  int32_t force_generic;    /* 1: never use the halo-tiled kernel (tests) */
 } fmd_wgrad_desc;
 
+/* Dispatches 3x3 stride-1 problems (K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0) to the
+ * halo-tiled kernel (csrc/wgrad_halo.hip), everything else to the per-tap kernel (csrc/wgrad.hip). */
 int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t s);
+/* Halo-tiled 3x3 weight gradient (partial slabs only, no reduce); returns 1 when not applicable. */
+int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t s);
 int64_t fmd_wgrad_workspace(const fmd_wgrad_desc* d);
 
 /* ------------------------------------------------------------- groupnorm

@@ -130,9 +130,12 @@ def test_conv_data_gradient(mode):
     _close(got, x.grad.permute(0, 2, 3, 1))
 
 
-@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro"])
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro", "s1_generic", "pro_generic"])
 def test_wgrad(mode):
+    """16x16, C=64, K=128: the 3x3 stride-1 modes run the halo kernel (csrc/wgrad_halo.hip) unless *_generic."""
     O = ops()
+    generic = mode.endswith("_generic")
+    mode = mode.replace("_generic", "")
     N, H, W, C, K = 2, 16, 16, 64, 128
     ks, s, up = (1, 1, False) if mode == "1x1" else (3, 2 if mode == "s2" else 1, mode == "up")
     pad = ks // 2
@@ -153,7 +156,44 @@ def test_wgrad(mode):
     dw = torch.zeros(K, C, ks, ks, device=DEV)
     db = torch.zeros(K, device=DEV)
     O.wgrad(xb.to(DEV), dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV), dw, ks=ks, stride=s,
-            pad=pad, upsample=up, pro=pro, db=db)
+            pad=pad, upsample=up, pro=pro, db=db, force_generic=generic)
+    torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
+    torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("case", ["concat_pro", "wide_dy_offset", "many_tiles"])
+def test_wgrad_halo_vs_torch(case):
+    """Halo-tiled wgrad on multi-tile / multi-split problems: two-source concat with GN+SiLU prologue,
+    a dY that is a channel slice of a wider tensor (ldy/dy_offset), and many tiles per split."""
+    O = ops()
+    N, H, W, C0, C1, K = 2, 32, 32, 64, 128, 128
+    if case == "wide_dy_offset":
+        C1, K = 0, 256
+    if case == "many_tiles":
+        N, H, W, C1 = 4, 64, 64, 0
+    C = C0 + C1
+    assert O.wgrad_halo_eligible(H, W, H, W, K, C, C0)
+    x0 = _rand_nhwc(N, H, W, C0, 31)
+    x1 = _rand_nhwc(N, H, W, C1, 32) if C1 else None
+    x = _to_nchw(torch.cat([x0, x1], -1) if C1 else x0)
+    a = torch.rand(N, C) + 0.5
+    b = torch.randn(N, C) * 0.2
+    xt = F.silu(x * a[:, :, None, None] + b[:, :, None, None]).to(torch.bfloat16).float()
+    w = _w(K, C, 3, 33).requires_grad_()
+    bias = torch.zeros(K, requires_grad=True)
+    y = F.conv2d(xt, w, bias, padding=1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    off = 0
+    if case == "wide_dy_offset":   # dY lives at channels [64, 64+K) of a 384-channel tensor
+        wide = torch.zeros(N, H, W, 384, dtype=torch.bfloat16)
+        wide[..., 64:64 + K] = dyn
+        dyn, off = wide, 64
+    dw = torch.zeros(K, C, 3, 3, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    O.wgrad(x0.to(DEV), dyn.to(DEV), dw, src1=x1.to(DEV) if C1 else None, pro=(a.to(DEV), b.to(DEV), True),
+            db=db, dy_offset=off)
     torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
     torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
 
