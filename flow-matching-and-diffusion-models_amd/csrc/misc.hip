@@ -407,6 +407,214 @@ __global__ void add_bf16_kernel(const bf16r* __restrict__ a, bf16r* __restrict__
   GRID_STRIDE(i, n) dst[i] = (bf16r)f2bf(bf2f(dst[i]) + bf2f(a[i]));
 }
 
+
+// ------------------------------------------------------------------ grouped linears
+// All ResBlock emb_layers (Linear(emb_dim, 2C or C), residual.py:63-68) of one UNet as ONE launch:
+// the groups' output rows are concatenated ([B][sum O]); a block owns 64 rows of one group.
+struct GLGroup { const float* w; const float* b; float* dw; float* db; long long O; long long off; };
+
+__global__ __launch_bounds__(256) void glinear_fwd_kernel(const float* __restrict__ x, int B, int I,
+                                                          const GLGroup* __restrict__ G, const int2* __restrict__ blk,
+                                                          int in_silu, float* __restrict__ y, int ys) {
+  extern __shared__ float xs[];   // [B][I] (SiLU applied)
+  for (int e = threadIdx.x; e < B * I; e += blockDim.x) {
+    const float v = x[e];
+    xs[e] = in_silu ? siluf_(v) : v;
+  }
+  __syncthreads();
+  const int2 bi = blk[blockIdx.x];
+  const GLGroup g = G[bi.x];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = bi.y + wid * 16 + (lane >> 2), p = lane & 3;
+  const bool act = r < g.O;
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+  if (act) {
+    const float* wr = g.w + (size_t)r * I;
+    for (int i = p * 4; i < I; i += 16) {
+      const f32x4 w4 = *(const f32x4*)(wr + i);
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        if (b < B) {
+          const f32x4 x4 = *(const f32x4*)(xs + b * I + i);
+          acc[b] += w4[0] * x4[0] + w4[1] * x4[1] + w4[2] * x4[2] + w4[3] * x4[3];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 32; ++b) {
+    if (b < B) {
+      float v = acc[b];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      if (act && p == 0) y[(size_t)b * ys + g.off + r] = v + (g.b ? g.b[r] : 0.f);
+    }
+  }
+}
+
+// dW[r][i] += sum_b dy[b][r] xin[b][i];  db[r] += sum_b dy[b][r];  dx partial[blk][rg][b][i] = sum_r dy[b][r] W[r][i]
+__global__ __launch_bounds__(256) void glinear_bwd_kernel(const float* __restrict__ x, int B, int I,
+                                                          const GLGroup* __restrict__ G, const int2* __restrict__ blk,
+                                                          int in_silu, const float* __restrict__ dy, int dys,
+                                                          float* __restrict__ part) {
+  extern __shared__ float sm[];   // xin [B][I] | dy rows [64][B]
+  float* xs = sm;
+  float* ds = sm + B * I;
+  const int2 bi = blk[blockIdx.x];
+  const GLGroup g = G[bi.x];
+  const int nr = min(64, (int)g.O - bi.y);
+  for (int e = threadIdx.x; e < B * I; e += blockDim.x) {
+    const float v = x[e];
+    xs[e] = in_silu ? siluf_(v) : v;
+  }
+  for (int e = threadIdx.x; e < 64 * B; e += blockDim.x) {
+    const int rr = e / B, b = e - rr * B;
+    ds[e] = rr < nr ? dy[(size_t)b * dys + g.off + bi.y + rr] : 0.f;
+  }
+  __syncthreads();
+  const int nq = I / 4, nrg = blockDim.x / nq;
+  const int q = threadIdx.x % nq, rg = threadIdx.x / nq;
+  const int i4 = q * 4;
+  float dx[32][4];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) dx[b][0] = dx[b][1] = dx[b][2] = dx[b][3] = 0.f;
+  for (int rr = rg; rr < nr; rr += nrg) {
+    const int r = bi.y + rr;
+    const f32x4 w4 = *(const f32x4*)(g.w + (size_t)r * I + i4);
+    f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      if (b < B) {
+        const float dv = ds[rr * B + b];
+        const f32x4 x4 = *(const f32x4*)(xs + b * I + i4);
+        gw += dv * x4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dx[b][e] += dv * w4[e];
+      }
+    }
+    f32x4* dwp = (f32x4*)(g.dw + (size_t)r * I + i4);
+    *dwp = *dwp + gw;
+    if (q == 0 && g.db) {
+      float sb = 0.f;
+      for (int b = 0; b < B; ++b) sb += ds[rr * B + b];
+      g.db[r] += sb;
+    }
+  }
+  float* pp = part + ((size_t)blockIdx.x * nrg + rg) * B * I;
+#pragma unroll
+  for (int b = 0; b < 32; ++b)
+    if (b < B) *(f32x4*)(pp + (size_t)b * I + i4) = f32x4{dx[b][0], dx[b][1], dx[b][2], dx[b][3]};
+}
+
+// dx[b][i] (+)= silu'(x) * sum_p part[p][b][i]
+__global__ void glinear_dx_reduce(const float* __restrict__ part, int np, int B, int I, const float* __restrict__ x,
+                                  int in_silu, float* __restrict__ dx, int acc) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * I; e += gridDim.x * blockDim.x) {
+    float v0 = 0.f, v1 = 0.f;
+    int p = 0;
+    for (; p + 2 <= np; p += 2) { v0 += part[(size_t)p * B * I + e]; v1 += part[(size_t)(p + 1) * B * I + e]; }
+    if (p < np) v0 += part[(size_t)p * B * I + e];
+    float v = v0 + v1;
+    if (in_silu) v *= silu_grad(x[e]);
+    dx[e] = acc ? dx[e] + v : v;
+  }
+}
+
+
+// ------------------------------------------------------------------ batched weight layouts
+// One launch re-derives every bf16 kernel layout of the UNet from the fp32 masters after the
+// optimizer step.  A block owns a 32 (k) x 32 (c) tile of one master weight w[K][C][T]: it reads the
+// tile once (contiguous T*32-float runs per k) into LDS and writes every requested layout of it with
+// contiguous 64-512 B runs.  Layouts (see fmd_prep_weights, fmd_tile_weights_halo):
+//   kind 0 base: mode 0 [R=Kpad][T][Cc=Cpad]; modes 1/3 [R=Cpad][T][Cc=Kpad] (3: taps flipped);
+//                mode 2 [R=Cpad][16][Cc=Kpad] (upsample + 3x3 data gradient, 4x4 effective taps)
+//   kind 1 halo tiles of a base layout: [ceil(R/128)][ceil(Cc/64)][T][8][128][8]
+// Job (16 x int64): w, K | C << 32, ks | nout << 32, first block | kt << 32 (k tiles),
+//                   then per output (<= 6): out, mode | kind << 8 | R << 16 | Cc << 40.
+constexpr int PT = 32;          // k and c tile
+constexpr int PTS = PT * 9 + 1; // LDS row stride (floats) per k: conflict-free transposed reads
+
+FMD_DEV float ptile_value(const float* tile, int kl, int cl, int ks, int mode, int tap) {
+  const int T = ks * ks;
+  if (mode == 0 || mode == 1) return tile[kl * PTS + cl * T + tap];
+  if (mode == 3) return tile[kl * PTS + cl * T + (T - 1 - tap)];
+  const int ry = tap >> 2, rx = tap & 3;
+  const int ylo = (ry == 0) ? 2 : (ry == 1 ? 1 : 0), yhi = (ry == 3) ? 0 : (ry == 2 ? 1 : 2);
+  const int xlo = (rx == 0) ? 2 : (rx == 1 ? 1 : 0), xhi = (rx == 3) ? 0 : (rx == 2 ? 1 : 2);
+  float v = 0.f;
+  for (int ky = ylo; ky <= yhi; ++ky)
+    for (int kx = xlo; kx <= xhi; ++kx) v += tile[kl * PTS + cl * 9 + ky * 3 + kx];
+  return v;
+}
+
+__global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __restrict__ jobs, int njobs) {
+  __shared__ float tile[PT * PTS];
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((jobs[mid * 16 + 3] & 0xffffffffLL) <= (long long)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const long long* J = jobs + lo * 16;
+  const float* w = (const float*)J[0];
+  const int K = (int)(J[1] & 0xffffffff), C = (int)(J[1] >> 32);
+  const int ks = (int)(J[2] & 0xffffffff), nout = (int)(J[2] >> 32);
+  const int kt = (int)(J[3] >> 32);
+  const int b = (int)((long long)blockIdx.x - (J[3] & 0xffffffffLL));
+  const int k0 = (b % kt) * PT, c0 = (b / kt) * PT;
+  const int T = ks * ks;
+  // ---- master tile w[k0:k0+32][c0:c0+32][:] (zero outside K x C)
+  for (int e = threadIdx.x; e < PT * PT * T; e += blockDim.x) {
+    const int kl = e / (PT * T), r = e - kl * (PT * T);   // r = cl * T + tap: contiguous in memory
+    const int k = k0 + kl, c = c0 + r / T;
+    tile[kl * PTS + r] = (k < K && c < C) ? w[((size_t)k * C + c0) * T + r] : 0.f;
+  }
+  __syncthreads();
+  for (int o = 0; o < nout; ++o) {
+    bf16r* out = (bf16r*)J[4 + 2 * o];
+    const long long desc = J[5 + 2 * o];
+    const int mode = (int)(desc & 0xff), kind = (int)((desc >> 8) & 0xff);
+    const int R = (int)((desc >> 16) & 0xffffff), Cc = (int)((desc >> 40) & 0xffffff);
+    const int To = mode == 2 ? 16 : T;
+    // tile coordinates in the layout's (row, col) space
+    const int r0 = mode == 0 ? k0 : c0, q0 = mode == 0 ? c0 : k0;
+    if (kind == 0) {
+      // [R][To][Cc]: for each (row, tap) a run of 32 cols
+      for (int e = threadIdx.x; e < PT * To * PT; e += blockDim.x) {
+        const int ql = e % PT, r = e / PT, tap = r % To, rl = r / To;
+        const int row = r0 + rl, col = q0 + ql;
+        if (row >= R || col >= Cc) continue;
+        const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
+        out[((size_t)row * To + tap) * Cc + col] = (bf16r)f2bf(ptile_value(tile, kl, cl, ks, mode, tap));
+      }
+    } else {
+      // [R/128][Cc/64][To][8][128][8]: 16-byte chunks of 8 cols, runs of 32 rows
+      const int nchunk = (Cc + 63) / 64;
+      for (int e = threadIdx.x; e < To * (PT / 8) * PT; e += blockDim.x) {
+        const int rl = e % PT, r = e / PT, kq = r % (PT / 8), tap = r / (PT / 8);
+        const int row = r0 + rl, col8 = q0 + kq * 8;
+        if (row >= ((R + 127) / 128) * 128 || col8 >= nchunk * 64) continue;
+        const int tr = row >> 7, co = row & 127, chunk = col8 >> 6, kc = (col8 >> 3) & 7;
+        unsigned int pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          float v2[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int ql = kq * 8 + 2 * h + u, col = q0 + ql;
+            const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
+            v2[u] = (row < R && col < Cc) ? ptile_value(tile, kl, cl, ks, mode, tap) : 0.f;
+          }
+          pk[h] = pack2(v2[0], v2[1]);
+        }
+        const size_t idx = ((((size_t)tr * nchunk + chunk) * To + tap) * 8 + kc) * 128 + co;
+        *(u32x4*)(out + idx * 8) = u32x4{pk[0], pk[1], pk[2], pk[3]};
+      }
+    }
+  }
+}
+
 }  // namespace
 
 #define LAUNCH(kernel, grid, ...)                                                   \
@@ -423,6 +631,12 @@ int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t m
   LAUNCH(prep_weights_kernel, grid_for(total), w, K, C, ks, mode, Kpad, Cpad, (bf16r*)out);
 }
 
+
+int fmd_prep_weights_batch(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s) {
+  if (njobs < 1 || nblocks < 1) return njobs == 0 ? 0 : -1;
+  hipLaunchKernelGGL(prep_batch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)s, (const long long*)jobs, njobs);
+  return (int)hipGetLastError();
+}
 
 int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s) {
   LAUNCH(nchw_to_nhwc_kernel, grid_for((long long)N * HW * Cpad), x, N, C, HW, Cpad, (bf16r*)y);
@@ -444,6 +658,32 @@ int fmd_linear(const float* x, int32_t B, int32_t I, const float* w, const float
                float* y, int32_t y_stride, fmd_stream_t s) {
   if (B > 32) return -1;
   LAUNCH(linear_kernel, (O + 3) / 4, x, B, I, w, b, O, in_silu, y, y_stride);
+}
+
+int fmd_grouped_linear(const float* x, int32_t B, int32_t I, const void* groups, const void* blocks, int32_t nblk,
+                       int32_t in_silu, float* y, int32_t y_stride, fmd_stream_t s) {
+  if (B < 1 || B > 32 || I % 16 || (size_t)B * I * 4 > 64 * 1024) return -1;
+  hipLaunchKernelGGL(glinear_fwd_kernel, dim3(nblk), dim3(256), (size_t)B * I * 4, (hipStream_t)s, x, B, I,
+                     (const GLGroup*)groups, (const int2*)blocks, in_silu, y, y_stride);
+  return (int)hipGetLastError();
+}
+
+int64_t fmd_grouped_linear_bwd_workspace(int32_t B, int32_t I, int32_t nblk) {
+  return (int64_t)nblk * (1024 / I) * B * I;
+}
+
+int fmd_grouped_linear_bwd(const float* x, int32_t B, int32_t I, const void* groups, const void* blocks,
+                           int32_t nblk, int32_t in_silu, const float* dy, int32_t dy_stride, float* dx,
+                           int32_t dx_acc, float* ws, fmd_stream_t s) {
+  if (B < 1 || B > 32 || (I != 128 && I != 256 && I != 512 && I != 1024)) return -1;
+  if ((size_t)(B * I + 64 * B) * 4 > 64 * 1024) return -1;
+  hipLaunchKernelGGL(glinear_bwd_kernel, dim3(nblk), dim3(256), (size_t)(B * I + 64 * B) * 4, (hipStream_t)s, x, B,
+                     I, (const GLGroup*)groups, (const int2*)blocks, in_silu, dy, dy_stride, ws);
+  int rc = (int)hipGetLastError();
+  if (rc || !dx) return rc;
+  hipLaunchKernelGGL(glinear_dx_reduce, dim3(grid_for((long long)B * I)), dim3(256), 0, (hipStream_t)s, ws,
+                     nblk * (1024 / I), B, I, x, in_silu, dx, dx_acc);
+  return (int)hipGetLastError();
 }
 
 int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t O, int32_t in_silu,

@@ -226,25 +226,74 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   }
 }
 
-__global__ void wgrad_reduce(const WArgs A, int splits) {
+// Stage 1 of a wide split-K reduction: group g sums slabs [g*Q, (g+1)*Q) into slab g*Q (in place:
+// every group writes only inside its own range).  16-byte loads, 4 independent chains.
+__global__ void wgrad_reduce_stage1(const WArgs A, int splits, int Q) {
   const fmd_wgrad_desc& d = A.d;
   const size_t per = (size_t)d.K * A.T * A.C;
-  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < per; idx += (size_t)gridDim.x * blockDim.x) {
-    // idx enumerates the reference layout [K][C][tap]
-    const int tap = (int)(idx % A.T);
-    const size_t kc = idx / A.T;
-    const int c = (int)(kc % A.C);
-    const int k = (int)(kc / A.C);
-    const size_t src = ((size_t)k * A.T + tap) * A.C + c;
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += d.ws[(size_t)s * per + src];
-    d.dw[idx] = d.accumulate ? d.dw[idx] + v : v;
+  const size_t nvec = per / 4;
+  const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int s0 = blockIdx.y * Q, s1 = min(splits, s0 + Q);
+  if (d.db && v < (size_t)d.K) {   // bias partials, same grouping
+    const float* wb = d.ws + (size_t)splits * per;
+    float b = 0.f;
+    for (int s = s0; s < s1; ++s) b += wb[(size_t)s * d.K + v];
+    ((float*)wb)[(size_t)s0 * d.K + v] = b;
+  }
+  if (v >= nvec) return;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    a0 += *(const f32x4*)(d.ws + (size_t)s * per + v * 4);
+    a1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * per + v * 4);
+    a2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * per + v * 4);
+    a3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * per + v * 4);
+  }
+  for (; s < s1; ++s) a0 += *(const f32x4*)(d.ws + (size_t)s * per + v * 4);
+  *(f32x4*)(d.ws + (size_t)s0 * per + v * 4) = (a0 + a1) + (a2 + a3);
+}
+
+// Sum the split-K slabs ws[s*sstride][k][tap][c] (s < nsl) and write the reference layout dW[k][c][tap];
+// db from the same (possibly pre-reduced) bias slabs.  One thread = 4 consecutive c of one (k, tap).
+__global__ void wgrad_reduce(const WArgs A, int splits, int nsl, int sstride) {
+  const fmd_wgrad_desc& d = A.d;
+  const size_t per = (size_t)d.K * A.T * A.C;
+  const size_t nvec = per / 4;   // C % 8 == 0
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {
+    const size_t src = v * 4;              // [k][tap][c]
+    const int c = (int)(src % A.C);
+    const size_t kt = src / A.C;
+    const int tap = (int)(kt % A.T);
+    const int k = (int)(kt / A.T);
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int s = 0;
+    for (; s + 4 <= nsl; s += 4) {
+      s0 += *(const f32x4*)(d.ws + (size_t)s * sstride * per + src);
+      s1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * sstride * per + src);
+      s2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * sstride * per + src);
+      s3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * sstride * per + src);
+    }
+    for (; s < nsl; ++s) s0 += *(const f32x4*)(d.ws + (size_t)s * sstride * per + src);
+    const f32x4 t = (s0 + s1) + (s2 + s3);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t o = ((size_t)k * A.C + c + e) * A.T + tap;
+      d.dw[o] = d.accumulate ? d.dw[o] + t[e] : t[e];
+    }
   }
   if (d.db) {
     const float* wb = d.ws + (size_t)splits * per;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < d.K; k += gridDim.x * blockDim.x) {
-      float v = 0.f;
-      for (int s = 0; s < splits; ++s) v += wb[(size_t)s * d.K + k];
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+      int s = 0;
+      for (; s + 4 <= nsl; s += 4) {
+        v0 += wb[(size_t)s * sstride * d.K + k];
+        v1 += wb[(size_t)(s + 1) * sstride * d.K + k];
+        v2 += wb[(size_t)(s + 2) * sstride * d.K + k];
+        v3 += wb[(size_t)(s + 3) * sstride * d.K + k];
+      }
+      for (; s < nsl; ++s) v0 += wb[(size_t)s * sstride * d.K + k];
+      const float v = (v0 + v1) + (v2 + v3);
       d.db[k] = d.accumulate ? d.db[k] + v : v;
     }
   }
@@ -288,8 +337,18 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   }
   if (rc) return rc;
   const size_t per = (size_t)d->K * A.T * A.C;
-  int blocks = (int)((per + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, A, splits);
+  const int vblocks = (int)((per / 4 + 255) / 256);
+  int nsl = splits, sstride = 1;
+  if (splits > 8) {   // two stages: enough threads in flight for a wide split
+    const int Q = 8;
+    sstride = Q;
+    nsl = (splits + Q - 1) / Q;
+    const int b1 = vblocks > (d->K + 255) / 256 ? vblocks : (d->K + 255) / 256;
+    hipLaunchKernelGGL(wgrad_reduce_stage1, dim3(b1, nsl), dim3(256), 0, s, A, splits, Q);
+    rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  int blocks = vblocks > 4096 ? 4096 : vblocks;
+  hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, A, splits, nsl, sstride);
   return (int)hipGetLastError();
 }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
+    "fmd_prep_weights_batch": [p, i32, i32, p],
     "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
     "fmd_nhwc_to_nchw": [p, i32, i32, i32, i32, i32, p, p],
     "fmd_sum_pool2": [p, i32, i32, i32, i32, p, i32, p],
@@ -62,6 +63,9 @@ SIGNATURES = {
     "fmd_linear": [p, i32, i32, p, p, i32, i32, p, i32, p],
     "fmd_linear_bwd": [p, i32, i32, p, i32, i32, p, i32, p, i32, p, p, p],
     "fmd_silu_bwd_f32": [p, p, p, i64, p],
+    "fmd_grouped_linear": [p, i32, i32, p, p, i32, i32, p, i32, p],
+    "fmd_grouped_linear_bwd_workspace": [i32, i32, i32],
+    "fmd_grouped_linear_bwd": [p, i32, i32, p, p, i32, i32, p, i32, p, i32, p, p],
     "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
     "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_noise_prepare": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
@@ -72,7 +76,7 @@ SIGNATURES = {
     "fmd_fill_from_table": [p, p, p, i32, p],
     "fmd_counter_add": [p, i32, p],
 }
-_RESTYPE = {"fmd_wgrad_workspace": i64, "fmd_halo_tiled_size": i64}
+_RESTYPE = {"fmd_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_grouped_linear_bwd_workspace": i64}
 
 _lib = None
 

@@ -77,73 +77,141 @@ def _gdest(a: Optional[Act]):
 
 
 class WeightCache:
-    """bf16 kernel-layout copies of the fp32 master weights, rebuilt when a weight changes."""
+    """bf16 kernel-layout copies of the fp32 master weights.
+
+    Entries are created lazily by the layers; after an optimizer step ``invalidate`` re-derives ALL of
+    them -- base layouts and halo tiles, directly from the fp32 masters -- in one batched launch
+    (fmd_prep_weights_batch), after refreshing the few fp32 derived buffers (padded biases, fused
+    q/k/v).  The device job table is rebuilt only when the set of entries or their storage changes."""
 
     def __init__(self):
         self._c = {}
         self._force = set()
+        self._jobs_key = None
+        self._jobs = None
+        self._nblk = 0
+
+    @staticmethod
+    def _ver(t):
+        return (t._version, t.data_ptr())
 
     def invalidate(self):
-        self._force = set(self._c.keys())
+        for key, e in self._c.items():          # fp32 derived buffers first: they feed the bf16 layouts
+            if e["kind"] == "pad":
+                e["buf"][: e["src"].numel()].copy_(e["src"].detach().reshape(-1))
+            elif e["kind"] == "fused":
+                o = 0
+                for w in e["src"]:
+                    e["buf"][o:o + w.shape[0]].copy_(w.detach())
+                    o += w.shape[0]
+        jobs = [(key, e) for key, e in self._c.items() if e["kind"] in ("prep", "tiled")]
+        if jobs:
+            self._launch_batch(jobs)
+        for key, e in self._c.items():
+            e["ver"] = self._ver(e["src"]) if e["kind"] != "fused" else tuple(self._ver(w) for w in e["src"])
+        self._force.clear()
+
+    def _launch_batch(self, jobs):
+        """One fmd_prep_weights_batch job per fp32 master: every layout of it from one read of each tile."""
+        key = tuple((e["src"].data_ptr(), e["buf"].data_ptr(), e["job"]) for _, e in jobs)
+        if key != self._jobs_key:
+            per_src = {}
+            for src_ptr, buf_ptr, job in key:
+                per_src.setdefault(src_ptr, []).append((buf_ptr, job))
+            rows, blk = [], 0
+            for src_ptr, outs in per_src.items():
+                for i in range(0, len(outs), 6):
+                    part = outs[i:i + 6]
+                    K, C, ks = part[0][1][:3]
+                    kp = cp = 0
+                    descs = []
+                    for buf_ptr, (_, _, _, mode, R, Cc, kind, _T, _n) in part:
+                        r_ext = -(-R // 128) * 128 if kind else R
+                        c_ext = -(-Cc // 64) * 64 if kind else Cc
+                        k_ext, c_ext2 = (r_ext, c_ext) if mode == 0 else (c_ext, r_ext)
+                        kp, cp = max(kp, k_ext), max(cp, c_ext2)
+                        descs += [buf_ptr, mode | (kind << 8) | (R << 16) | (Cc << 40)]
+                    kt, ct = -(-kp // 32), -(-cp // 32)
+                    row = [src_ptr, K | (C << 32), ks | (len(part) << 32), blk | (kt << 32)] + descs
+                    rows.append(row + [0] * (16 - len(row)))
+                    blk += kt * ct
+            dev = jobs[0][1]["buf"].device
+            self._jobs = torch.tensor(rows, dtype=torch.int64).to(dev)
+            self._njobs = len(rows)
+            self._nblk = blk
+            self._jobs_key = key
+        from .. import _lib as L
+        L.call("fmd_prep_weights_batch", self._jobs.data_ptr(), self._njobs, self._nblk, ops.stream())
+
+    def _fresh(self, key, src_ver):
+        e = self._c.get(key)
+        return e is not None and e["ver"] == src_ver and key not in self._force
 
     def get(self, w: torch.Tensor, mode: int, Kpad=None, Cpad=None):
         key = (id(w), mode, Kpad, Cpad)
-        ver = (w._version, w.data_ptr())
-        ent = self._c.get(key)
-        if ent is None or ent[0] != ver or key in self._force:
-            buf = ops.prep_weights(w.detach(), mode, Kpad, Cpad, out=None if ent is None else ent[1])
-            self._c[key] = (ver, buf)
+        if not self._fresh(key, self._ver(w)):
+            e = self._c.get(key)
+            buf = ops.prep_weights(w.detach(), mode, Kpad, Cpad, out=None if e is None else e["buf"])
+            K, C = w.shape[0], w.shape[1]
+            ks = w.shape[2] if w.dim() == 4 else 1
+            R, T, Cc = buf.shape
+            self._c[key] = dict(kind="prep", src=w, buf=buf, ver=self._ver(w),
+                                job=(K, C, ks, mode, R, Cc, 0, T, buf.numel()))
             self._force.discard(key)
-        return self._c[key][1]
+        return self._c[key]["buf"]
 
     def tiled(self, w: torch.Tensor, mode: int, Kpad=None, Cpad=None):
         """Halo-kernel tiling of ``get(w, mode, ...)`` (csrc/conv_halo.hip)."""
-        base = self.get(w, mode, Kpad, Cpad)
         key = (id(w), "tiled", mode, Kpad, Cpad)
-        ver = (w._version, w.data_ptr())
-        ent = self._c.get(key)
-        if ent is None or ent[0] != ver or key in self._force:
-            buf = ops.tile_weights(base, out=None if ent is None else ent[1])
-            self._c[key] = (ver, buf)
+        if not self._fresh(key, self._ver(w)):
+            base = self.get(w, mode, Kpad, Cpad)
+            e = self._c.get(key)
+            buf = ops.tile_weights(base, out=None if e is None else e["buf"])
+            K, C = w.shape[0], w.shape[1]
+            ks = w.shape[2] if w.dim() == 4 else 1
+            R, T, Cc = base.shape
+            self._c[key] = dict(kind="tiled", src=w, buf=buf, ver=self._ver(w),
+                                job=(K, C, ks, mode, R, Cc, 1, T, buf.numel()))
             self._force.discard(key)
-        return self._c[key][1]
+        return self._c[key]["buf"]
 
     def padded(self, v: torch.Tensor, n: int):
         key = (id(v), "pad", n)
-        ver = (v._version, v.data_ptr())
-        ent = self._c.get(key)
-        if ent is None or ent[0] != ver or key in self._force:
-            buf = ent[1] if ent is not None else torch.zeros(n, device=v.device, dtype=F32)
+        if not self._fresh(key, self._ver(v)):
+            e = self._c.get(key)
+            buf = e["buf"] if e is not None else torch.zeros(n, device=v.device, dtype=F32)
             buf[: v.numel()].copy_(v.detach().reshape(-1))
-            self._c[key] = (ver, buf)
+            self._c[key] = dict(kind="pad", src=v, buf=buf, ver=self._ver(v))
             self._force.discard(key)
-        return self._c[key][1]
+        return self._c[key]["buf"]
 
     def fused(self, ws, key_name):
         """Concatenate several fp32 tensors along dim 0 (fused q/k/v projection)."""
         key = (tuple(id(w) for w in ws), key_name)
-        ver = tuple((w._version, w.data_ptr()) for w in ws)
-        ent = self._c.get(key)
-        if ent is None or ent[0] != ver or key in self._force:
-            buf = ent[1] if ent is not None else torch.empty((sum(w.shape[0] for w in ws), *ws[0].shape[1:]),
+        ver = tuple(self._ver(w) for w in ws)
+        if not self._fresh(key, ver):
+            e = self._c.get(key)
+            buf = e["buf"] if e is not None else torch.empty((sum(w.shape[0] for w in ws), *ws[0].shape[1:]),
                                                              device=ws[0].device, dtype=F32)
             o = 0
             for w in ws:
                 buf[o:o + w.shape[0]].copy_(w.detach())
                 o += w.shape[0]
-            self._c[key] = (ver, buf)
+            self._c[key] = dict(kind="fused", src=list(ws), buf=buf, ver=ver)
             self._force.discard(key)
-        return self._c[key][1]
+        return self._c[key]["buf"]
 
 
 class Ctx:
-    __slots__ = ("emb", "demb", "tape", "N")
+    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all")
 
     def __init__(self, emb, save, N):
         self.emb = emb
         self.demb = torch.zeros_like(emb) if save else None
         self.tape: Optional[List] = [] if save else None
         self.N = N
+        self.eo_all = None      # [N][sum O] grouped emb projections of all ResBlocks
+        self.demb_all = None
 
 
 def _check_conv(c: Conv, ks, stride, pad):
@@ -165,6 +233,18 @@ class UNetEngine:
         else:
             raise TypeError(type(model))
         self.wc = WeightCache()
+        self.gl, self.gl_slot = self._group_emb_layers(model)
+
+    @staticmethod
+    def _group_emb_layers(model):
+        """ResBlocks whose emb projection feeds the block (scale-shift or added embedding) share one
+        grouped launch; a mixed emb_activation_before_proj keeps the per-block path."""
+        blocks = [mod for mod in model.modules() if isinstance(mod, ResBlockND)
+                  and (mod.use_scale_shift_norm or mod.add_embedding_to_hidden)]
+        if not blocks or len({bool(b.emb_activation_before_proj) for b in blocks}) != 1:
+            return None, {}
+        gl = ops.GroupedLinear([b.emb_layers for b in blocks], blocks[0].emb_activation_before_proj)
+        return gl, {id(b): (gl.off[i], gl.O[i]) for i, b in enumerate(blocks)}
 
     @property
     def m(self):
@@ -242,16 +322,22 @@ class UNetEngine:
         _check_conv(c2, 3, 1, 1)
         g1, g2 = m.norm1, m.norm2
         el = m.emb_layers
-        eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
         ss = m.use_scale_shift_norm
         add = (not ss) and m.add_embedding_to_hidden
+        slot = self.gl_slot.get(id(m)) if ctx.eo_all is not None else None
+        if slot is not None:   # view into the grouped projection (row stride = gl.total)
+            eo = ctx.eo_all[:, slot[0]:slot[0] + slot[1]]
+            es = self.gl.total
+        else:
+            eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
+            es = eo.shape[1]
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         h, hst = ops.conv(x0.t, Cout, self.wc.get(c1.weight, 0), src1=x1.t if x1 else None, pro=(a1, b1, True),
-                          bias=c1.bias, bias_nc=eo if add else None, want_stats=True,
+                          bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=True,
                           wgt_tiled=self.wc.tiled(c1.weight, 0))
         if ss:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
-                                      emb_stride=2 * Cout, emb_mode=1)
+                                      emb_stride=es, emb_mode=1)
         else:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias)
         sk = m.skip_connection
@@ -281,14 +367,18 @@ class UNetEngine:
                 extra, _ = ops.conv(dy, Cin, self.wc.get(sc.weight, 1), ks=1, pad=0, transposed=True,
                                     out_hw_=(H, W))
             dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, H, W, ep=(h, None, a2, b2), want_stats=True)
-            demb = torch.empty_like(eo)
+            if slot is not None:
+                demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
+            else:
+                demb = torch.empty_like(eo)
+                ds_ = demb.shape[1]
             if ss:
                 P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
-                                             g2.bias.grad, emb=eo, emb_stride=2 * Cout, emb_mode=1, demb=demb,
-                                             demb_stride=2 * Cout)
+                                             g2.bias.grad, emb=eo, emb_stride=es, emb_mode=1, demb=demb,
+                                             demb_stride=ds_)
             elif add:
                 P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
-                                             g2.bias.grad, emb_mode=2, demb=demb, demb_stride=Cout, fwd=hst)
+                                             g2.bias.grad, emb_mode=2, demb=demb, demb_stride=ds_, fwd=hst)
             else:
                 P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
                                              g2.bias.grad)
@@ -303,7 +393,7 @@ class UNetEngine:
             d0, acc0 = _gdest(x0)
             d1, acc1 = _gdest(x1)
             ops.gn_bwd_apply(dz1, x0.t, x1.t if x1 else None, P1, Q1, R1, extra, d0, acc0, d1, acc1)
-            if ss or add:
+            if (ss or add) and slot is None:
                 ops.linear_bwd(ctx.emb, el.weight, demb, el.weight.grad, el.bias.grad, dx=ctx.demb, dx_acc=True,
                                in_silu=m.emb_activation_before_proj)
         ctx.tape.append(bwd)
@@ -398,12 +488,20 @@ class UNetEngine:
         h1 = ops.linear(feats, l1.weight, l1.bias)
         emb = ops.linear(h1, l2.weight, l2.bias, in_silu=True)
         ctx = Ctx(emb, ctx_save, N)
+        if self.gl is not None:
+            ctx.eo_all = self.gl.forward(emb)
         if ctx.tape is not None:
             def bwd():
                 dh1 = torch.empty_like(h1)
                 ops.linear_bwd(h1, l2.weight, ctx.demb, l2.weight.grad, l2.bias.grad, dx=dh1, in_silu=True)
                 ops.linear_bwd(feats, l1.weight, dh1, l1.weight.grad, l1.bias.grad)
             ctx.tape.append(bwd)
+            if self.gl is not None:
+                ctx.demb_all = torch.zeros_like(ctx.eo_all)
+
+                def gbwd():   # runs after every ResBlock wrote its demb slice, before the time MLP backward
+                    self.gl.backward(emb, ctx.demb_all, dx=ctx.demb, dx_acc=True)
+                ctx.tape.append(gbwd)
         return ctx
 
     # ---------------------------------------------------------------- model

@@ -293,6 +293,66 @@ def linear_bwd(x, w, dy, dw, db, dx=None, dx_acc=False, in_silu=False, dy_stride
               int(dx_acc), _p(dw), _p(db), stream())
 
 
+class GroupedLinear:
+    """Every ResBlock ``emb_layers`` projection (residual.py:63-68) of a UNet as one launch each way
+    (csrc/misc.hip glinear_*): outputs are concatenated [B][sum O]; group g owns columns
+    [off_g, off_g + O_g).  The device descriptor table is rebuilt only when a parameter or gradient
+    storage moves (never during hipGraph capture once warmed up)."""
+
+    ROWS = 64
+
+    def __init__(self, linears, in_silu: bool):
+        self.linears = list(linears)
+        self.in_silu = bool(in_silu)
+        self.O = [int(l.weight.shape[0]) for l in self.linears]
+        self.I = int(self.linears[0].weight.shape[1])
+        self.off = []
+        o = 0
+        for n in self.O:
+            self.off.append(o)
+            o += n
+        self.total = o
+        self.blocks_host = [(g, r0) for g, n in enumerate(self.O) for r0 in range(0, n, self.ROWS)]
+        self._key = None
+        self._groups = None
+        self._blocks = None
+
+    def _table(self, dev):
+        key = tuple((l.weight.data_ptr(), l.bias.data_ptr() if l.bias is not None else 0,
+                     l.weight.grad.data_ptr() if l.weight.grad is not None else 0,
+                     l.bias.grad.data_ptr() if (l.bias is not None and l.bias.grad is not None) else 0)
+                    for l in self.linears)
+        if key != self._key:
+            rows = [[w, b, gw, gb, n, off] for (w, b, gw, gb), n, off in zip(key, self.O, self.off)]
+            self._groups = torch.tensor(rows, dtype=torch.int64).to(dev)
+            self._blocks = torch.tensor(self.blocks_host, dtype=torch.int32).to(dev)
+            self._key = key
+        return self._groups, self._blocks
+
+    def forward(self, x):
+        _need_cuda(x, "GroupedLinear")
+        B = x.shape[0]
+        x = x.contiguous()
+        g, blk = self._table(x.device)
+        y = torch.empty((B, self.total), device=x.device, dtype=F32)
+        _lib.call("fmd_grouped_linear", _p(x), B, self.I, _p(g), _p(blk), blk.shape[0], int(self.in_silu), _p(y),
+                  self.total, stream())
+        return y
+
+    def backward(self, x, dy, dx=None, dx_acc=False):
+        for l in self.linears:
+            if l.weight.grad is None:
+                l.weight.grad = torch.zeros_like(l.weight)
+            if l.bias is not None and l.bias.grad is None:
+                l.bias.grad = torch.zeros_like(l.bias)
+        B = x.shape[0]
+        g, blk = self._table(x.device)
+        nws = int(_lib.lib().fmd_grouped_linear_bwd_workspace(B, self.I, blk.shape[0]))
+        ws = torch.empty((nws,), device=x.device, dtype=F32)
+        _lib.call("fmd_grouped_linear_bwd", _p(x.contiguous()), B, self.I, _p(g), _p(blk), blk.shape[0],
+                  int(self.in_silu), _p(dy), self.total, _p(dx), int(dx_acc), _p(ws), stream())
+
+
 def silu_bwd(x, dy):
     dx = torch.empty_like(x)
     _lib.call("fmd_silu_bwd_f32", _p(x), _p(dy), _p(dx), x.numel(), stream())

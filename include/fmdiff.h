@@ -134,6 +134,12 @@ int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0,
  * [Cpad][16][Kpad] data gradient of nearest-x2 upsample + 3x3 conv (4x4 taps). */
 int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t Kpad, int32_t Cpad,
                      void* out, fmd_stream_t s);
+/* All bf16 weight layouts of a model in one launch (after each optimizer step).  jobs: device int64
+ * [njobs][16], one per fp32 master w[K][C][ks*ks] = {w, K | C<<32, ks | nout<<32, first block | ktiles<<32,
+ * then nout (<= 6) pairs {out, mode | kind<<8 | R<<16 | Cc<<40}}; kind 0 = the fmd_prep_weights layout
+ * (R rows x T x Cc), kind 1 = its halo tiles.  A block covers a 32x32 (k, c) tile of one master; jobs
+ * sorted by first block; nblocks = total. */
+int fmd_prep_weights_batch(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s);
 int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s);
 int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
                      fmd_stream_t s);
@@ -152,6 +158,16 @@ int fmd_linear(const float* x, int32_t B, int32_t I, const float* w, const float
 int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t O, int32_t in_silu,
                    const float* dy, int32_t dy_stride, float* dx, int32_t dx_acc, float* dw, float* db,
                    fmd_stream_t s);
+/* Grouped linears: every ResBlock emb_layers projection of the UNet in one launch.  groups: device
+ * array of {const float* w; const float* b; float* dw; float* db; int64 O; int64 off} (row offset of the
+ * group in y / dy); blocks: device int2 array {group, first row} of 64-row blocks.  The backward
+ * accumulates dW/db (+=) and writes / accumulates dx (with SiLU' when in_silu). */
+int fmd_grouped_linear(const float* x, int32_t B, int32_t I, const void* groups, const void* blocks, int32_t nblk,
+                       int32_t in_silu, float* y, int32_t y_stride, fmd_stream_t s);
+int64_t fmd_grouped_linear_bwd_workspace(int32_t B, int32_t I, int32_t nblk);
+int fmd_grouped_linear_bwd(const float* x, int32_t B, int32_t I, const void* groups, const void* blocks,
+                           int32_t nblk, int32_t in_silu, const float* dy, int32_t dy_stride, float* dx,
+                           int32_t dx_acc, float* ws, fmd_stream_t s);
 int fmd_silu_bwd_f32(const float* x, const float* dy, float* dx, int64_t n, fmd_stream_t s);
 
 /* ----------------------------------------------------------- attention

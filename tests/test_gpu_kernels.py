@@ -342,3 +342,58 @@ def test_halo_conv_matches_generic(case):
         ta = sa.slab.view(N, -1, K, 2).sum(1)
         tb = sb.slab.view(N, -1, K, 2).sum(1)
         torch.testing.assert_close(ta, tb, rtol=2e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("in_silu", [False, True])
+def test_grouped_linear_vs_torch(in_silu):
+    """fmd_grouped_linear(_bwd): several emb projections (O = 256, 1024, 128) in one launch each way."""
+    O = ops()
+    torch.manual_seed(5)
+    B, I = 8, 512
+    lins = [torch.nn.Linear(I, n).to(DEV) for n in (256, 1024, 128)]
+    x = torch.randn(B, I, device=DEV)
+    gl = O.GroupedLinear(lins, in_silu)
+    y = gl.forward(x)
+    xr = x.clone().requires_grad_()
+    xin = F.silu(xr) if in_silu else xr
+    refs = [l(xin) for l in lins]
+    torch.testing.assert_close(y, torch.cat(refs, 1), rtol=1e-4, atol=1e-4)
+    dy = torch.randn_like(y)
+    torch.autograd.backward(refs, [dy[:, o:o + n] for o, n in zip(gl.off, gl.O)])
+    want_w = [l.weight.grad.clone() for l in lins]
+    want_b = [l.bias.grad.clone() for l in lins]
+    for l in lins:
+        l.weight.grad = torch.full_like(l.weight, 0.5)   # backward accumulates
+        l.bias.grad = torch.full_like(l.bias, 0.25)
+    dx = torch.ones(B, I, device=DEV)
+    gl.backward(x, dy, dx=dx, dx_acc=True)
+    torch.testing.assert_close(dx, xr.grad + 1, rtol=1e-4, atol=1e-4)
+    for l, w, b in zip(lins, want_w, want_b):
+        torch.testing.assert_close(l.weight.grad, w + 0.5, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(l.bias.grad, b + 0.25, rtol=1e-4, atol=1e-4)
+
+
+def test_weight_cache_batched_refresh_matches_individual_preps():
+    """fmd_prep_weights_batch (one launch, all layouts from the fp32 masters) == the per-weight
+    fmd_prep_weights / fmd_tile_weights_halo results, bit for bit."""
+    from fmdiff.runtime.engine import WeightCache
+    torch.manual_seed(3)
+    wc = WeightCache()
+    ws = [torch.randn(128, 128, 3, 3, device=DEV), torch.randn(256, 384, 3, 3, device=DEV),
+          torch.randn(1, 128, 3, 3, device=DEV), torch.randn(512, 256, 1, 1, device=DEV),
+          torch.randn(256, 256, 3, 3, device=DEV), torch.randn(768, 512, 1, device=DEV)]
+    want = {}
+    reqs = [(0, 0, None, None), (0, 3, None, None), (0, 1, None, None), (1, 0, None, None), (1, 3, None, None),
+            (2, 0, 8, None), (2, 3, 8, None), (3, 0, None, None), (3, 1, None, None), (4, 2, None, None),
+            (4, 0, None, None), (5, 0, None, None)]
+    for wi, mode, kp, cp in reqs:
+        want[("b", wi, mode, kp)] = wc.get(ws[wi], mode, kp, cp).clone()
+        if mode in (0, 3) and ws[wi].dim() == 4 and ws[wi].shape[-1] == 3:
+            want[("t", wi, mode, kp)] = wc.tiled(ws[wi], mode, kp, cp).clone()
+    for e in wc._c.values():
+        e["buf"].zero_()
+    wc.invalidate()
+    torch.cuda.synchronize()
+    for (kind, wi, mode, kp), ref in want.items():
+        got = wc.get(ws[wi], mode, kp, None) if kind == "b" else wc.tiled(ws[wi], mode, kp, None)
+        assert torch.equal(got, ref), (kind, wi, mode, kp)
