@@ -253,49 +253,41 @@ __global__ void wgrad_reduce_stage1(const WArgs A, int splits, int Q) {
   *(f32x4*)(d.ws + (size_t)s0 * per + v * 4) = (a0 + a1) + (a2 + a3);
 }
 
-// Sum the split-K slabs ws[s*sstride][k][tap][c] (s < nsl) and write the reference layout dW[k][c][tap];
-// db from the same (possibly pre-reduced) bias slabs.  One thread = 4 consecutive c of one (k, tap).
-__global__ void wgrad_reduce(const WArgs A, int splits, int nsl, int sstride) {
+// Sum the split-K slabs ws[s*sstride][k][tap][c] (s < nsl) and write the reference layout dW[k][c][tap]
+// (+ db from the same, possibly pre-reduced, bias slabs).  A block owns (k, 64 channels): it reads
+// [tap][64 c] runs and writes the contiguous dW[k][c0:c0+64][:] run through LDS.
+constexpr int RC = 64;
+
+__global__ __launch_bounds__(256) void wgrad_reduce(const WArgs A, int splits, int nsl, int sstride) {
   const fmd_wgrad_desc& d = A.d;
+  __shared__ float res[RC * 25 + 1];   // [c][tap], T <= 25
   const size_t per = (size_t)d.K * A.T * A.C;
-  const size_t nvec = per / 4;   // C % 8 == 0
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {
-    const size_t src = v * 4;              // [k][tap][c]
-    const int c = (int)(src % A.C);
-    const size_t kt = src / A.C;
-    const int tap = (int)(kt % A.T);
-    const int k = (int)(kt / A.T);
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+  const int k = blockIdx.x, c0 = blockIdx.y * RC;
+  const int nc = min(RC, A.C - c0);
+  const int n = A.T * RC;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int tap = e / RC, cl = e - tap * RC;
+    if (cl >= nc) continue;
+    const size_t src = ((size_t)k * A.T + tap) * A.C + c0 + cl;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     int s = 0;
     for (; s + 4 <= nsl; s += 4) {
-      s0 += *(const f32x4*)(d.ws + (size_t)s * sstride * per + src);
-      s1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * sstride * per + src);
-      s2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * sstride * per + src);
-      s3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * sstride * per + src);
+      v0 += d.ws[(size_t)s * sstride * per + src];
+      v1 += d.ws[(size_t)(s + 1) * sstride * per + src];
+      v2 += d.ws[(size_t)(s + 2) * sstride * per + src];
+      v3 += d.ws[(size_t)(s + 3) * sstride * per + src];
     }
-    for (; s < nsl; ++s) s0 += *(const f32x4*)(d.ws + (size_t)s * sstride * per + src);
-    const f32x4 t = (s0 + s1) + (s2 + s3);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const size_t o = ((size_t)k * A.C + c + e) * A.T + tap;
-      d.dw[o] = d.accumulate ? d.dw[o] + t[e] : t[e];
-    }
+    for (; s < nsl; ++s) v0 += d.ws[(size_t)s * sstride * per + src];
+    res[cl * A.T + tap] = (v0 + v1) + (v2 + v3);
   }
-  if (d.db) {
+  __syncthreads();
+  float* out = d.dw + ((size_t)k * A.C + c0) * A.T;
+  for (int e = threadIdx.x; e < nc * A.T; e += blockDim.x) out[e] = d.accumulate ? out[e] + res[e] : res[e];
+  if (d.db && blockIdx.y == 0 && threadIdx.x == 0) {
     const float* wb = d.ws + (size_t)splits * per;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < d.K; k += gridDim.x * blockDim.x) {
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-      int s = 0;
-      for (; s + 4 <= nsl; s += 4) {
-        v0 += wb[(size_t)s * sstride * d.K + k];
-        v1 += wb[(size_t)(s + 1) * sstride * d.K + k];
-        v2 += wb[(size_t)(s + 2) * sstride * d.K + k];
-        v3 += wb[(size_t)(s + 3) * sstride * d.K + k];
-      }
-      for (; s < nsl; ++s) v0 += wb[(size_t)s * sstride * d.K + k];
-      const float v = (v0 + v1) + (v2 + v3);
-      d.db[k] = d.accumulate ? d.db[k] + v : v;
-    }
+    float v = 0.f;
+    for (int s = 0; s < nsl; ++s) v += wb[(size_t)s * sstride * d.K + k];
+    d.db[k] = d.accumulate ? d.db[k] + v : v;
   }
 }
 
@@ -348,7 +340,7 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
     if (rc) return rc;
   }
-  int blocks = vblocks > 4096 ? 4096 : vblocks;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(blocks), dim3(256), 0, s, A, splits, nsl, sstride);
+  if (A.T > 25) return -4;
+  hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl, sstride);
   return (int)hipGetLastError();
 }
