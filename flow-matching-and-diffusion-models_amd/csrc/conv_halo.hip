@@ -1,21 +1,25 @@
 // Halo-tiled 3x3 stride-1 convolution for gfx950 -- the UNet's dominant problem.
 //
 // Workgroup = 512 threads (8 waves) computing a 16x16-pixel x 128-output-channel
-// tile.  Per 64-channel chunk of the input, the (16+2)x(16+2) halo of the tile is
-// gathered ONCE (GroupNorm affine + SiLU applied once per element, zero padding,
-// optional nearest-x2 upsample = a 10x10 low-resolution halo, optional two-source
-// concat) into LDS, and all 9 taps read their shifted 16-pixel rows from that
-// single image: 9x less gather/transform work and ~7x less activation traffic
-// than a per-tap implicit GEMM.  Per tap, a 128x64 weight slice streams through
-// a double-buffered LDS tile (weights are pre-tiled in HBM by fmd_prep_weights
-// mode 4, so each slice is one contiguous 16 KiB block); the next chunk's halo
-// is gathered in 9 pieces behind the current chunk's MFMAs, one barrier per tap.
+// tile; two workgroups share a CU (76 KiB of LDS each), so one workgroup's
+// staging, barriers, prologue and epilogue overlap the other's MFMAs.  Per
+// 32-channel chunk of the input, the (16+2)x(16+2) halo of the tile is gathered
+// ONCE (GroupNorm affine + SiLU applied once per element, zero padding, optional
+// nearest-x2 upsample = a 10x10 low-resolution halo, optional two-source concat)
+// into LDS, and all 9 taps read their shifted 16-pixel rows from that single
+// image: 9x less gather/transform work and ~7x less activation traffic than a
+// per-tap implicit GEMM.  Per tap, a 128x32 weight slice (pre-tiled in HBM by
+// fmd_prep_weights_batch / fmd_tile_weights_halo, so each slice is one
+// contiguous 8 KiB block) is copied global -> LDS by DMA into a double-buffered
+// pair of tiles; two taps per step, one barrier per step, and the next chunk's
+// halo is gathered in 4 pieces behind the current chunk's MFMAs.
 //
-// LDS images are chunk-major ([16-byte k-chunk plane][row]): an MFMA fragment
-// read touches 16 consecutive rows of one plane = one 256-byte bank row, so
-// every ds_read_b128 is conflict-free for any row offset (tap shifts); planes
-// are padded to 338 rows so the 16-byte writes of one position's chunks land
-// in distinct banks.
+// LDS images are chunk-major ([16-byte k-chunk plane][row], plane stride 336
+// rows == 0 mod 16): an MFMA fragment read is 16 consecutive rows of one plane
+// per 16-lane group, so every ds_read_b128 lane group of gfx950 touches 16
+// distinct 16-byte bank slots for any tap shift.  Staging lanes are mapped
+// 8 consecutive positions per channel group, so the 8-lane groups of
+// ds_write_b128 are conflict-free too.
 //
 // Same epilogue contract as csrc/conv.hip (bias, per-sample bias, residual,
 // second 1x1 GEMM over src2|src3, data-gradient SiLU' + GN-backward sums,
@@ -27,13 +31,15 @@ namespace {
 
 constexpr int TH = 16, TW = 16;           // output tile
 constexpr int BCO = 128;                  // output channels per tile
-constexpr int BK = 64;                    // input channels per chunk
-constexpr int KC = BK / 8;                // 16-byte chunks per position
+constexpr int BK = FMD_HALO_BK;           // input channels per chunk (32)
+constexpr int KC = BK / 8;                // 16-byte chunks per position (4)
 constexpr int NT = 512;
 constexpr int HALO = (TH + 2) * (TW + 2); // 324 positions
-constexpr int HPAD = 338;                 // plane stride (rows): 338*16 B == 32 mod 128
-constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer
-constexpr int WBUF = KC * BCO * 8;        // bf16 elements per weight buffer (16 KiB)
+constexpr int HPAD = 336;                 // plane stride (rows): == 0 mod 16 bank slots
+constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer (21 KiB)
+constexpr int WBUF = KC * BCO * 8;        // bf16 elements per weight tile (8 KiB = one 16 B DMA per thread)
+static_assert(WBUF == NT * 8, "one weight DMA per thread");
+static_assert(2 * HBUF + 4 * WBUF >= TH * TW * BCO, "epilogue tile fits in the staging LDS");
 
 struct HArgs {
   fmd_conv_desc d;
@@ -49,25 +55,65 @@ struct HArgs {
 constexpr int TRACE_WG = 16, TRACE_STEPS = 40, TRACE_PH = 4;
 static unsigned long long* g_trace = nullptr;
 
+// staged piece h (16 bytes) of a chunk: blocks of 32 = 8 consecutive positions x KC channel groups
+FMD_DEV int piece_pos(int h) { return (h >> 5) * 8 + (h & 7); }
+FMD_DEV int piece_kc(int h) { return (h >> 3) & (KC - 1); }
+
+// LDS (one __shared__ object, so hipcc's LDS-DMA wait tracking sees a single staging array):
+//   [2 halo buffers][4 weight tiles][GN affine table a[C] | b[C]][epilogue bias | ep_a | ep_b of the tile]
+constexpr int CMAX = 512;                              // widest GN-prologue input the affine table holds
+constexpr int SM_H = 0;
+constexpr int SM_W = SM_H + 2 * HBUF * 2;              // bytes
+constexpr int SM_COEF = SM_W + 4 * WBUF * 2;
+constexpr int SM_EPI = SM_COEF + 2 * CMAX * 4;
+constexpr int SM_BYTES = SM_EPI + 3 * BCO * 4;
+static_assert(SM_BYTES <= 163840 / 2, "two workgroups per CU");
+
+// end of a pipeline step: this wave's weight DMAs (and, if keep == 0, its halo prefetch) have
+// landed and its LDS stores are done; then the workgroup barrier.  Raw s_barrier: __syncthreads()
+// would drain the halo prefetch that is meant to stay in flight across the barrier.
+template <int KEEP>
+FMD_DEV void step_barrier() {
+  if (KEEP) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16-byte LDS-DMA (global_load_lds_dwordx4) issued through inline asm: hipcc neither counts it nor
+// makes later ds_reads wait for it (its builtin form drains vmcnt before every following LDS read),
+// so the pipeline's own counted waits in step_barrier() are the only ones.  lds_dst: wave-uniform
+// LDS byte address; lane i lands at lds_dst + 16 i.
+FMD_DEV void glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
 template <bool UP, int PRO>
-__global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo(const HArgs A) {
   constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
-  constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk
-  constexpr int TOT1 = KC * HPOS;                          // 16-byte pieces of a main chunk
-  constexpr int PC1 = ((TOT1 + 3) / 4 + 7) & ~7;           // pieces staged per step (4 staging steps per chunk)
-  constexpr int LPT = (PC1 + NT - 1) / NT;                 // loads per thread per staging step (2 | 1)
+  constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk (100 | 324)
+  constexpr int TOT1 = ((HPOS + 7) / 8) * 8 * KC;          // staged pieces of a main chunk
+  constexpr int PC1 = ((TOT1 + 3) / 4 + 31) & ~31;         // pieces staged per step (4 staging steps per chunk)
+  constexpr int LPT = (PC1 + NT - 1) / NT;                 // loads per thread per staging step (1)
   constexpr int LPRO = (TOT1 + NT - 1) / NT;               // loads per thread for the prologue's full chunk
-  __shared__ __attribute__((aligned(16))) bf16r lds[2 * HBUF + 4 * WBUF];   // 2 halo + 2x2 weight tiles
-  bf16r* hbuf = lds;
-  bf16r* wbuf = lds + 2 * HBUF;
+  constexpr int SEG2 = TH * TW * KC;                       // pieces of a 1x1 chunk (1024)
+  static_assert(LPT == 1, "one staged piece per thread and step");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+  bf16r* const lds = (bf16r*)smem;
+  bf16r* const hbuf = (bf16r*)(smem + SM_H);
+  bf16r* const wbuf = (bf16r*)(smem + SM_W);
+  float* const coef = (float*)(smem + SM_COEF);
+  float* const epi = (float*)(smem + SM_EPI);   // [3][BCO]: summed bias, ep_a, ep_b of this tile's couts
+  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
 
   const fmd_conv_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid >> 2, wpx = wid & 3;   // 2 x 4 waves: 64 couts x 4 pixel rows each
   const int l16 = lane & 15, lq = lane >> 4;
-  const int kc = tid & (KC - 1);             // staged pieces start at multiples of 8: the 16-byte channel group is fixed
-  const int tp = tid >> 3;                   // position of this thread within a piece
+  const int kc = piece_kc(tid);              // staged pieces start at multiples of 32: the channel group is fixed
 
   const int per_img = A.tiles_x * A.tiles_y;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -86,17 +132,24 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
   const int nchunks = A.nchunk1 + A.nchunk2;
 
-  // pixel index of every halo position of a main chunk (-1: zero padding); 32-bit offsets
-  // (N*H*W*C < 2^31 is checked on the host).  Written once, read by the stagers of every chunk.
-  __shared__ int pixtab[HPOS];
-  for (int pos = tid; pos < HPOS; pos += NT) {
-    const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-    const int y = hy0 + py, x = hx0 + px;
-    pixtab[pos] = (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? (n * d.Hs + y) * d.Ws + x : -1;
+  // the GN affine of image n for every input channel, and the epilogue's per-cout vectors
+  if (PRO != 0) {
+    for (int i = tid; i < 2 * A.C; i += NT)
+      coef[i] = i < A.C ? d.pro_a[(size_t)n * A.C + i] : d.pro_b[(size_t)n * A.C + (i - A.C)];
   }
-  __syncthreads();
+  if (tid < BCO) {
+    const int co = co0 + tid;
+    const bool ok = co < d.K;
+    float bsum = 0.f;
+    if (ok && d.bias) bsum += d.bias[co];
+    if (ok && d.bias2) bsum += d.bias2[co];
+    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)n * d.K + co];
+    epi[tid] = bsum;
+    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)n * d.K + co] : 0.f;
+    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)n * d.K + co] : 0.f;
+  }
 
-  // ---- weights: one contiguous 16 KiB tile per step, copied global -> LDS by the DMA path
+  // ---- weights: one contiguous 8 KiB tile per tap, copied global -> LDS by the DMA path
   // slot = tap index over the whole reduction: 9 per 3x3 chunk, then 1 per 1x1 chunk; wtile = 0..3
   auto load_w = [&](int slot, int wtile) {
     const bf16r* src;
@@ -105,20 +158,17 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
     } else {
       src = A.wt2 + ((size_t)tco * A.nchunk2 + (slot - A.nchunk1 * 9)) * WBUF;
     }
-    bf16r* dst = wbuf + wtile * WBUF + wid * 64 * 8;
-    __builtin_amdgcn_global_load_lds((const void*)(src + tid * 8), (__attribute__((address_space(3))) void*)dst,
-                                     16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + (tid + NT) * 8),
-                                     (__attribute__((address_space(3))) void*)(dst + NT * 8), 16, 0, 0);
+    const unsigned dst = lds_base + SM_W + (unsigned)(wtile * WBUF + wid * 64 * 8) * 2;
+    glds16(src + tid * 8, __builtin_amdgcn_readfirstlane(dst));
   };
 
   // ---- halo staging through registers (the GN/SiLU transform happens between load and LDS store)
-  constexpr int LMAX = 9;
+  constexpr int LMAX = LPRO > 2 ? LPRO : 2;
   u32x4 rh[LMAX];
   int hoff[LMAX];            // LDS element offset; -1: no store; bit 30: store zeros (padding)
-  float ca[8], cb[8];        // GN affine of this thread's 8 channels of the chunk being staged
   const bf16r* cbase = s0;   // this thread's channel group of the chunk being staged
   int cs = 0;                // its pixel stride
+  int cch = 0;               // its first channel (GN affine table index)
   bool cok = false;
 
   auto setup = [&](int chunk) {
@@ -127,37 +177,57 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
       cok = c < A.C;
       cbase = !cok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
       cs = (c < d.C0) ? d.C0 : d.C1;
-      if (PRO != 0) {
-        const int cc = cok ? c : 0;
-        const f32x4* pa = (const f32x4*)(d.pro_a + (size_t)n * A.C + cc);
-        const f32x4* pb = (const f32x4*)(d.pro_b + (size_t)n * A.C + cc);
-        const f32x4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { ca[e] = a0[e]; ca[4 + e] = a1[e]; cb[e] = b0[e]; cb[4 + e] = b1[e]; }
-      }
+      cch = cok ? c : 0;
     } else {
       const int c = (chunk - A.nchunk1) * BK + kc * 8;
       cok = c < A.C23;
       cbase = !cok ? s2 : (c < d.C2) ? s2 + c : s3 + (c - d.C2);
       cs = (c < d.C2) ? d.C2 : d.C3;
+      cch = 0;
     }
   };
-  auto load_main = [&](int k, int h, bool act) {   // h: piece index (multiple-of-8 base + tid)
-    const int pos = act ? h >> 3 : 0;
-    const int pix = pixtab[pos];
-    const bool valid = pix >= 0 && cok;
-    rh[k] = *(const u32x4*)(cbase + (valid ? pix : 0) * cs);
-    hoff[k] = !act ? -1 : ((kc * HPAD + pos) * 8) | (valid ? 0 : (1 << 30));
+  // address + LDS destination of staged piece h (main chunk: halo position; 1x1 chunk: interior pixel).
+  // One load instruction whichever the source, so no branch-dependent register hazards reach the loop.
+  auto piece_src = [&](int h, bool act, bool seg2, int& off) -> const bf16r* {
+    const int pos = piece_pos(h);
+    int pix, lpos;
+    bool valid;
+    if (!seg2) {
+      const bool on = act && pos < HPOS;
+      const int py = pos / HROW, px = pos - (pos / HROW) * HROW;   // constant divisor: mul-shift
+      const int y = hy0 + py, x = hx0 + px;
+      valid = on && cok && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
+      pix = (n * d.Hs + y) * d.Ws + x;
+      lpos = pos;
+      act = on;
+    } else {
+      const int py = pos >> 4, px = pos & 15;
+      pix = (n * d.Ho + ty0 + py) * d.Wo + tx0 + px;
+      valid = act && cok;
+      lpos = (py + 1) * (TW + 2) + px + 1;
+    }
+    off = !act ? -1 : ((kc * HPAD + lpos) * 8) | (valid ? 0 : (1 << 30));
+    return cbase + (valid ? pix : 0) * cs;
   };
-  auto load_seg2 = [&](int k, int p) {   // p: interior position 0..255
-    const int py = p >> 4, px = p & 15;
-    const int pix = (n * d.Ho + ty0 + py) * d.Wo + tx0 + px;
-    rh[k] = *(const u32x4*)(cbase + (cok ? pix : 0) * cs);
-    hoff[k] = ((kc * HPAD + (py + 1) * (TW + 2) + px + 1) * 8) | (cok ? 0 : (1 << 30));
+  auto load_main = [&](int k, int h, bool act) {
+    int off;
+    const bf16r* src = piece_src(h, act, false, off);
+    rh[k] = *(const u32x4*)src;
+    hoff[k] = off;
   };
-  auto store = [&](int buf, int k, bool transform) {
+  auto load_seg2 = [&](int k, int h, bool act) {
+    int off;
+    const bf16r* src = piece_src(h, act, true, off);
+    rh[k] = *(const u32x4*)src;
+    hoff[k] = off;
+  };
+  auto store = [&](int buf, int k, bool transform, int c) {
     u32x4 v = rh[k];
     if (PRO != 0 && transform) {
+      const f32x4 a0 = *(const f32x4*)(coef + c), a1 = *(const f32x4*)(coef + c + 4);
+      const f32x4 b0 = *(const f32x4*)(coef + A.C + c), b1 = *(const f32x4*)(coef + A.C + c + 4);
+      const float ca[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float cb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float lo = bf_lo(v[e]) * ca[2 * e] + cb[2 * e];
@@ -177,27 +247,23 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
     const bf16r* hb = hbuf + hb_i * HBUF;
     const bf16r* wb = wbuf + wb_i * WBUF;
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    bf16x8 af[4];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int pl = ks * 4 + lq;   // 16-byte plane this lane reads
-      bf16x8 af[4];
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(wb + (lq * BCO + wco * 64 + 16 * i + l16) * 8);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(wb + (pl * BCO + wco * 64 + 16 * i + l16) * 8);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int py = wpx * 4 + j;
-        int pos;
-        if (UP && !seg2) {
-          const int ly = ((ty0 + py + ky - 1) >> 1) - hy0;
-          const int lx = ((tx0 + l16 + kx - 1) >> 1) - hx0;
-          pos = ly * HROW + lx;
-        } else {
-          pos = (py + ky) * (TW + 2) + l16 + kx;
-        }
-        const bf16x8 bv = *(const bf16x8*)(hb + (pl * HPAD + pos) * 8);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
+    for (int j = 0; j < 4; ++j) {
+      const int py = wpx * 4 + j;
+      int pos;
+      if (UP && !seg2) {
+        const int ly = ((ty0 + py + ky - 1) >> 1) - hy0;
+        const int lx = ((tx0 + l16 + kx - 1) >> 1) - hx0;
+        pos = ly * HROW + lx;
+      } else {
+        pos = (py + ky) * (TW + 2) + l16 + kx;
       }
+      const bf16x8 bv = *(const bf16x8*)(hb + (lq * HPAD + pos) * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
     }
   };
 
@@ -208,94 +274,90 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   };
   mark(0, 0);
   // ---- prologue: the full halo of chunk 0 (always a 3x3 chunk) + the weights of step 0
+  __syncthreads();   // affine + epilogue tables (no DMA in flight yet)
   setup(0);
   load_w(0, 0);
   if (A.nchunk1 * 9 > 1) load_w(1, 1);
 #pragma unroll
   for (int k = 0; k < LPRO; ++k) load_main(k, tid + NT * k, tid + NT * k < TOT1);
 #pragma unroll
-  for (int k = 0; k < LPRO; ++k) store(0, k, true);
+  for (int k = 0; k < LPRO; ++k) store(0, k, true, cch);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
+  step_barrier<0>();
 
-  // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8); the next chunk is staged in 4
-  //      pieces behind the MFMAs of steps 0-3.  Waves of the two cout halves share a SIMD pairwise:
-  //      wco 0 transforms its staged piece before its first tap, wco 1 after it, so one wave's
-  //      GroupNorm/SiLU VALU work overlaps the other's MFMAs.
+  // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8).  The next chunk's halo is staged in
+  //      4 pieces: piece i is loaded into registers in step i (after that step's weight DMA, so the
+  //      DMA's counted wait leaves it in flight across the barrier) and transformed + stored in step
+  //      i+1.  Waves of the two cout halves share a SIMD pairwise: wco 0 stores before its first tap,
+  //      wco 1 after it, so one wave's GroupNorm/SiLU VALU work overlaps the other's MFMAs.
   const int T1 = A.nchunk1 * 9;
   int wb = 0;   // weight double-buffer of the current step (tiles 2*wb, 2*wb+1)
   int s = 0;
+  int pc = 0;   // affine-table channel of the pending piece
   for (int chunk = 0; chunk < A.nchunk1; ++chunk) {
     const int nx = chunk + 1;
     const bool more = nx < nchunks, nseg2 = nx >= A.nchunk1;
-    if (more) setup(nx);
 #pragma unroll 1
     for (int ps = 0; ps < 5; ++ps) {
       const int slot = chunk * 9 + 2 * ps;
       const bool two = ps < 4;
-      const bool st = more && ps < 4;
-      if (st) {
-        if (!nseg2) {
-#pragma unroll
-          for (int k = 0; k < LPT; ++k) {
-            const int hl = tid + NT * k;
-            load_main(k, ps * PC1 + hl, hl < PC1 && ps * PC1 + hl < TOT1);
-          }
-        } else {
-          load_seg2(0, ps * (NT / 8) + tp);
+      const bool pend = more && ps > 0;    // piece ps-1 of chunk nx waits in registers
+      const bool issue = more && ps < 4;   // piece ps of chunk nx is loaded this step
+      auto issue_loads = [&]() {
+        // weights of the next step: the next pair of this chunk, the first pair of the next chunk,
+        // or the first 1x1 slot
+        const int nslot = slot + (two ? 2 : 1);
+        if (nslot < A.nsteps_slots) {
+          load_w(nslot, 2 * (wb ^ 1));
+          const bool ntwo = nslot < T1 && (nslot - (nslot / 9) * 9) < 8;
+          if (ntwo) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
         }
-      }
-      // weights of the next step: the next pair of this chunk, the first pair of the next chunk,
-      // or the first 1x1 slot
-      const int nslot = slot + (two ? 2 : 1);
-      if (nslot < A.nsteps_slots) {
-        load_w(nslot, 2 * (wb ^ 1));
-        const bool ntwo = nslot < T1 && (nslot - (nslot / 9) * 9) < 8;
-        if (ntwo) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
-      }
+        // one halo load per step, always (a dummy in-bounds read when nothing is staged): the register
+        // then has the same load -> consume pattern on every path, so hipcc's waits stay counted
+        if (issue && ps == 0) setup(nx);
+        const int h = ps * (nseg2 ? SEG2 / 4 : PC1) + tid;
+        const bool act = issue && (nseg2 ? tid < SEG2 / 4 : (tid < PC1 && h < TOT1));
+        int off;
+        const bf16r* src = piece_src(h, act, nseg2, off);
+        rh[0] = *(const u32x4*)src;
+        hoff[0] = off;
+      };
       mark(s + 1, 0);
-      if (wco == 0) {
-        if (st) {
-#pragma unroll
-          for (int k = 0; k < (nseg2 ? 1 : LPT); ++k) store(nx & 1, k, !nseg2);
-        }
-        compute(chunk & 1, 2 * ps, false, 2 * wb);
-      } else {
-        compute(chunk & 1, 2 * ps, false, 2 * wb);
-        if (st) {
-#pragma unroll
-          for (int k = 0; k < (nseg2 ? 1 : LPT); ++k) store(nx & 1, k, !nseg2);
-        }
-      }
+      asm volatile("" ::"v"(rh[0]));   // the previous step's halo load is consumed here, on every path
+      if (pend) store(nx & 1, 0, !nseg2, pc);
+      issue_loads();
+      compute(chunk & 1, 2 * ps, false, 2 * wb);
+      pc = cch;
       mark(s + 1, 1);
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
       mark(s + 1, 2);
-      __syncthreads();
+      step_barrier<1>();
       mark(s + 1, 3);
       wb ^= 1;
       ++s;
     }
   }
+  asm volatile("" ::"v"(rh[0]));
   // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, next chunk staged whole
   for (int chunk = A.nchunk1; chunk < nchunks; ++chunk) {
     const int nx = chunk + 1;
     const bool more = nx < nchunks;
+    const int slot = T1 + (chunk - A.nchunk1);
+    if (slot + 1 < A.nsteps_slots) load_w(slot + 1, 2 * (wb ^ 1));
     if (more) {
       setup(nx);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) load_seg2(k, tp + 64 * k);
+      for (int k = 0; k < SEG2 / NT; ++k) load_seg2(k, tid + NT * k, true);
     }
-    const int slot = T1 + (chunk - A.nchunk1);
-    if (slot + 1 < A.nsteps_slots) load_w(slot + 1, 2 * (wb ^ 1));
     compute(chunk & 1, 4, true, 2 * wb);
     if (more) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) store(nx & 1, k, false);
+      for (int k = 0; k < SEG2 / NT; ++k) store(nx & 1, k, false, 0);
     }
-    __syncthreads();
+    step_barrier<0>();
     wb ^= 1;
     ++s;
   }
@@ -307,33 +369,46 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
   const bool stats = d.stats != nullptr;
   const bool dep = d.ep_a != nullptr;
   const bool hasx = d.ep_x0 != nullptr;
-  float st1[4][4], st2[4][4];
+  // per-channel sums of this lane's 4 pixels, reduced over the wave's 16 pixel lanes per cout block:
+  // slab row = one wave's 64 pixels (4 rows x 16) of one image; any bijection works for GN
+  const int srow = tile * 4 + wpx;
+  auto flush_stats = [&](int i, const float* a4, const float* q4) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { st1[i][r] = 0.f; st2[i][r] = 0.f; }
+    for (int r = 0; r < 4; ++r) {
+      const float a = row16_sum_to_last(a4[r]), q = row16_sum_to_last(q4[r]);
+      const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
+      if (l16 == 15 && co < K) {
+        float* sp = d.stats + ((size_t)srow * K + co) * 2;
+        sp[0] = a;
+        sp[1] = q;
+      }
+    }
+  };
 
   if (co0 + BCO <= K && !d.out_f32 && !d.accumulate && !(d.resid && hasx)) {
     // Fast path: the 256-pixel x 128-channel tile goes through LDS ([pixel][16-byte chunk ^ (pixel & 15)],
     // conflict-free for the lanes' 8-byte reads), so every global access is a coalesced 16-byte one.
-    bf16r* tileb = lds;   // 64 KiB inside the (now idle) halo buffers
+    bf16r* tileb = lds;   // 64 KiB inside the (now idle) halo + weight buffers
     const bool side = d.resid != nullptr || hasx;
     if (side) {
-      u32x4 sv[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
-        const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-        const int c = co0 + c16 * 8;
-        const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
-                           : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
-                                           : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-        sv[k] = *(const u32x4*)src;
-      }
+      for (int half = 0; half < 2; ++half) {
+        u32x4 sv[4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
-        *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
+        for (int k = 0; k < 4; ++k) {
+          const int q = tid + NT * (4 * half + k), pi = q >> 4, c16 = q & 15;
+          const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+          const int c = co0 + c16 * 8;
+          const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
+                             : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
+                                             : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
+          sv[k] = *(const u32x4*)src;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = tid + NT * (4 * half + k), pi = q >> 4, c16 = q & 15;
+          *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
+        }
       }
       __syncthreads();
     }
@@ -341,14 +416,9 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
     for (int i = 0; i < 4; ++i) {
       const int cl = wco * 64 + 16 * i + 4 * lq;   // channel within the tile (multiple of 4)
       const int co = co0 + cl;
-      f32x4 bias = f32x4{0.f, 0.f, 0.f, 0.f}, ea = bias, eb = bias;
-      if (d.bias) bias += *(const f32x4*)(d.bias + co);
-      if (d.bias2) bias += *(const f32x4*)(d.bias2 + co);
-      if (d.bias_nc) bias += *(const f32x4*)(d.bias_nc + (size_t)n * K + co);
-      if (dep) {
-        ea = *(const f32x4*)(d.ep_a + (size_t)n * K + co);
-        eb = *(const f32x4*)(d.ep_b + (size_t)n * K + co);
-      }
+      const f32x4 bias = *(const f32x4*)(epi + cl);
+      const f32x4 ea = *(const f32x4*)(epi + BCO + cl), eb = *(const f32x4*)(epi + 2 * BCO + cl);
+      float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int pi = (wpx * 4 + j) * 16 + l16;
@@ -378,11 +448,12 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
           const float w[4] = {bf_lo(o[0]), bf_hi(o[0]), bf_lo(o[1]), bf_hi(o[1])};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            st1[i][r] += w[r];
-            st2[i][r] += hasx ? w[r] * xv[r] : w[r] * w[r];
+            st1[r] += w[r];
+            st2[r] += hasx ? w[r] * xv[r] : w[r] * w[r];
           }
         }
       }
+      if (stats) flush_stats(i, st1, st2);
     }
     __syncthreads();
 #pragma unroll
@@ -406,6 +477,7 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
           if (d.bias_nc) bias[r] += d.bias_nc[(size_t)n * K + co + r];
         }
       }
+      float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
   #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int y = ty0 + wpx * 4 + j, x = tx0 + l16;
@@ -463,36 +535,15 @@ __global__ __launch_bounds__(512) void conv3x3_halo(const HArgs A) {
         if (stats) {
   #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            st1[i][r] += v[r];
-            st2[i][r] += hasx ? v[r] * xv[r] : v[r] * v[r];
+            st1[r] += v[r];
+            st2[r] += hasx ? v[r] * xv[r] : v[r] * v[r];
           }
         }
       }
+      if (stats) flush_stats(i, st1, st2);
     }
   }
   mark(0, 2);
-  if (stats) {
-    // slab row = one wave's 64 pixels (4 rows x 16) of one image; any bijection works for GN
-    const int srow = tile * 4 + wpx;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a = st1[i][r], q = st2[i][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          q += __shfl_xor(q, o, 64);
-        }
-        const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
-        if (l16 == 0 && co < K) {
-          float* sp = d.stats + ((size_t)srow * K + co) * 2;
-          sp[0] = a;
-          sp[1] = q;
-        }
-      }
-    }
-  }
 }
 
 // [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
@@ -522,6 +573,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
+  if (d->pro_a && d->C0 + d->C1 > CMAX) return 1;   // the GN affine table holds CMAX channels
   if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
       (long long)d->N * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
   HArgs A;

@@ -530,7 +530,7 @@ __global__ void glinear_dx_reduce(const float* __restrict__ part, int np, int B,
 // contiguous 64-512 B runs.  Layouts (see fmd_prep_weights, fmd_tile_weights_halo):
 //   kind 0 base: mode 0 [R=Kpad][T][Cc=Cpad]; modes 1/3 [R=Cpad][T][Cc=Kpad] (3: taps flipped);
 //                mode 2 [R=Cpad][16][Cc=Kpad] (upsample + 3x3 data gradient, 4x4 effective taps)
-//   kind 1 halo tiles of a base layout: [ceil(R/128)][ceil(Cc/64)][T][8][128][8]
+//   kind 1 halo tiles of a base layout: [ceil(R/128)][ceil(Cc/BK)][T][BK/8][128][8], BK = FMD_HALO_BK
 // Job (16 x int64): w, K | C << 32, ks | nout << 32, first block | kt << 32 (k tiles),
 //                   then per output (<= 6): out, mode | kind << 8 | R << 16 | Cc << 40.
 constexpr int PT = 32;          // k and c tile
@@ -589,13 +589,14 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
         out[((size_t)row * To + tap) * Cc + col] = (bf16r)f2bf(ptile_value(tile, kl, cl, ks, mode, tap));
       }
     } else {
-      // [R/128][Cc/64][To][8][128][8]: 16-byte chunks of 8 cols, runs of 32 rows
-      const int nchunk = (Cc + 63) / 64;
+      // [R/128][Cc/BK][To][BK/8][128][8]: 16-byte chunks of 8 cols, runs of 32 rows
+      constexpr int HBK = FMD_HALO_BK;
+      const int nchunk = (Cc + HBK - 1) / HBK;
       for (int e = threadIdx.x; e < To * (PT / 8) * PT; e += blockDim.x) {
         const int rl = e % PT, r = e / PT, kq = r % (PT / 8), tap = r / (PT / 8);
         const int row = r0 + rl, col8 = q0 + kq * 8;
-        if (row >= ((R + 127) / 128) * 128 || col8 >= nchunk * 64) continue;
-        const int tr = row >> 7, co = row & 127, chunk = col8 >> 6, kc = (col8 >> 3) & 7;
+        if (row >= ((R + 127) / 128) * 128 || col8 >= nchunk * HBK) continue;
+        const int tr = row >> 7, co = row & 127, chunk = col8 / HBK, kc = (col8 % HBK) >> 3;
         unsigned int pk[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
           }
           pk[h] = pack2(v2[0], v2[1]);
         }
-        const size_t idx = ((((size_t)tr * nchunk + chunk) * To + tap) * 8 + kc) * 128 + co;
+        const size_t idx = ((((size_t)tr * nchunk + chunk) * To + tap) * (HBK / 8) + kc) * 128 + co;
         *(u32x4*)(out + idx * 8) = u32x4{pk[0], pk[1], pk[2], pk[3]};
       }
     }

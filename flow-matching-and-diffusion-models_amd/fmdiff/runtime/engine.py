@@ -41,6 +41,7 @@ from ..nn.params import Conv, Identity
 BF16 = torch.bfloat16
 F32 = torch.float32
 CPAD = 8      # NHWC channel padding of the model input / output (16-byte rows)
+HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdiff.h)
 
 
 class Act:
@@ -127,7 +128,7 @@ class WeightCache:
                     descs = []
                     for buf_ptr, (_, _, _, mode, R, Cc, kind, _T, _n) in part:
                         r_ext = -(-R // 128) * 128 if kind else R
-                        c_ext = -(-Cc // 64) * 64 if kind else Cc
+                        c_ext = -(-Cc // HALO_BK) * HALO_BK if kind else Cc
                         k_ext, c_ext2 = (r_ext, c_ext) if mode == 0 else (c_ext, r_ext)
                         kp, cp = max(kp, k_ext), max(cp, c_ext2)
                         descs += [buf_ptr, mode | (kind << 8) | (R << 16) | (Cc << 40)]

@@ -102,10 +102,14 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
     return max(1, min(nk // 4, -(-2 * NUM_CU // tiles), 32))
 
 
-def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False) -> bool:
+HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
+
+
+def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False, Cin=0,
+                  pro=False) -> bool:
     """Mirror of fmd_conv_halo's applicability test (csrc/conv_halo.hip): 3x3 s1 p1 forward gather,
-    16x16 output tiles, K > 16 and at least 128 workgroups."""
-    return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed
+    16x16 output tiles, K > 16, at least 128 workgroups, GN-prologue inputs of at most HALO_CMAX channels."""
+    return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed and not (pro and Cin > HALO_CMAX)
             and Ho % 16 == 0 and Wo % 16 == 0 and N * (Ho // 16) * (Wo // 16) * -(-K // 128) >= 128
             and (Ho == 2 * Hs if upsample else Ho == Hs))
 
@@ -147,7 +151,8 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
     bpx = 256 if K <= 16 else 128
-    halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed)
+    halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
+                                                  pro is not None)
     d.force_generic = int(force_generic)
     if halo:
         splits = 1

@@ -78,7 +78,9 @@ typedef struct fmd_conv_desc {
 int fmd_conv(const fmd_conv_desc* d, fmd_stream_t s);
 /* Halo-tiled 3x3 stride-1 conv; returns 1 (nothing launched) when the problem does not qualify. */
 int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t s);
-/* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, 64-channel chunk, tap) 16 KiB tiles. */
+/* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
+#define FMD_HALO_BK 32
+/* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);
 int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* out, fmd_stream_t s);
 

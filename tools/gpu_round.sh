@@ -1,0 +1,16 @@
+#!/bin/bash
+# GPU-box helper: GPU tests -> smoke -> bench (1 GPU) -> rocprofv3 kernel-trace stats.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+if [ -z "$SKIP_TESTS" ]; then
+  step tests timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -rA > gpurun_out/gpu_tests.log 2>&1
+  step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+fi
+step bench timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_out/bench.json 2> gpurun_out/bench.err
+step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+  python bench.py --steps 5 --warmup 2 --no-cpu-baseline --sampler-steps 5 > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err
+find gpurun_out/prof -name "*stats*"
