@@ -1,0 +1,420 @@
+// Output head of the UNet: GroupNorm -> SiLU -> 3x3 conv to K <= 8 channels (fp32 output,
+// channels padded to Kp = 8), and its backward.  Replaces the reference's final
+// ``out = nn.Sequential(norm, SiLU, ConvND(model_channels -> out_channels, 3))``
+// (src/models/unet/unet.py:286-293 / unet_diffusers_nd.py conv_norm_out + conv_out) and the
+// autograd of that conv (src/nn/ops/convolution.py:53).
+//
+// K is 1 for every BASELINE config: an MFMA tile would waste 15/16 of its rows and the
+// per-tap implicit GEMM re-applies the GN/SiLU transform 9 times per element, so these are
+// VALU kernels around a once-per-element transform:
+//   head_fwd   : 16x16-pixel tile per workgroup, thread = pixel; per 32-channel chunk the
+//                transformed (18x18) halo is staged once in LDS (chunk-major planes, as in
+//                conv_halo.hip) and every tap reads it; weights of the chunk in LDS (broadcast).
+//   head_dgrad : thread = 8 channels x one tile row; dpred's 18x18 halo (Kp = 8 bf16 = 16 B per
+//                pixel) in LDS; epilogue = SiLU' of the forward pre-activation, bf16 store and the
+//                GroupNorm-backward sums (sum dz, sum dz*x) per 64-pixel slab row.
+//   head_wgrad : per chunk, thread = (8-channel group, tap, pixel phase) summing dpred * t over
+//                the tile from LDS; per-workgroup partials [wg][K][C][9] + [wg][K] reduced by
+//                slot_sum + head_wgrad_finish into the reference [K][C][3][3] layout.
+#include "common.h"
+#include "../../include/fmdiff.h"
+
+namespace {
+
+constexpr int HT = 16;                 // tile edge
+constexpr int HR = HT + 2;             // halo row (18)
+constexpr int HPOS = HR * HR;          // 324
+constexpr int HPADP = 336;             // plane stride (16-byte rows), == 0 mod 16
+constexpr int CK = 32;                 // channels per chunk
+constexpr int KCP = CK / 8;            // 16-byte planes per chunk
+constexpr int NTH = 256;
+
+FMD_DEV int hp_pos(int h) { return (h >> 5) * 8 + (h & 7); }
+FMD_DEV int hp_kc(int h) { return (h >> 3) & (KCP - 1); }
+
+// stage the GN+SiLU-transformed halo of channels [c0, c0+32) of tile (n, ty0, tx0) into halo[4][336]
+FMD_DEV void stage_halo(u32x4* halo, const bf16r* __restrict__ h, int n, int H, int W, int C, int ty0, int tx0,
+                        int c0, const float* __restrict__ pa, const float* __restrict__ pb, int tid) {
+  constexpr int TOT = ((HPOS + 7) / 8) * 8 * KCP;   // 1312 pieces
+  for (int q = tid; q < TOT; q += NTH) {
+    const int pos = hp_pos(q), kc = hp_kc(q);
+    if (pos >= HPOS) continue;
+    const int y = ty0 - 1 + pos / HR, x = tx0 - 1 + pos % HR;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      const int c = c0 + kc * 8;
+      const u32x4 r = *(const u32x4*)(h + ((size_t)(n * H + y) * W + x) * C + c);
+      const f32x4 a0 = *(const f32x4*)(pa + (size_t)n * C + c), a1 = *(const f32x4*)(pa + (size_t)n * C + c + 4);
+      const f32x4 b0 = *(const f32x4*)(pb + (size_t)n * C + c), b1 = *(const f32x4*)(pb + (size_t)n * C + c + 4);
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = pack2(siluf_(bf_lo(r[e]) * av[2 * e] + bv[2 * e]), siluf_(bf_hi(r[e]) * av[2 * e + 1] + bv[2 * e + 1]));
+    }
+    halo[kc * HPADP + pos] = v;
+  }
+}
+
+struct HeadArgs {
+  const bf16r* h;       // [N][H][W][C] GN input
+  const float* pa;      // [N][C]
+  const float* pb;
+  const float* w;       // [K][C][3][3]
+  const float* bias;    // [K] or null
+  const bf16r* dpred;   // [N][H][W][8]
+  float* out;           // fp32 [N][H][W][Kp]
+  bf16r* dz;            // [N][H][W][C]
+  float* stats;         // [N*H*W/64][C][2]
+  float* ws;            // wgrad partials
+  int N, H, W, C, K, Kp;
+  int tiles_x, tiles_y, ntiles, tiles_per_wg;
+};
+
+template <int KT>
+__global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
+  __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
+  __shared__ __attribute__((aligned(16))) float wl[KT][9][CK];   // chunk weights [k][tap][c]
+  const int tid = threadIdx.x;
+  const int tile = blockIdx.x, per = A.tiles_x * A.tiles_y;
+  const int n = tile / per, tr = tile - n * per;
+  const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+  const int py = tid >> 4, px = tid & 15;
+  float acc[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) acc[k] = 0.f;
+  for (int c0 = 0; c0 < A.C; c0 += CK) {
+    stage_halo(halo, A.h, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
+    for (int i = tid; i < KT * 9 * CK; i += NTH) {
+      const int k = i / (9 * CK), r = i - k * 9 * CK, tap = r / CK, c = r - tap * CK;
+      wl[k][tap][c] = k < A.K ? A.w[((size_t)k * A.C + c0 + c) * 9 + tap] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int pos = (py + tap / 3) * HR + px + tap % 3;
+#pragma unroll
+      for (int kc = 0; kc < KCP; ++kc) {
+        const u32x4 v = halo[kc * HPADP + pos];
+        const float t[8] = {bf_lo(v[0]), bf_hi(v[0]), bf_lo(v[1]), bf_hi(v[1]),
+                            bf_lo(v[2]), bf_hi(v[2]), bf_lo(v[3]), bf_hi(v[3])};
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          const f32x4 w0 = *(const f32x4*)&wl[k][tap][kc * 8], w1 = *(const f32x4*)&wl[k][tap][kc * 8 + 4];
+          acc[k] += t[0] * w0[0] + t[1] * w0[1] + t[2] * w0[2] + t[3] * w0[3] +
+                    t[4] * w1[0] + t[5] * w1[1] + t[6] * w1[2] + t[7] * w1[3];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const size_t p = ((size_t)(n * A.H) + ty0 + py) * A.W + tx0 + px;
+  float* o = A.out + p * A.Kp;
+  for (int k = 0; k < A.Kp; k += 4) {
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k + e;
+      float r = 0.f;
+#pragma unroll
+      for (int j = 0; j < KT; ++j)
+        if (j == kk) r = acc[j];
+      v[e] = kk < A.K ? r + (A.bias ? A.bias[kk] : 0.f) : 0.f;
+    }
+    *(f32x4*)(o + k) = v;
+  }
+}
+
+// dz[p][c] = silu'(a x + b) * sum_{tap,k} dpred[p - tap + 1][k] W[k][c][tap]; stats (sum dz, sum dz*x)
+template <int KT>
+__global__ __launch_bounds__(256) void head_dgrad(const HeadArgs A) {
+  __shared__ __attribute__((aligned(16))) float dp[HPOS][KT];          // dpred halo (fp32)
+  __shared__ __attribute__((aligned(16))) float wl[9][KT][128];        // weights of this 128-channel block
+  const int tid = threadIdx.x;
+  const int tile = blockIdx.x, per = A.tiles_x * A.tiles_y;
+  const int n = tile / per, tr = tile - n * per;
+  const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+  const int cb0 = blockIdx.y * 128;
+  const int g = tid & 15, r = tid >> 4;   // 8 channels x one tile row
+  for (int pos = tid; pos < HPOS; pos += NTH) {
+    const int y = ty0 - 1 + pos / HR, x = tx0 - 1 + pos % HR;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (y >= 0 && y < A.H && x >= 0 && x < A.W) {
+      const u32x4 q = *(const u32x4*)(A.dpred + ((size_t)(n * A.H + y) * A.W + x) * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[2 * e] = bf_lo(q[e]); v[2 * e + 1] = bf_hi(q[e]); }
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k) dp[pos][k] = v[k];
+  }
+  for (int i = tid; i < 9 * KT * 128; i += NTH) {
+    const int tap = i / (KT * 128), rr = i - tap * KT * 128, k = rr / 128, c = rr - k * 128;
+    wl[tap][k][c] = (k < A.K && cb0 + c < A.C) ? A.w[((size_t)k * A.C + cb0 + c) * 9 + tap] : 0.f;
+  }
+  __syncthreads();
+  const int c = cb0 + g * 8;
+  const bool cok = c < A.C;
+  float a[8], b[8], s1[8], s2[8];
+  if (cok) {
+    const f32x4 a0 = *(const f32x4*)(A.pa + (size_t)n * A.C + c), a1 = *(const f32x4*)(A.pa + (size_t)n * A.C + c + 4);
+    const f32x4 b0 = *(const f32x4*)(A.pb + (size_t)n * A.C + c), b1 = *(const f32x4*)(A.pb + (size_t)n * A.C + c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a[e] = a0[e]; a[4 + e] = a1[e]; b[e] = b0[e]; b[4 + e] = b1[e]; }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int x = 0; x < HT; ++x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap % 3;
+      const int pos = (r + 2 - ky) * HR + x + 2 - kx;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const float d = dp[pos][k];
+        const f32x4 w0 = *(const f32x4*)&wl[tap][k][g * 8], w1 = *(const f32x4*)&wl[tap][k][g * 8 + 4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[e] += d * w0[e]; acc[4 + e] += d * w1[e]; }
+      }
+    }
+    if (cok) {
+      const size_t p = ((size_t)(n * A.H) + ty0 + r) * A.W + tx0 + x;
+      const u32x4 xr = *(const u32x4*)(A.h + p * A.C + c);
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x0 = bf_lo(xr[e]), x1 = bf_hi(xr[e]);
+        o[e] = pack2(acc[2 * e] * silu_grad(a[2 * e] * x0 + b[2 * e]),
+                     acc[2 * e + 1] * silu_grad(a[2 * e + 1] * x1 + b[2 * e + 1]));
+        const float w0 = bf_lo(o[e]), w1 = bf_hi(o[e]);
+        s1[2 * e] += w0; s2[2 * e] += w0 * x0;
+        s1[2 * e + 1] += w1; s2[2 * e + 1] += w1 * x1;
+      }
+      *(u32x4*)(A.dz + p * A.C + c) = o;
+    }
+  }
+  // the wave's 4 rows x 16 pixels = one 64-pixel slab row: sum lanes g, g+16, g+32, g+48
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] += __shfl_xor(s1[e], 16, 64);
+    s1[e] += __shfl_xor(s1[e], 32, 64);
+    s2[e] += __shfl_xor(s2[e], 16, 64);
+    s2[e] += __shfl_xor(s2[e], 32, 64);
+  }
+  if ((r & 3) == 0 && cok) {
+    const int srow = tile * 4 + (r >> 2);
+    float* sp = A.stats + ((size_t)srow * A.C + c) * 2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sp[2 * e] = s1[e]; sp[2 * e + 1] = s2[e]; }
+  }
+}
+
+// per-workgroup partials: slot[wg] = {[k][c][tap] (reference layout per k), [k] bias}; the workgroup
+// owns tiles [wg*tpw, (wg+1)*tpw) and keeps its sums in registers across them, chunk by chunk
+template <int KT>
+__global__ __launch_bounds__(256) void head_wgrad(const HeadArgs A) {
+  __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
+  __shared__ __attribute__((aligned(16))) float dp[256][KT];
+  __shared__ __attribute__((aligned(16))) float red[7][36][KT * 8];
+  __shared__ float bsum[4][KT];
+  const int tid = threadIdx.x;
+  const int per = A.tiles_x * A.tiles_y;
+  const int combo = tid % 36, phase = tid / 36;   // 7 phases x 36 (kc, tap); threads 252..255 only stage
+  const int kc = combo / 9, tap = combo % 9;
+  const size_t slot = (size_t)KT * A.C * 9 + KT;
+  float* wsw = A.ws + (size_t)blockIdx.x * slot;
+  const int t0 = blockIdx.x * A.tiles_per_wg, t1 = min(A.ntiles, t0 + A.tiles_per_wg);
+  float dbs[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) dbs[k] = 0.f;
+  for (int c0 = 0; c0 < A.C; c0 += CK) {
+    float acc[KT][8];
+#pragma unroll
+    for (int k = 0; k < KT; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const int n = t / per, tr = t - n * per;
+      const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+      {
+        const int py = tid >> 4, px = tid & 15;
+        const u32x4 q = *(const u32x4*)(A.dpred + (((size_t)(n * A.H) + ty0 + py) * A.W + tx0 + px) * 8);
+        const float v[8] = {bf_lo(q[0]), bf_hi(q[0]), bf_lo(q[1]), bf_hi(q[1]),
+                            bf_lo(q[2]), bf_hi(q[2]), bf_lo(q[3]), bf_hi(q[3])};
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          dp[tid][k] = v[k];
+          if (c0 == 0) dbs[k] += v[k];
+        }
+      }
+      stage_halo(halo, A.h, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
+      __syncthreads();
+      if (phase < 7) {
+        for (int p = phase; p < 256; p += 7) {
+          const int pos = ((p >> 4) + tap / 3) * HR + (p & 15) + tap % 3;
+          const u32x4 v = halo[kc * HPADP + pos];
+          const float tv[8] = {bf_lo(v[0]), bf_hi(v[0]), bf_lo(v[1]), bf_hi(v[1]),
+                               bf_lo(v[2]), bf_hi(v[2]), bf_lo(v[3]), bf_hi(v[3])};
+#pragma unroll
+          for (int k = 0; k < KT; ++k) {
+            const float d = dp[p][k];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[k][e] += d * tv[e];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (phase < 7) {
+#pragma unroll
+      for (int k = 0; k < KT; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[phase][combo][k * 8 + e] = acc[k][e];
+    }
+    __syncthreads();
+    // sum the 7 phases; write this chunk's part of the slot
+    for (int i = tid; i < 36 * KT * 8; i += NTH) {
+      const int cmb = i / (KT * 8), r = i - cmb * KT * 8, k = r / 8, e = r % 8;
+      float sum = 0.f;
+#pragma unroll
+      for (int ph = 0; ph < 7; ++ph) sum += red[ph][cmb][r];
+      wsw[((size_t)k * A.C + c0 + (cmb / 9) * 8 + e) * 9 + cmb % 9] = sum;
+    }
+    __syncthreads();
+  }
+  // bias partials: every thread summed its own pixel of each tile
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    const float v = wave_sum(dbs[k]);
+    if ((tid & 63) == 0) bsum[tid >> 6][k] = v;
+  }
+  __syncthreads();
+  if (tid < KT) wsw[slot - KT + tid] = bsum[0][tid] + bsum[1][tid] + bsum[2][tid] + bsum[3][tid];
+}
+
+// out[s][i] = sum over slots g in split s of in[g][i]  (i < len; slots of stride `stride`)
+__global__ void slot_sum(const float* __restrict__ in, int nslots, size_t stride, int len, int per_split,
+                         float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  const int g0 = blockIdx.y * per_split, g1 = min(nslots, g0 + per_split);
+  float s0 = 0.f, s1 = 0.f;
+  int g = g0;
+  for (; g + 2 <= g1; g += 2) { s0 += in[(size_t)g * stride + i]; s1 += in[(size_t)(g + 1) * stride + i]; }
+  if (g < g1) s0 += in[(size_t)g * stride + i];
+  out[(size_t)blockIdx.y * len + i] = s0 + s1;
+}
+
+// dw[k][c][tap] += sum_s part[s][k][c][tap];  db[k] += sum_s part[s][KT*C*9 + k]
+__global__ void head_wgrad_finish(const float* __restrict__ part, int ns, int KT, int K, int C, float* __restrict__ dw,
+                                  float* __restrict__ db) {
+  const int len = KT * C * 9 + KT;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float s = 0.f;
+  if (i < K * C * 9) {
+    for (int g = 0; g < ns; ++g) s += part[(size_t)g * len + i];
+    dw[i] += s;
+  } else if (db && i >= KT * C * 9 && i < KT * C * 9 + K) {
+    for (int g = 0; g < ns; ++g) s += part[(size_t)g * len + i];
+    db[i - KT * C * 9] += s;
+  }
+}
+
+int kt_of(int K) { return K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : 8; }
+
+HeadArgs make(const void* h, int N, int H, int W, int C, const float* pa, const float* pb, const float* w, int K) {
+  HeadArgs A{};
+  A.h = (const bf16r*)h;
+  A.pa = pa;
+  A.pb = pb;
+  A.w = w;
+  A.N = N; A.H = H; A.W = W; A.C = C; A.K = K; A.Kp = 8;
+  A.tiles_x = W / HT;
+  A.tiles_y = H / HT;
+  A.ntiles = N * A.tiles_x * A.tiles_y;
+  return A;
+}
+
+bool shape_ok(int N, int H, int W, int C, int K) {
+  return N > 0 && H % HT == 0 && W % HT == 0 && C % CK == 0 && K >= 1 && K <= 8 &&
+         (long long)N * H * W * C < (1LL << 31);
+}
+
+constexpr int WG_WGRAD = 512;   // head_wgrad workgroups (each loops over its share of tiles)
+constexpr int RED_SPLIT = 16;   // first reduction stage: WG_WGRAD slots -> RED_SPLIT partial sums
+
+}  // namespace
+
+extern "C" {
+
+int fmd_head_fwd(const void* h, int32_t N, int32_t H, int32_t W, int32_t C, const float* pro_a, const float* pro_b,
+                 const float* w, const float* bias, int32_t K, float* out, fmd_stream_t s) {
+  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b) return -1;
+  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, w, K);
+  A.bias = bias;
+  A.out = out;
+  const dim3 g(A.ntiles);
+  hipStream_t st = (hipStream_t)s;
+  switch (kt_of(K)) {
+    case 1: hipLaunchKernelGGL(head_fwd<1>, g, dim3(NTH), 0, st, A); break;
+    case 2: hipLaunchKernelGGL(head_fwd<2>, g, dim3(NTH), 0, st, A); break;
+    case 4: hipLaunchKernelGGL(head_fwd<4>, g, dim3(NTH), 0, st, A); break;
+    default: hipLaunchKernelGGL(head_fwd<8>, g, dim3(NTH), 0, st, A); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int fmd_head_dgrad(const void* dpred, const float* w, int32_t K, const void* h, const float* pro_a, const float* pro_b,
+                   int32_t N, int32_t H, int32_t W, int32_t C, void* dz, float* stats, fmd_stream_t s) {
+  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b || !stats) return -1;
+  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, w, K);
+  A.dpred = (const bf16r*)dpred;
+  A.dz = (bf16r*)dz;
+  A.stats = stats;
+  const dim3 g(A.ntiles, (C + 127) / 128);
+  hipStream_t st = (hipStream_t)s;
+  switch (kt_of(K)) {
+    case 1: hipLaunchKernelGGL(head_dgrad<1>, g, dim3(NTH), 0, st, A); break;
+    case 2: hipLaunchKernelGGL(head_dgrad<2>, g, dim3(NTH), 0, st, A); break;
+    case 4: hipLaunchKernelGGL(head_dgrad<4>, g, dim3(NTH), 0, st, A); break;
+    default: hipLaunchKernelGGL(head_dgrad<8>, g, dim3(NTH), 0, st, A); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int64_t fmd_head_wgrad_workspace(int32_t N, int32_t H, int32_t W, int32_t C, int32_t K) {
+  (void)N; (void)H; (void)W;
+  const int kt = kt_of(K);
+  return (int64_t)(WG_WGRAD + RED_SPLIT) * ((int64_t)kt * C * 9 + kt);
+}
+
+int fmd_head_wgrad(const void* dpred, int32_t K, const void* h, const float* pro_a, const float* pro_b, int32_t N,
+                   int32_t H, int32_t W, int32_t C, float* dw, float* db, float* ws, fmd_stream_t s) {
+  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b || !ws || !dw) return -1;
+  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, nullptr, K);
+  A.dpred = (const bf16r*)dpred;
+  A.ws = ws;
+  const int nwg = A.ntiles < WG_WGRAD ? A.ntiles : WG_WGRAD;
+  A.tiles_per_wg = (A.ntiles + nwg - 1) / nwg;
+  const int kt = kt_of(K);
+  hipStream_t st = (hipStream_t)s;
+  switch (kt) {
+    case 1: hipLaunchKernelGGL(head_wgrad<1>, dim3(nwg), dim3(NTH), 0, st, A); break;
+    case 2: hipLaunchKernelGGL(head_wgrad<2>, dim3(nwg), dim3(NTH), 0, st, A); break;
+    case 4: hipLaunchKernelGGL(head_wgrad<4>, dim3(nwg), dim3(NTH), 0, st, A); break;
+    default: hipLaunchKernelGGL(head_wgrad<8>, dim3(nwg), dim3(NTH), 0, st, A); break;
+  }
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  const int len = kt * C * 9 + kt;
+  float* part = ws + (size_t)WG_WGRAD * len;
+  const int per_split = (nwg + RED_SPLIT - 1) / RED_SPLIT;
+  hipLaunchKernelGGL(slot_sum, dim3((len + 255) / 256, RED_SPLIT), dim3(256), 0, st, ws, nwg, (size_t)len, len,
+                     per_split, part);
+  rc = (int)hipGetLastError();
+  if (rc) return rc;
+  hipLaunchKernelGGL(head_wgrad_finish, dim3((len + 255) / 256), dim3(256), 0, st, part, RED_SPLIT, kt, K, C, dw, db);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -458,6 +458,20 @@ class UNetEngine:
         K = conv.out_channels
         Kp = max(CPAD, -(-K // 8) * 8)
         a, b, mr = ops.gn_prep(_stats(h), None, N, H * W, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
+        if Kp == CPAD and ops.head_eligible(H, W, Cc, K):
+            # VALU head kernels (csrc/head.hip): the GN/SiLU transform once per element, no MFMA padding
+            out = ops.head_fwd(h.t, (a, b), conv.weight, conv.bias, K, Kp)
+            if ctx.tape is not None:
+                def bwd(dpred):
+                    ops.head_wgrad(dpred, K, h.t, (a, b), conv.weight.grad,
+                                   conv.bias.grad if conv.bias is not None else None)
+                    dz, s12 = ops.head_dgrad(dpred, conv.weight, K, h.t, (a, b))
+                    P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
+                                              norm.weight.grad, norm.bias.grad)
+                    g, acc = _gdest(h)
+                    ops.gn_bwd_apply(dz, h.t, None, P, Q, R, None, g, acc)
+                self._head_bwd = bwd
+            return out
         w = self.wc.get(conv.weight, 0, Kp, None)
         bias = self.wc.padded(conv.bias, Kp)
         out, _ = ops.conv(h.t, Kp, w, pro=(a, b, True), bias=bias, out_f32=True)

@@ -185,6 +185,39 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     return out, st
 
 
+def head_eligible(H, W, C, K) -> bool:
+    """Mirror of the head kernels' shape test (csrc/head.hip)."""
+    return H % 16 == 0 and W % 16 == 0 and C % 32 == 0 and 1 <= K <= 8
+
+
+def head_fwd(h, pro, w, bias, K, Kp=8):
+    """out fp32 NHWC [N,H,W,Kp] = conv3x3(SiLU(a*h+b)) for the first K channels (csrc/head.hip)."""
+    _need_cuda(h, "head_fwd")
+    N, H, W, Cc = h.shape
+    out = torch.empty((N, H, W, Kp), device=h.device, dtype=F32)
+    _lib.call("fmd_head_fwd", _p(h), N, H, W, Cc, _p(pro[0]), _p(pro[1]), _p(w.contiguous()), _p(bias), K, _p(out),
+              stream())
+    return out
+
+
+def head_dgrad(dpred, w, K, h, pro):
+    """(dz bf16 NHWC, Stats(sum dz, sum dz*h)) of the head conv (csrc/head.hip)."""
+    N, H, W, Cc = h.shape
+    dz = torch.empty_like(h)
+    slab = torch.empty((N * H * W // 64, Cc, 2), device=h.device, dtype=F32)
+    _lib.call("fmd_head_dgrad", _p(dpred), _p(w.contiguous()), K, _p(h), _p(pro[0]), _p(pro[1]), N, H, W, Cc, _p(dz),
+              _p(slab), stream())
+    return dz, Stats(slab, 64)
+
+
+def head_wgrad(dpred, K, h, pro, dw, db):
+    N, H, W, Cc = h.shape
+    n = int(_lib.lib().fmd_head_wgrad_workspace(N, H, W, Cc, K))
+    ws = torch.empty((n,), device=h.device, dtype=F32)
+    _lib.call("fmd_head_wgrad", _p(dpred), K, _p(h), _p(pro[0]), _p(pro[1]), N, H, W, Cc, _p(dw), _p(db), _p(ws),
+              stream())
+
+
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
     """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip)."""
     return (ks == 3 and stride == 1 and pad == 1 and not upsample and Ho == Hs and Wo == Ws and Ho % 8 == 0

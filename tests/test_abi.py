@@ -63,3 +63,16 @@ def test_product_path_has_no_cpu_fallback():
     x = torch.zeros(1, 8, 8, 16, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         ops.conv(x, 16, torch.zeros(16, 9, 16, dtype=torch.bfloat16))
+
+
+def test_every_host_module_imports():
+    """Import every host-side module of the package (no GPU needed): catches syntax/import errors in
+    code paths only the GPU tests exercise."""
+    import importlib
+    import pkgutil
+
+    import fmdiff
+    names = [m.name for m in pkgutil.walk_packages(fmdiff.__path__, "fmdiff.")]
+    assert "fmdiff.runtime.engine" in names
+    for n in names:
+        importlib.import_module(n)

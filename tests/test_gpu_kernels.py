@@ -397,3 +397,49 @@ def test_weight_cache_batched_refresh_matches_individual_preps():
     for (kind, wi, mode, kp), ref in want.items():
         got = wc.get(ws[wi], mode, kp, None) if kind == "b" else wc.tiled(ws[wi], mode, kp, None)
         assert torch.equal(got, ref), (kind, wi, mode, kp)
+
+
+@pytest.mark.parametrize("K", [1, 3])
+def test_head_kernels_vs_torch(K):
+    """csrc/head.hip: GN-affine+SiLU -> 3x3 conv to K <= 8 channels (fp32 out, Kp = 8), its data gradient
+    (SiLU' epilogue + GN-backward sums) and weight/bias gradients, vs torch fp32 autograd on the same
+    bf16-rounded inputs.  Tolerance: 1e-2 x max|ref| (bf16 transformed activations / bf16 dz)."""
+    O = ops()
+    N, H, W, C = 2, 32, 48, 64
+    g = torch.Generator().manual_seed(11)
+    h = _rand_nhwc(N, H, W, C, 12)
+    a = torch.rand(N, C, generator=g) + 0.5
+    b = torch.randn(N, C, generator=g) * 0.2
+    w = torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9)
+    bias = torch.randn(K, generator=g) * 0.1
+    dpred = (torch.randn(N, H, W, 8, generator=g) * 0.5).to(torch.bfloat16)
+    dpred[..., K:] = 0
+    hd, ad, bd = h.to(DEV), a.to(DEV), b.to(DEV)
+    out = O.head_fwd(hd, (ad, bd), w.to(DEV), bias.to(DEV), K)
+    # reference
+    x = _to_nchw(h).requires_grad_()
+    z = x * a[:, :, None, None] + b[:, :, None, None]
+    t = F.silu(z)
+    wr = w.clone().requires_grad_()
+    br = bias.clone().requires_grad_()
+    ref = F.conv2d(t, wr, br, padding=1)
+    _close(out[..., :K], ref.permute(0, 2, 3, 1), rel=1e-2)
+    assert out[..., K:].abs().max().item() == 0.0
+    dref = _to_nchw(dpred)[:, :K]
+    ref.backward(dref)
+    dw = torch.zeros(K, C, 3, 3, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    O.head_wgrad(dpred.to(DEV), K, hd, (ad, bd), dw, db)
+    _close(dw, wr.grad, rel=1e-2)
+    _close(db, br.grad, rel=1e-2)
+    dz, st = O.head_dgrad(dpred.to(DEV), w.to(DEV), K, hd, (ad, bd))
+    # dz = dL/dz of the pre-activation (the GN-backward input)
+    zr = z.detach().requires_grad_()
+    F.conv2d(F.silu(zr), w, bias, padding=1).backward(dref)
+    dz_ref = zr.grad.permute(0, 2, 3, 1)
+    _close(dz, dz_ref, rel=1e-2)
+    s = st.slab.double().cpu().view(N, -1, C, 2).sum(1)
+    xs = h.double().view(N, -1, C)
+    dzd = dz.double().cpu().view(N, -1, C)
+    torch.testing.assert_close(s[..., 0], dzd.sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(s[..., 1], (dzd * xs).sum(1), rtol=1e-4, atol=1e-3)
