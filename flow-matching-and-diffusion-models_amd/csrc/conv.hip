@@ -21,6 +21,7 @@ namespace {
 
 struct KArgs {
   fmd_conv_desc d;
+  fmd_gn_apply_desc g;   // GNA kernels: GroupNorm-backward apply epilogue (fmd_conv_gn_apply)
   int M;          // N*Ho*Wo
   int T;          // ks*ks taps
   int C;          // C0 + C1
@@ -29,9 +30,12 @@ struct KArgs {
   int per_split;  // K-iterations per split
   int ntp, ntc;   // pixel tiles, cout tiles
   int stats_rows; // pixels per stats slab row (64) or 0
+  int par;        // stride-2 transposed 3x3: one launch z-slice per output parity class (sub-pixel
+                  // decomposition: only the 1/2/2/4 taps that hit a class are iterated, not all 9)
+  int Mfull;      // N*Ho*Wo (== M unless par)
 };
 
-template <int BCO, int BPX, int WM, int WN, int BK>
+template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
 __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   constexpr int NT = 256;
   constexpr int CH = BK / 8;                  // 16-byte chunks per LDS row
@@ -56,8 +60,23 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   const int tco = b % A.ntc, tpx = b / A.ntc;
   const int co0 = tco * BCO, px0 = tpx * BPX;
   const int split = blockIdx.y;
-  const int kk0 = split * A.per_split;
-  const int kk1 = min(A.nk, kk0 + A.per_split);
+  // parity class (par): output pixels (2qy + cy, 2qx + cx); taps ky in {1} (cy = 0) or {0, 2} (cy = 1)
+  const int cy = A.par ? (int)(blockIdx.z >> 1) : 0, cx = A.par ? (int)(blockIdx.z & 1) : 0;
+  const int nkx = cx ? 2 : 1;
+  const int Tc = A.par ? (cy ? 2 : 1) * nkx : A.T;
+  const int nk1 = A.par ? ((A.C + BK - 1) / BK) * Tc : A.nk1;
+  const int nkt = A.par ? nk1 : A.nk;
+  const int per_split = A.par ? (nkt + (int)gridDim.y - 1) / (int)gridDim.y : A.per_split;
+  const int kk0 = split * per_split;
+  const int kk1 = min(nkt, kk0 + per_split);
+  const int Wq = A.par ? d.Wo >> 1 : d.Wo;
+  const int HWq = A.par ? (d.Ho >> 1) * Wq : d.Ho * d.Wo;
+  // pixel index of the layout (output tensor / split-K slab) for tile pixel p
+  auto pmap = [&](int p) -> int {
+    if (!A.par) return p;
+    const int n = p / HWq, rem = p - n * HWq, qy = rem / Wq, qx = rem - qy * Wq;
+    return (n * d.Ho + 2 * qy + cy) * d.Wo + 2 * qx + cx;
+  };
 
   const int HWo = d.Ho * d.Wo;
   const int cch = tid % CH;      // this thread's 16B chunk within a BK slice
@@ -69,11 +88,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   for (int j = 0; j < AX; ++j) {
     const int p = px0 + rbase + j * RPP;
     if (p < A.M) {
-      const int n = p / HWo;
-      const int rem = p - n * HWo;
+      const int n = p / HWq;
+      const int rem = p - n * HWq;
       pn[j] = n;
-      poy[j] = rem / d.Wo;
-      pox[j] = rem - poy[j] * d.Wo;
+      poy[j] = rem / Wq;
+      pox[j] = rem - poy[j] * Wq;
+      if (A.par) { poy[j] = 2 * poy[j] + cy; pox[j] = 2 * pox[j] + cx; }
     } else {
       pn[j] = -1; poy[j] = 0; pox[j] = 0;
     }
@@ -94,13 +114,17 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
 
   auto load = [&](int kk) {
     int c, tap = 0, seg;
-    if (kk < A.nk1) {
-      const int cb = kk / A.T;
-      tap = kk - cb * A.T;
+    if (kk < nk1) {
+      const int cb = kk / Tc;
+      tap = kk - cb * Tc;
+      if (A.par) {   // class-local tap -> 3x3 tap
+        const int iy = tap / nkx, ix = tap - (tap / nkx) * nkx;
+        tap = (cy ? 2 * iy : 1) * 3 + (cx ? 2 * ix : 1);
+      }
       c = cb * BK + cch * 8;
       seg = 0;
     } else {
-      c = (kk - A.nk1) * BK + cch * 8;
+      c = (kk - nk1) * BK + cch * 8;
       seg = 1;
     }
     cur_c = c;
@@ -260,14 +284,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
   if (d.splits > 1) {
-    float* ws = d.ws + (size_t)split * A.M * K;
+    float* ws = d.ws + (size_t)split * A.Mfull * K;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int co = co0 + wm * (BCO / WM) + 16 * i + 4 * lq;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int p = px0 + wn * (BPX / WN) + 16 * j + l16;
-        if (p >= A.M) continue;
+        const int pt = px0 + wn * (BPX / WN) + 16 * j + l16;
+        if (pt >= A.M) continue;
+        const int p = pmap(pt);
         float* dst = ws + (size_t)p * K + co;
         if (co + 3 < K) {
           *(f32x4*)dst = acc[i][j];
@@ -275,6 +300,70 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
           for (int r = 0; r < 4; ++r)
             if (co + r < K) dst[r] = acc[i][j][r];
         }
+      }
+    }
+    return;
+  }
+
+  if (GNA) {
+    // dx = acc + P*dz + Q*x + R (+ dx): the 1x1 skip-conv data gradient fused into the GroupNorm
+    // backward of the same ResBlock input (gn_bwd_apply with extra = this conv's output, which is
+    // rounded to bf16 exactly as that path stored it).  The tile goes through LDS so every global
+    // access below is a coalesced 16-byte one (16 threads = one pixel's 128 channels).
+    static_assert(BPX * BCO * 2 <= 2 * (BCO + BPX) * BK * 2, "GNA tile fits the staging LDS");
+    const fmd_gn_apply_desc& g = A.g;
+    const int C = K, C0 = g.C0, C1 = K - g.C0;
+    bf16r* tile = lds;   // [BPX][BCO] bf16, 16-byte chunk index ^ (pixel & 15)
+    constexpr int CHT = BCO / 8;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cl = wm * (BCO / WM) + 16 * i + 4 * lq;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int pi = wn * (BPX / WN) + 16 * j + l16;
+        u32x2 o;
+        o[0] = pack2(acc[i][j][0], acc[i][j][1]);
+        o[1] = pack2(acc[i][j][2], acc[i][j][3]);
+        *(u32x2*)(tile + pi * BCO + (((cl >> 3) ^ (pi & (CHT - 1))) * 8) + (cl & 7)) = o;
+      }
+    }
+    __syncthreads();
+    const int c16 = tid % CHT;
+    const int co = co0 + c16 * 8;
+    if (co < K) {
+      const bool first = co < C0;   // C0 % 8 == 0: the 8 channels are in one source
+      const int accf = first ? g.acc0 : g.acc1;
+#pragma unroll 2
+      for (int q = tid; q < BPX * CHT; q += 256) {
+        const int pi = q / CHT;
+        const int p = px0 + pi;
+        if (p >= A.M) break;
+        const int n = p / HWo;
+        const u32x4 ve = *(const u32x4*)(tile + pi * BCO + ((c16 ^ (pi & (CHT - 1))) * 8));
+        const u32x4 vz = *(const u32x4*)((const bf16r*)g.dz + (size_t)p * C + co);
+        const u32x4 vx = first ? *(const u32x4*)((const bf16r*)g.x0 + (size_t)p * C0 + co)
+                               : *(const u32x4*)((const bf16r*)g.x1 + (size_t)p * C1 + (co - C0));
+        bf16r* dst = first ? (bf16r*)g.dx0 + (size_t)p * C0 + co : (bf16r*)g.dx1 + (size_t)p * C1 + (co - C0);
+        u32x4 old = {0u, 0u, 0u, 0u};
+        if (accf) old = *(const u32x4*)dst;
+        const float* pp = g.P + (size_t)n * C + co;
+        const float* qq = g.Q + (size_t)n * C + co;
+        const float* rr = g.R + (size_t)n * C + co;
+        const f32x4 P0 = *(const f32x4*)pp, P1 = *(const f32x4*)(pp + 4);
+        const f32x4 Q0 = *(const f32x4*)qq, Q1 = *(const f32x4*)(qq + 4);
+        const f32x4 R0 = *(const f32x4*)rr, R1 = *(const f32x4*)(rr + 4);
+        const float Pv[8] = {P0[0], P0[1], P0[2], P0[3], P1[0], P1[1], P1[2], P1[3]};
+        const float Qv[8] = {Q0[0], Q0[1], Q0[2], Q0[3], Q1[0], Q1[1], Q1[2], Q1[3]};
+        const float Rv[8] = {R0[0], R0[1], R0[2], R0[3], R1[0], R1[1], R1[2], R1[3]};
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float lo = Pv[2 * e] * bf_lo(vz[e]) + Qv[2 * e] * bf_lo(vx[e]) + Rv[2 * e] + bf_lo(ve[e]);
+          float hi = Pv[2 * e + 1] * bf_hi(vz[e]) + Qv[2 * e + 1] * bf_hi(vx[e]) + Rv[2 * e + 1] + bf_hi(ve[e]);
+          if (accf) { lo += bf_lo(old[e]); hi += bf_hi(old[e]); }
+          o[e] = pack2(lo, hi);
+        }
+        *(u32x4*)dst = o;
       }
     }
     return;
@@ -303,8 +392,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int p = px0 + wn * (BPX / WN) + 16 * j + l16;
-      if (p >= A.M) continue;
+      const int pt = px0 + wn * (BPX / WN) + 16 * j + l16;
+      if (pt >= A.M) continue;
+      const int p = pmap(pt);
       const int n = p / HWo;
       float v[4];
 #pragma unroll
@@ -429,10 +519,11 @@ __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
   }
 }
 
-template <int BCO, int BPX, int WM, int WN, int BK>
-int launch(const fmd_conv_desc* d, hipStream_t s) {
+template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
+int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = nullptr) {
   KArgs A;
   A.d = *d;
+  if (g) A.g = *g;
   A.M = d->N * d->Ho * d->Wo;
   A.T = d->ks * d->ks;
   A.C = d->C0 + d->C1;
@@ -440,6 +531,10 @@ int launch(const fmd_conv_desc* d, hipStream_t s) {
   A.nk = A.nk1 + (d->src2 ? (d->C2 + d->C3 + BK - 1) / BK : 0);
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nk + splits - 1) / splits;
+  A.Mfull = A.M;
+  A.par = d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
+          !d->stats && !d->src2 && !GNA;
+  if (A.par) A.M = d->N * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
   A.ntp = (A.M + BPX - 1) / BPX;
   A.ntc = (d->K + BCO - 1) / BCO;
   A.stats_rows = 64;
@@ -448,8 +543,8 @@ int launch(const fmd_conv_desc* d, hipStream_t s) {
     const int wrows = BPX / WN;
     if (wrows != 64 || (d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
   }
-  dim3 grid(A.ntp * A.ntc, splits);
-  hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK>), grid, dim3(256), 0, s, A);
+  dim3 grid(A.ntp * A.ntc, splits, A.par ? 4 : 1);
+  hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);
   return (int)hipGetLastError();
 }
 
@@ -486,4 +581,17 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
   }
   return rc;
+}
+
+// 1x1 (or any generic-path) conv whose epilogue is the GroupNorm-backward apply of fmd_gn_bwd_apply:
+// dx = conv(...) + P*dz + Q*x + R (+ dx), split over the concat sources at g->C0.  d: no split-K, no
+// stats/bias/residual/out (the result only exists as dx).
+extern "C" int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if ((d->C0 % 8) || (d->C1 % 8) || (d->C2 % 8) || (d->C3 % 8) || d->ks < 1 || d->N < 1) return -1;
+  if (d->splits > 1 || d->stats || d->bias || d->bias2 || d->bias_nc || d->resid || d->ep_x0 || d->src2) return -5;
+  if (!g || !g->dz || !g->x0 || !g->P || !g->Q || !g->R || !g->dx0 || (g->C0 % 8)) return -7;
+  if (g->C0 < d->K && (!g->x1 || !g->dx1)) return -7;
+  if (d->K <= 64) return launch<64, 128, 2, 2, 64, true>(d, s, g);
+  return launch<128, 128, 2, 2, 64, true>(d, s, g);
 }

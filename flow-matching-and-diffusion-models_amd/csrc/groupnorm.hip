@@ -239,6 +239,12 @@ __global__ void gn_bwd_apply_kernel(const bf16r* __restrict__ dz, const bf16r* _
     const float* pp = P + (size_t)n * C + c;
     const float* qq = Q + (size_t)n * C + c;
     const float* rr = R + (size_t)n * C + c;
+    const f32x4 P0 = *(const f32x4*)pp, P1 = *(const f32x4*)(pp + 4);
+    const f32x4 Q0 = *(const f32x4*)qq, Q1 = *(const f32x4*)(qq + 4);
+    const f32x4 R0 = *(const f32x4*)rr, R1 = *(const f32x4*)(rr + 4);
+    const float Pv[8] = {P0[0], P0[1], P0[2], P0[3], P1[0], P1[1], P1[2], P1[3]};
+    const float Qv[8] = {Q0[0], Q0[1], Q0[2], Q0[3], Q1[0], Q1[1], Q1[2], Q1[3]};
+    const float Rv[8] = {R0[0], R0[1], R0[2], R0[3], R1[0], R1[1], R1[2], R1[3]};
     bf16r* dst = first ? dx0 + p * C0 + c : dx1 + p * C1 + (c - C0);
     const int acc = first ? acc0 : acc1;
     u32x4 old = {0u, 0u, 0u, 0u};
@@ -246,8 +252,8 @@ __global__ void gn_bwd_apply_kernel(const bf16r* __restrict__ dz, const bf16r* _
     u32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float lo = pp[2 * e] * bf_lo(vz[e]) + qq[2 * e] * bf_lo(vx[e]) + rr[2 * e];
-      float hi = pp[2 * e + 1] * bf_hi(vz[e]) + qq[2 * e + 1] * bf_hi(vx[e]) + rr[2 * e + 1];
+      float lo = Pv[2 * e] * bf_lo(vz[e]) + Qv[2 * e] * bf_lo(vx[e]) + Rv[2 * e];
+      float hi = Pv[2 * e + 1] * bf_hi(vz[e]) + Qv[2 * e + 1] * bf_hi(vx[e]) + Rv[2 * e + 1];
       if (extra) { lo += bf_lo(ve[e]); hi += bf_hi(ve[e]); }
       if (acc) { lo += bf_lo(old[e]); hi += bf_hi(old[e]); }
       o[e] = pack2(lo, hi);

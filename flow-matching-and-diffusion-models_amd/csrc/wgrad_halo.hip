@@ -104,9 +104,12 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       const int pos = q >> 3;
       const bool act = pos < HPOSW;
       const int hy = act ? pos / HR : 0, hx = act ? pos - (pos / HR) * HR : 0;
+      // logical (possibly nearest-x2-upsampled) input coordinates; the upsample is a gather of the
+      // stored low-resolution pixel, so the LDS image is the same as without it
       const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-      const bool valid = act && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
-      const int pix = valid ? (n * d.Hs + y) * d.Ws + x : 0;
+      const bool valid = act && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
+      const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
+      const int pix = valid ? (n * d.Hs + sy) * d.Ws + sx : 0;
       rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
     }
@@ -242,11 +245,12 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 
 }  // namespace
 
-// 3x3 / stride 1 / pad 1 / no upsample, K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
+// 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
 // Returns 1 (nothing launched) when the problem does not qualify.  d->splits = pixel-tile splits.
 extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->upsample) return 1;
-  if (d->Ho != d->Hs || d->Wo != d->Ws || d->Ho % WTH || d->Wo % WTW) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1) return 1;
+  if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
+  if (d->Ho % WTH || d->Wo % WTW) return 1;
   const int C = d->C0 + d->C1;
   if (d->K % WCO || C % WCI || (d->C0 % 8) || !d->ws) return 1;
   const int ldy = d->ldy > 0 ? d->ldy : d->K;

@@ -39,10 +39,19 @@ class WgradDesc(C.Structure):
     ]
 
 
+class GnApplyDesc(C.Structure):
+    """Mirror of ``fmd_gn_apply_desc``."""
+    _fields_ = [
+        ("dz", p), ("x0", p), ("x1", p), ("C0", i32), ("P", p), ("Q", p), ("R", p),
+        ("dx0", p), ("acc0", i32), ("dx1", p), ("acc1", i32),
+    ]
+
+
 # name -> argtypes (restype is int32 unless listed in _RESTYPE)
 SIGNATURES = {
     "fmd_conv": [C.POINTER(ConvDesc), p],
     "fmd_conv_halo": [C.POINTER(ConvDesc), p],
+    "fmd_conv_gn_apply": [C.POINTER(ConvDesc), C.POINTER(GnApplyDesc), p],
     "fmd_wgrad": [C.POINTER(WgradDesc), p],
     "fmd_wgrad_workspace": [C.POINTER(WgradDesc)],
     "fmd_wgrad_halo": [C.POINTER(WgradDesc), p],

@@ -365,8 +365,7 @@ class UNetEngine:
             else:
                 sc = sk.conv
                 ops.wgrad(x0.t, dy, sc.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0, db=sc.bias.grad)
-                extra, _ = ops.conv(dy, Cin, self.wc.get(sc.weight, 1), ks=1, pad=0, transposed=True,
-                                    out_hw_=(H, W))
+                extra = None   # the skip data gradient is fused into the GroupNorm-1 backward below
             dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, H, W, ep=(h, None, a2, b2), want_stats=True)
             if slot is not None:
                 demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
@@ -393,7 +392,11 @@ class UNetEngine:
                                          g1.bias.grad)
             d0, acc0 = _gdest(x0)
             d1, acc1 = _gdest(x1)
-            ops.gn_bwd_apply(dz1, x0.t, x1.t if x1 else None, P1, Q1, R1, extra, d0, acc0, d1, acc1)
+            if isinstance(sk, Identity):
+                ops.gn_bwd_apply(dz1, x0.t, x1.t if x1 else None, P1, Q1, R1, extra, d0, acc0, d1, acc1)
+            else:
+                ops.conv1x1_gn_apply(dy, self.wc.get(sk.conv.weight, 1), dz1, x0.t, x1.t if x1 else None,
+                                     P1, Q1, R1, d0, acc0, d1, acc1)
             if (ss or add) and slot is None:
                 ops.linear_bwd(ctx.emb, el.weight, demb, el.weight.grad, el.bias.grad, dx=ctx.demb, dx_acc=True,
                                in_silu=m.emb_activation_before_proj)

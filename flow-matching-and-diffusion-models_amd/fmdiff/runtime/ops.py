@@ -13,7 +13,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import _lib
-from .._lib import ConvDesc, WgradDesc
+from .._lib import ConvDesc, GnApplyDesc, WgradDesc
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -88,6 +88,24 @@ def gn_bwd_apply(dz, x0, x1, P, Q, R, extra, dx0, acc0, dx1=None, acc1=0):
     C1 = x1.shape[-1] if x1 is not None else 0
     _lib.call("fmd_gn_bwd_apply", _p(dz), _p(x0), _p(x1), C0, C1, N * H * W, H * W, _p(P), _p(Q), _p(R),
               _p(extra), _p(dx0), int(acc0), _p(dx1), int(acc1), stream())
+
+
+def conv1x1_gn_apply(dy, wgt_t, dz, x0, x1, P, Q, R, dx0, acc0, dx1=None, acc1=0):
+    """dx = dy @ W^T (1x1 data gradient, ``wgt_t`` = mode-1 weights [C][1][K]) + P*dz + Q*x + R (+ dx):
+    the ResBlock skip-conv data gradient fused into the block input's GroupNorm backward
+    (fmd_conv_gn_apply; == conv(..., transposed=True) followed by gn_bwd_apply(extra=...))."""
+    _need_cuda(dy, "conv1x1_gn_apply")
+    N, H, W, Kd = dy.shape
+    Ct = dz.shape[-1]
+    d = ConvDesc()
+    d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, H, W, Kd, 0, H, W, Ct
+    d.ks, d.stride, d.pad, d.upsample, d.transposed = 1, 1, 0, 0, 1
+    d.src0, d.wgt, d.splits = _p(dy), _p(wgt_t), 1
+    g = GnApplyDesc()
+    g.dz, g.x0, g.x1, g.C0 = _p(dz), _p(x0), _p(x1), x0.shape[-1]
+    g.P, g.Q, g.R = _p(P), _p(Q), _p(R)
+    g.dx0, g.acc0, g.dx1, g.acc1 = _p(dx0), int(acc0), _p(dx1), int(acc1)
+    _lib.call("fmd_conv_gn_apply", C.byref(d), C.byref(g), stream())
 
 
 def out_hw(Hs, ks, stride, pad, upsample):
@@ -220,7 +238,8 @@ def head_wgrad(dpred, K, h, pro, dw, db):
 
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
     """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip)."""
-    return (ks == 3 and stride == 1 and pad == 1 and not upsample and Ho == Hs and Wo == Ws and Ho % 8 == 0
+    return (ks == 3 and stride == 1 and pad == 1 and (Ho == 2 * Hs and Wo == 2 * Ws if upsample else
+                                                      Ho == Hs and Wo == Ws) and Ho % 8 == 0
             and Wo % 16 == 0 and K % 128 == 0 and C % 64 == 0 and C0 % 8 == 0 and (ldy or K) % 8 == 0)
 
 

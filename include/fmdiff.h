@@ -78,6 +78,25 @@ typedef struct fmd_conv_desc {
 int fmd_conv(const fmd_conv_desc* d, fmd_stream_t s);
 /* Halo-tiled 3x3 stride-1 conv; returns 1 (nothing launched) when the problem does not qualify. */
 int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t s);
+/* GroupNorm-backward apply fused as a conv epilogue (fmd_conv_gn_apply):
+ * dx = conv(d) + P*dz + Q*x + R (+ dx if acc), x/dx split over two concat sources at C0. */
+typedef struct fmd_gn_apply_desc {
+  const void* dz;           /* bf16 [M][C] (C = the conv's K) */
+  const void* x0;           /* bf16 [M][C0] forward GroupNorm input */
+  const void* x1;           /* bf16 [M][C - C0] or NULL */
+  int32_t C0;
+  const float* P;           /* [N][C] */
+  const float* Q;
+  const float* R;
+  void* dx0;                /* bf16 [M][C0] */
+  int32_t acc0;
+  void* dx1;                /* bf16 [M][C - C0] or NULL */
+  int32_t acc1;
+} fmd_gn_apply_desc;
+/* The ResBlock skip-conv data gradient fused into the GroupNorm backward of the block input
+ * (replaces conv(dy, W_skip^T) + fmd_gn_bwd_apply(extra = that)). */
+int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_stream_t s);
+
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */

@@ -109,9 +109,13 @@ def test_conv_splitk_matches():
     _close(b, a.float(), rel=8e-3)
 
 
-@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1"])
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "s2_split"])
 def test_conv_data_gradient(mode):
+    """Data gradients through the generic implicit GEMM; s2 runs the parity-class decomposition of the
+    stride-2 transposed gather (csrc/conv.hip ``par``), s2_split the same with split-K partial slabs."""
     O = ops()
+    split = mode.endswith("_split")
+    mode = mode.replace("_split", "")
     N, H, W, C, K = 2, 16, 16, 64, 128
     ks, s, up = (1, 1, False) if mode == "1x1" else (3, 2 if mode == "s2" else 1, mode == "up")
     pad = ks // 2
@@ -126,11 +130,11 @@ def test_conv_data_gradient(mode):
         got, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 2), ks=4, stride=2, pad=1, out_hw_=(H, W))
     else:
         got, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 1), ks=ks, stride=s, pad=pad, transposed=True,
-                        out_hw_=(H, W))
+                        out_hw_=(H, W), splits=3 if split else None)
     _close(got, x.grad.permute(0, 2, 3, 1))
 
 
-@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro", "s1_generic", "pro_generic"])
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro", "s1_generic", "pro_generic", "up_generic"])
 def test_wgrad(mode):
     """16x16, C=64, K=128: the 3x3 stride-1 modes run the halo kernel (csrc/wgrad_halo.hip) unless *_generic."""
     O = ops()
@@ -443,3 +447,30 @@ def test_head_kernels_vs_torch(K):
     dzd = dz.double().cpu().view(N, -1, C)
     torch.testing.assert_close(s[..., 0], dzd.sum(1), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(s[..., 1], (dzd * xs).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("C0,C1,Kd", [(128, 128, 128), (64, 0, 256), (256, 128, 128)])
+def test_conv1x1_gn_apply_vs_torch(C0, C1, Kd):
+    """fmd_conv_gn_apply: the ResBlock skip-conv data gradient (dy @ W_skip) fused into the GroupNorm
+    backward apply dx = P*dz + Q*x + R + extra (+ dx), over a two-source concat, vs torch fp32."""
+    O = ops()
+    N, H, W = 2, 16, 16
+    C = C0 + C1
+    g = torch.Generator().manual_seed(21)
+    dy = _rand_nhwc(N, H, W, Kd, 22)
+    w = torch.randn(Kd, C, 1, 1, generator=g) / math.sqrt(Kd)
+    dz = _rand_nhwc(N, H, W, C, 23)
+    x = _rand_nhwc(N, H, W, C, 24)
+    P, Q, R = (torch.randn(N, C, generator=g) * s for s in (1.0, 0.3, 0.1))
+    old0 = _rand_nhwc(N, H, W, C0, 25)
+    ref = (dy.float().view(N, -1, Kd) @ _bfw(w).view(Kd, C)).view(N, H, W, C)
+    ref = ref + P[:, None, None] * dz.float() + Q[:, None, None] * x.float() + R[:, None, None]
+    ref[..., :C0] += old0.float()
+    d0 = old0.to(DEV).contiguous()
+    d1 = torch.empty(N, H, W, C1, device=DEV, dtype=torch.bfloat16) if C1 else None
+    x0 = x[..., :C0].contiguous().to(DEV)
+    x1 = x[..., C0:].contiguous().to(DEV) if C1 else None
+    O.conv1x1_gn_apply(dy.to(DEV), O.prep_weights(w.to(DEV), 1), dz.to(DEV), x0, x1, P.to(DEV), Q.to(DEV),
+                       R.to(DEV), d0, 1, d1, 0)
+    got = torch.cat([d0, d1], -1) if C1 else d0
+    _close(got, ref)
