@@ -213,7 +213,17 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_kernel(const bf16r* __restrict
 // 16-byte loads -- the raw-reshape head split is undone during staging by 32-bit index math on the
 // head's contiguous channel slice -- then 4 lanes per query (or key) split the head dim, so a
 // 256-thread block covers 64 rows and the dot-product chains are dh/4 deep.
-constexpr int SQ = 64;            // rows per block
+// all-reduce over each group of LPR (4 or 16) consecutive lanes with DPP (VALU, no LDS crossbar)
+template <int LPR>
+FMD_DEV float group_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false));
+  if (LPR == 16) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xf, 0xf, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xf, 0xf, false));
+  }
+  return v;
+}
 constexpr int SLAB_MAX = 7936;    // T * dh: two fp32 [T][dh] planes (+ 2T) stay under 64 KiB of LDS
 
 struct Slab {
@@ -276,7 +286,7 @@ FMD_DEV void stage_qkv(const bf16r* base, const Slab& S, float scale, float* qs,
   }
 }
 
-template <int DG>
+template <int DG, int LPR>
 __global__ __launch_bounds__(256) void attn_fwd_slab(const bf16r* __restrict__ qkv, Slab S, int heads,
                                                      bf16r* __restrict__ o, float* __restrict__ lse) {
   extern __shared__ float sm[];
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(256) void attn_fwd_slab(const bf16r* __restrict__ q
   const float scale = 1.0f / sqrtf((float)dh);
   stage_qkv(base, S, scale, nullptr, ks, vs);
   __syncthreads();
-  const int r = blockIdx.x * SQ + (threadIdx.x >> 2), g = threadIdx.x & 3;
+  const int r = blockIdx.x * (256 / LPR) + (int)(threadIdx.x / LPR), g = threadIdx.x & (LPR - 1);
   const bool live = r < T;
   const int d0 = g * DG;
   float q[DG], acc[DG];
@@ -304,8 +314,7 @@ __global__ __launch_bounds__(256) void attn_fwd_slab(const bf16r* __restrict__ q
 #pragma unroll
     for (int i = 0; i < DG; ++i)
       if (d0 + i < dh) sc += q[i] * ks[j * dh + d0 + i];
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
+    sc = group_sum<LPR>(sc);
     const float mn = fmaxf(m, sc);
     const float corr = __expf(m - mn);
     const float p = __expf(sc - mn);
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(256) void attn_fwd_slab(const bf16r* __restrict__ q
 }
 
 // dQ per query row: delta = dO.O, dS = P (dO.V - delta), dQ = scale * sum_k dS K
-template <int DG>
+template <int DG, int LPR>
 __global__ __launch_bounds__(256) void attn_bwd_q_slab(const bf16r* __restrict__ qkv, const bf16r* __restrict__ o,
                                                        const bf16r* __restrict__ dout, const float* __restrict__ lse,
                                                        Slab S, int heads, float* __restrict__ delta,
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_slab(const bf16r* __restrict__
   const float scale = 1.0f / sqrtf((float)dh);
   stage_qkv(base, S, scale, nullptr, ks, vs);
   __syncthreads();
-  const int r = blockIdx.x * SQ + (threadIdx.x >> 2), g = threadIdx.x & 3;
+  const int r = blockIdx.x * (256 / LPR) + (int)(threadIdx.x / LPR), g = threadIdx.x & (LPR - 1);
   const bool live = r < T;
   const int d0 = g * DG;
   const bf16r* ob = o + (size_t)b * T * S.inner;
@@ -355,18 +364,15 @@ __global__ __launch_bounds__(256) void attn_bwd_q_slab(const bf16r* __restrict__
     dl += ok ? dov[i] * bf2f(ob[S.o_off(r, d0 + i)]) : 0.f;
     dq[i] = 0.f;
   }
-  dl += __shfl_xor(dl, 1, 64);
-  dl += __shfl_xor(dl, 2, 64);
+  dl = group_sum<LPR>(dl);
   const float L = live ? lse[((size_t)b * heads + S.h) * T + r] : 0.f;
   for (int j = 0; j < T; ++j) {
     float sc = 0.f, dp = 0.f;
 #pragma unroll
     for (int i = 0; i < DG; ++i)
       if (d0 + i < dh) { sc += q[i] * ks[j * dh + d0 + i]; dp += dov[i] * vs[j * dh + d0 + i]; }
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
-    dp += __shfl_xor(dp, 1, 64);
-    dp += __shfl_xor(dp, 2, 64);
+    sc = group_sum<LPR>(sc);
+    dp = group_sum<LPR>(dp);
     const float ds = __expf(sc - L) * (dp - dl);
 #pragma unroll
     for (int i = 0; i < DG; ++i)
@@ -381,7 +387,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_slab(const bf16r* __restrict__
 }
 
 // dK, dV per key row: dV = sum_q P dO, dK = sum_q dS (scale Q)
-template <int DG>
+template <int DG, int LPR>
 __global__ __launch_bounds__(256) void attn_bwd_kv_slab(const bf16r* __restrict__ qkv, const bf16r* __restrict__ dout,
                                                         const float* __restrict__ lse,
                                                         const float* __restrict__ delta, Slab S, int heads,
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_slab(const bf16r* __restrict_
     dls[e] = delta[((size_t)b * heads + S.h) * T + e];
   }
   __syncthreads();
-  const int r = blockIdx.x * SQ + (threadIdx.x >> 2), g = threadIdx.x & 3;
+  const int r = blockIdx.x * (256 / LPR) + (int)(threadIdx.x / LPR), g = threadIdx.x & (LPR - 1);
   const bool live = r < T;
   const int d0 = g * DG;
   float kv[DG], vv[DG], dk[DG], dv[DG];
@@ -422,10 +428,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_slab(const bf16r* __restrict_
 #pragma unroll
     for (int i = 0; i < DG; ++i)
       if (d0 + i < dh) { sc += qs[j * dh + d0 + i] * kv[i]; dp += dos[j * dh + d0 + i] * vv[i]; }
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
-    dp += __shfl_xor(dp, 1, 64);
-    dp += __shfl_xor(dp, 2, 64);
+    sc = group_sum<LPR>(sc);
+    dp = group_sum<LPR>(dp);
     const float p = __expf(sc - ls[j]);
     const float ds = p * (dp - dls[j]);
 #pragma unroll
@@ -442,11 +446,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_slab(const bf16r* __restrict_
     }
 }
 
+// (DG, LPR): head-dim elements per lane and lanes per row; 16 lanes per row once dh >= 32, so a
+// T = 64 head needs 4 blocks and a 8-image batch with 4 heads fills 128 blocks
 template <typename F>
 int dispatch_dg(int dh, F&& f) {
-  if (dh <= 8) return f(std::integral_constant<int, 2>{});
-  if (dh <= 32) return f(std::integral_constant<int, 8>{});
-  return f(std::integral_constant<int, 16>{});
+  if (dh <= 8) return f(std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
+  if (dh <= 16) return f(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
+  if (dh <= 32) return f(std::integral_constant<int, 2>{}, std::integral_constant<int, 16>{});
+  return f(std::integral_constant<int, 4>{}, std::integral_constant<int, 16>{});
 }
 
 }  // namespace
@@ -456,10 +463,11 @@ extern "C" int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t 
   if (dh > DMAX || dh < 1) return -1;
   if (T * dh <= SLAB_MAX && dh % 8 == 0) {
     Slab S{T, dh, heads * dh, raw, 0};
-    const dim3 grid((T + SQ - 1) / SQ, heads, B);
     const size_t shm = (size_t)2 * T * dh * 4;
-    return dispatch_dg(dh, [&](auto dg) {
-      hipLaunchKernelGGL((attn_fwd_slab<decltype(dg)::value>), grid, dim3(256), shm, (hipStream_t)s,
+    return dispatch_dg(dh, [&](auto dg, auto lpr) {
+      constexpr int LPR = decltype(lpr)::value;
+      const dim3 grid((T + 256 / LPR - 1) / (256 / LPR), heads, B);
+      hipLaunchKernelGGL((attn_fwd_slab<decltype(dg)::value, LPR>), grid, dim3(256), shm, (hipStream_t)s,
                          (const bf16r*)qkv, S, heads, (bf16r*)o, lse);
       return (int)hipGetLastError();
     });
@@ -476,14 +484,14 @@ extern "C" int fmd_attention_bwd(const void* qkv, const void* o, const void* dou
   if (dh > DMAX || dh < 1) return -1;
   if (T * dh <= SLAB_MAX && dh % 8 == 0) {
     Slab S{T, dh, heads * dh, raw, 0};
-    const dim3 grid((T + SQ - 1) / SQ, heads, B);
-    return dispatch_dg(dh, [&](auto dg) {
-      constexpr int DG = decltype(dg)::value;
-      hipLaunchKernelGGL((attn_bwd_q_slab<DG>), grid, dim3(256), (size_t)2 * T * dh * 4, (hipStream_t)s,
+    return dispatch_dg(dh, [&](auto dg, auto lpr) {
+      constexpr int DG = decltype(dg)::value, LPR = decltype(lpr)::value;
+      const dim3 grid((T + 256 / LPR - 1) / (256 / LPR), heads, B);
+      hipLaunchKernelGGL((attn_bwd_q_slab<DG, LPR>), grid, dim3(256), (size_t)2 * T * dh * 4, (hipStream_t)s,
                          (const bf16r*)qkv, (const bf16r*)o, (const bf16r*)dout, lse, S, heads, delta, (bf16r*)dqkv);
       int rc = (int)hipGetLastError();
       if (rc) return rc;
-      hipLaunchKernelGGL((attn_bwd_kv_slab<DG>), grid, dim3(256), (size_t)(2 * T * dh + 2 * T) * 4,
+      hipLaunchKernelGGL((attn_bwd_kv_slab<DG, LPR>), grid, dim3(256), (size_t)(2 * T * dh + 2 * T) * 4,
                          (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)dout, lse, delta, S, heads,
                          (bf16r*)dqkv);
       return (int)hipGetLastError();

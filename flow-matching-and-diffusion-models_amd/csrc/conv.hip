@@ -556,7 +556,7 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if ((d->C0 % 8) || (d->C1 % 8) || (d->C2 % 8) || (d->C3 % 8) || d->ks < 1 || d->N < 1) return -1;
   if (d->C3 && !d->src3) return -6;
   if (d->C1 && !d->src1) return -2;
-  if (d->src2 && !d->wgt2) return -3;
+  if (d->src2 && !d->wgt2 && !d->wgt2_tiled) return -3;
   if (d->pro_a && !d->pro_b) return -4;
   if (d->splits > 1 && (!d->ws || d->stats)) return -5;
   (void)C;
@@ -565,6 +565,7 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
     rc = fmd_conv_halo(d, stream);   // 3x3 stride-1 problems with >= 128 16x16 tiles
     if (rc != 1) return rc;
   }
+  if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
   if (d->K <= 16)
     rc = launch<16, 256, 1, 4, 64>(d, s);
   else if (d->K <= 64)

@@ -259,8 +259,11 @@ class UNetEngine:
         """Plain 3x3 conv (input conv, DownsampleND, UpsampleND)."""
         _check_conv(conv, 3, stride, 1)
         Cin = x.C
-        w = self.wc.get(conv.weight, 0, None, Cin)
-        wt = self.wc.tiled(conv.weight, 0, None, Cin) if stride == 1 else None
+        N_, Hs_, Ws_, _ = x.t.shape
+        Ho_ = ops.out_hw(Hs_, 3, stride, 1, upsample)
+        halo = stride == 1 and ops.halo_eligible(N_, Hs_, Ho_, ops.out_hw(Ws_, 3, stride, 1, upsample),
+                                                 conv.out_channels, upsample=upsample)
+        w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
                            bias=conv.bias, want_stats=True, wgt_tiled=wt)
         o = Act(out, st)
@@ -284,12 +287,20 @@ class UNetEngine:
             ctx.tape.append(bwd)
         return o
 
+    def _wts(self, w, mode, halo: bool, Kpad=None, Cpad=None):
+        """(base, tiled) kernel layouts of ``w``: only the one the chosen conv path reads is derived
+        (and refreshed by every optimizer step), the other is None."""
+        if halo:
+            return None, self.wc.tiled(w, mode, Kpad, Cpad)
+        return self.wc.get(w, mode, Kpad, Cpad), None
+
     def dgrad3x3(self, w, dy, Cin, H, W, *, stride=1, Kpad=None, **kw):
         """Data gradient of a 3x3 pad-1 conv.  Stride 1 = forward gather with flipped taps (so it runs on
         the halo-tiled kernel); stride 2 = transposed gather."""
         if stride == 1:
-            return ops.conv(dy, Cin, self.wc.get(w, 3, Kpad, None), ks=3, stride=1, pad=1, out_hw_=(H, W),
-                            wgt_tiled=self.wc.tiled(w, 3, Kpad, None), **kw)
+            halo = ops.halo_eligible(dy.shape[0], H, H, W, Cin)
+            base, tiled = self._wts(w, 3, halo, Kpad, None)
+            return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=(H, W), wgt_tiled=tiled, **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,
                         out_hw_=(H, W), **kw)
 
@@ -333,9 +344,11 @@ class UNetEngine:
             eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
             es = eo.shape[1]
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
-        h, hst = ops.conv(x0.t, Cout, self.wc.get(c1.weight, 0), src1=x1.t if x1 else None, pro=(a1, b1, True),
+        halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
+        w1, w1t = self._wts(c1.weight, 0, halo1)
+        h, hst = ops.conv(x0.t, Cout, w1, src1=x1.t if x1 else None, pro=(a1, b1, True),
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=True,
-                          wgt_tiled=self.wc.tiled(c1.weight, 0))
+                          wgt_tiled=w1t)
         if ss:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
                                       emb_stride=es, emb_mode=1)
@@ -349,10 +362,12 @@ class UNetEngine:
             kw["resid"] = x0.t
         else:
             _check_conv(sk.conv, 1, 1, 0)
-            kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=self.wc.get(sk.conv.weight, 0),
-                      wgt2_tiled=self.wc.tiled(sk.conv.weight, 0), bias2=sk.conv.bias)
-        out, ost = ops.conv(h, Cout, self.wc.get(c2.weight, 0), pro=(a2, b2, True), bias=c2.bias, want_stats=True,
-                            wgt_tiled=self.wc.tiled(c2.weight, 0), **kw)
+        halo2 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cout, pro=True)
+        if not isinstance(sk, Identity):
+            s2, s2t = self._wts(sk.conv.weight, 0, halo2)
+            kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
+        w2, w2t = self._wts(c2.weight, 0, halo2)
+        out, ost = ops.conv(h, Cout, w2, pro=(a2, b2, True), bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
         o = Act(out, ost)
         if ctx.tape is None:
             return o

@@ -236,7 +236,7 @@ def test_groupnorm_forward_backward():
     torch.testing.assert_close(demb[:, C:].cpu(), dz.sum((2, 3)), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32)])
+@pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32), (1, 64, 2, 16)])
 def test_attention(raw, T, heads, dh):
     O = ops()
     B = 2
