@@ -235,6 +235,13 @@ class UNetEngine:
             raise TypeError(type(model))
         self.wc = WeightCache()
         self.gl, self.gl_slot = self._group_emb_layers(model)
+        # weight gradients (+ their split-K reductions) may run on a second HIP stream beside the
+        # data-gradient chain (they are off its critical path until the optimizer step).  Off by default:
+        # measured on MI355X the halo wgrad/dgrad kernels then contend for LDS and the step does not
+        # get faster (28.9 vs 28.8 ms).
+        self.side_stream_wgrad = False
+        self._side = None
+        self._side_keep = []
 
     @staticmethod
     def _group_emb_layers(model):
@@ -272,9 +279,13 @@ class UNetEngine:
 
             def bwd():
                 dy = o.grad
-                ops.wgrad(x.t, dy, self._wgrad_target(conv, Cin), ks=3, stride=stride, pad=1, upsample=upsample,
-                          db=conv.bias.grad if conv.bias is not None else None)
-                self._wgrad_finish(conv, Cin)
+
+                def wg():
+                    tgt = self._wgrad_target(conv, Cin)
+                    ops.wgrad(x.t, dy, tgt, ks=3, stride=stride, pad=1, upsample=upsample,
+                              db=conv.bias.grad if conv.bias is not None else None)
+                    self._wgrad_finish(conv, Cin, tgt)
+                self._wg(wg)
                 if not x.need_grad:
                     return
                 if upsample:
@@ -286,6 +297,25 @@ class UNetEngine:
                     self.dgrad3x3(conv.weight, dy, Cin, H, W, stride=stride, out=g, accumulate=bool(acc))
             ctx.tape.append(bwd)
         return o
+
+    def _wg(self, fn):
+        """Issue ``fn`` (weight-gradient work) on the side stream after everything queued so far on the
+        current stream; ``fn`` (and so every tensor it references) is kept alive until ``_join``."""
+        if not self.side_stream_wgrad:
+            fn()
+            return
+        main = torch.cuda.current_stream()
+        if self._side is None or self._side.device != main.device:
+            self._side = torch.cuda.Stream(device=main.device)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            fn()
+        self._side_keep.append(fn)
+
+    def _join(self):
+        if self._side is not None and self._side_keep:
+            torch.cuda.current_stream().wait_stream(self._side)
+        self._side_keep = []
 
     def _wts(self, w, mode, halo: bool, Kpad=None, Cpad=None):
         """(base, tiled) kernel layouts of ``w``: only the one the chosen conv path reads is derived
@@ -308,16 +338,14 @@ class UNetEngine:
         """fp32 buffer the wgrad kernel writes: param.grad itself unless channels were padded."""
         if conv.weight.shape[1] == Cin and conv.weight.shape[0] % 8 == 0:
             return conv.weight.grad
-        self._pad_tmp = torch.zeros((max(8, -(-conv.weight.shape[0] // 8) * 8), Cin, *conv.weight.shape[2:]),
-                                    device=conv.weight.device, dtype=F32)
-        return self._pad_tmp
+        return torch.zeros((max(8, -(-conv.weight.shape[0] // 8) * 8), Cin, *conv.weight.shape[2:]),
+                           device=conv.weight.device, dtype=F32)
 
-    def _wgrad_finish(self, conv: Conv, Cin: int):
-        if conv.weight.shape[1] == Cin and conv.weight.shape[0] % 8 == 0:
+    def _wgrad_finish(self, conv: Conv, Cin: int, tgt):
+        if tgt is conv.weight.grad:
             return
         K, C = conv.weight.shape[:2]
-        conv.weight.grad.add_(self._pad_tmp[:K, :C])
-        self._pad_tmp = None
+        conv.weight.grad.add_(tgt[:K, :C])
 
     def res_block(self, m: ResBlockND, xs: List[Act], ctx: Ctx):
         x0 = xs[0]
@@ -374,13 +402,15 @@ class UNetEngine:
 
         def bwd():
             dy = o.grad
-            ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
-            if isinstance(sk, Identity):
-                extra = dy
-            else:
-                sc = sk.conv
-                ops.wgrad(x0.t, dy, sc.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0, db=sc.bias.grad)
-                extra = None   # the skip data gradient is fused into the GroupNorm-1 backward below
+
+            def wg2():
+                ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
+                if not isinstance(sk, Identity):
+                    ops.wgrad(x0.t, dy, sk.conv.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0,
+                              db=sk.conv.bias.grad)
+            self._wg(wg2)
+            # the skip data gradient (non-identity) is fused into the GroupNorm-1 backward below
+            extra = dy if isinstance(sk, Identity) else None
             dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, H, W, ep=(h, None, a2, b2), want_stats=True)
             if slot is not None:
                 demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
@@ -400,7 +430,8 @@ class UNetEngine:
             dh = torch.empty_like(h)
             ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
             del dz2
-            ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True), db=c1.bias.grad)
+            self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
+                                       db=c1.bias.grad))
             dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, H, W, ep=(x0.t, x1.t if x1 else None, a1, b1),
                                     want_stats=True)
             P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,
@@ -451,15 +482,17 @@ class UNetEngine:
 
         def bwd():
             dy = y.grad
-            ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad)
+            self._wg(lambda: ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad))
             do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
             dqkv = ops.attention_bwd(qkv, o, do, lse, T, heads, dh, raw)
-            if qparts is None:
-                ops.wgrad(x.t, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
-            else:
-                for i, l in enumerate(qparts):
-                    ops.wgrad(x.t, dqkv, l.weight.grad, ks=1, pad=0, pro=(a, b, False), db=l.bias.grad,
-                              dy_offset=i * inner)
+            def wgq():
+                if qparts is None:
+                    ops.wgrad(x.t, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
+                else:
+                    for i, l in enumerate(qparts):
+                        ops.wgrad(x.t, dqkv, l.weight.grad, ks=1, pad=0, pro=(a, b, False), db=l.bias.grad,
+                                  dy_offset=i * inner)
+            self._wg(wgq)
             dz, s12 = ops.conv(dqkv, Cc, self.wc.get(wq, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W),
                                ep=(x.t, None, None, None), want_stats=True)
             P, Q, R = ops.gn_bwd_prep(s12, N, T, Cc, norm.num_groups, mr, norm.weight, norm.bias, norm.weight.grad,
@@ -481,8 +514,8 @@ class UNetEngine:
             out = ops.head_fwd(h.t, (a, b), conv.weight, conv.bias, K, Kp)
             if ctx.tape is not None:
                 def bwd(dpred):
-                    ops.head_wgrad(dpred, K, h.t, (a, b), conv.weight.grad,
-                                   conv.bias.grad if conv.bias is not None else None)
+                    self._wg(lambda: ops.head_wgrad(dpred, K, h.t, (a, b), conv.weight.grad,
+                                                    conv.bias.grad if conv.bias is not None else None))
                     dz, s12 = ops.head_dgrad(dpred, conv.weight, K, h.t, (a, b))
                     P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
                                               norm.weight.grad, norm.bias.grad)
@@ -495,11 +528,13 @@ class UNetEngine:
         out, _ = ops.conv(h.t, Kp, w, pro=(a, b, True), bias=bias, out_f32=True)
         if ctx.tape is not None:
             def bwd(dpred):
-                tmpw = torch.zeros((Kp, Cc, 3, 3), device=out.device, dtype=F32)
-                tmpb = torch.zeros((Kp,), device=out.device, dtype=F32)
-                ops.wgrad(h.t, dpred, tmpw, pro=(a, b, True), db=tmpb, accumulate=False)
-                conv.weight.grad.add_(tmpw[:K])
-                conv.bias.grad.add_(tmpb[:K])
+                def wgh():
+                    tmpw = torch.zeros((Kp, Cc, 3, 3), device=out.device, dtype=F32)
+                    tmpb = torch.zeros((Kp,), device=out.device, dtype=F32)
+                    ops.wgrad(h.t, dpred, tmpw, pro=(a, b, True), db=tmpb, accumulate=False)
+                    conv.weight.grad.add_(tmpw[:K])
+                    conv.bias.grad.add_(tmpb[:K])
+                self._wg(wgh)
                 dz, s12 = self.dgrad3x3(conv.weight, dpred, Cc, H, W, Kpad=Kp, ep=(h.t, None, a, b),
                                         want_stats=True)
                 P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
@@ -614,6 +649,7 @@ class UNetEngine:
         self._head_bwd(dpred)
         for fn in reversed(ctx.tape):
             fn()
+        self._join()   # every weight gradient has landed before anyone reads .grad
         ctx.tape = None
         self._head_bwd = None
 
