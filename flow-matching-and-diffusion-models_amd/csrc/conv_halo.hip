@@ -49,11 +49,17 @@ struct HArgs {
   int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
   const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
-  unsigned long long* trace;   // debug: s_memtime per phase for the first TRACE_WG workgroups, else null
+  int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
+                               // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
 };
 
-constexpr int TRACE_WG = 16, TRACE_STEPS = 40, TRACE_PH = 4;
-static unsigned long long* g_trace = nullptr;
+#ifdef FMD_HALO_DBG
+#define HDBG(bit) (A.dbg & (bit))
+#else
+#define HDBG(bit) false
+#endif
+
+static int g_dbg = 0;
 
 // staged piece h (16 bytes) of a chunk: blocks of 32 = 8 consecutive positions x KC channel groups
 FMD_DEV int piece_pos(int h) { return (h >> 5) * 8 + (h & 7); }
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
   auto store = [&](int buf, int k, bool transform, int c) {
     u32x4 v = rh[k];
-    if (PRO != 0 && transform) {
+    if (PRO != 0 && transform && !HDBG(2)) {
       const f32x4 a0 = *(const f32x4*)(coef + c), a1 = *(const f32x4*)(coef + c + 4);
       const f32x4 b0 = *(const f32x4*)(coef + A.C + c), b1 = *(const f32x4*)(coef + A.C + c + 4);
       const float ca[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
@@ -267,12 +273,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   };
 
-  const bool tr = A.trace != nullptr && blockIdx.x < TRACE_WG && lane == 0;
-  auto mark = [&](int step, int ph) {
-    if (tr && step < TRACE_STEPS)
-      A.trace[((blockIdx.x * 8 + wid) * TRACE_STEPS + step) * TRACE_PH + ph] = __builtin_amdgcn_s_memtime();
-  };
-  mark(0, 0);
   // ---- prologue: the full halo of chunk 0 (always a 3x3 chunk) + the weights of step 0
   __syncthreads();   // affine + epilogue tables (no DMA in flight yet)
   setup(0);
@@ -295,7 +295,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   //      wco 1 after it, so one wave's GroupNorm/SiLU VALU work overlaps the other's MFMAs.
   const int T1 = A.nchunk1 * 9;
   int wb = 0;   // weight double-buffer of the current step (tiles 2*wb, 2*wb+1)
-  int s = 0;
   int pc = 0;   // affine-table channel of the pending piece
   for (int chunk = 0; chunk < A.nchunk1; ++chunk) {
     const int nx = chunk + 1;
@@ -310,7 +309,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // weights of the next step: the next pair of this chunk, the first pair of the next chunk,
         // or the first 1x1 slot
         const int nslot = slot + (two ? 2 : 1);
-        if (nslot < A.nsteps_slots) {
+        if (nslot < A.nsteps_slots && !HDBG(8)) {
           load_w(nslot, 2 * (wb ^ 1));
           const bool ntwo = nslot < T1 && (nslot - (nslot / 9) * 9) < 8;
           if (ntwo) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
@@ -322,22 +321,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const bool act = issue && (nseg2 ? tid < SEG2 / 4 : (tid < PC1 && h < TOT1));
         int off;
         const bf16r* src = piece_src(h, act, nseg2, off);
-        rh[0] = *(const u32x4*)src;
+        if (HDBG(1)) {
+          rh[0] = u32x4{0u, 0u, 0u, 0u};
+        } else {
+          rh[0] = *(const u32x4*)src;
+        }
         hoff[0] = off;
       };
-      mark(s + 1, 0);
       asm volatile("" ::"v"(rh[0]));   // the previous step's halo load is consumed here, on every path
       if (pend) store(nx & 1, 0, !nseg2, pc);
       issue_loads();
       compute(chunk & 1, 2 * ps, false, 2 * wb);
       pc = cch;
-      mark(s + 1, 1);
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
-      mark(s + 1, 2);
       step_barrier<1>();
-      mark(s + 1, 3);
       wb ^= 1;
-      ++s;
     }
   }
   asm volatile("" ::"v"(rh[0]));
@@ -359,10 +357,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
     step_barrier<0>();
     wb ^= 1;
-    ++s;
   }
 
-  mark(0, 1);
+  if (HDBG(4)) return;
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
   const int Ho = d.Ho, Wo = d.Wo;
@@ -391,24 +388,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     bf16r* tileb = lds;   // 64 KiB inside the (now idle) halo + weight buffers
     const bool side = d.resid != nullptr || hasx;
     if (side) {
+      // the whole 64 KiB side tile in flight at once (the main loop's fragments are dead here)
+      u32x4 sv[8];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        u32x4 sv[4];
+      for (int k = 0; k < 8; ++k) {
+        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
+        const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+        const int c = co0 + c16 * 8;
+        const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
+                           : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
+                                           : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
+        sv[k] = *(const u32x4*)src;
+      }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = tid + NT * (4 * half + k), pi = q >> 4, c16 = q & 15;
-          const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-          const int c = co0 + c16 * 8;
-          const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
-                             : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
-                                             : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-          sv[k] = *(const u32x4*)src;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = tid + NT * (4 * half + k), pi = q >> 4, c16 = q & 15;
-          *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
-        }
+      for (int k = 0; k < 8; ++k) {
+        const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
+        *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
       }
       __syncthreads();
     }
@@ -543,7 +538,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (stats) flush_stats(i, st1, st2);
     }
   }
-  mark(0, 2);
 }
 
 // [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
@@ -588,7 +582,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.nsteps_slots = A.nchunk1 * 9 + A.nchunk2;
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
-  A.trace = g_trace;
+  A.dbg = g_dbg;
   const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;   // too few tiles to fill the chip: the split-K implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
@@ -606,10 +600,9 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   return (int)hipGetLastError();
 }
 
-// Debug hook (not part of the public ABI): record per-phase s_memtime stamps of the next launches
-// into buf [TRACE_WG][8 waves][TRACE_STEPS][TRACE_PH] (u64); null disables.  tools/halo_trace.py.
-extern "C" int fmd_debug_halo_trace(void* buf) {
-  g_trace = (unsigned long long*)buf;
+// Debug hook (not part of the public ABI): ablation flags of the next launches (see HArgs::dbg).
+extern "C" int fmd_debug_halo_flags(int flags) {
+  g_dbg = flags;
   return 0;
 }
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--hw", type=int, default=256)
     ap.add_argument("--c", type=int, default=128)
+    ap.add_argument("--dbg", default="", help="comma list of halo ablation flag values to time as well")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N, H, W, C, K = 8, a.hw, a.hw, a.c, a.c
@@ -63,9 +64,16 @@ def main():
 
     probs = dict(fwd=(fwd, 2 * N * H * W * K * C * 9), cat=(cat, 2 * N * H * W * K * 2 * C * 9),
                  dgrad=(dgrad, 2 * N * H * W * K * C * 9), wgrad=(wgrad, 2 * N * H * W * K * C * 9))
-    for name, (fn, flops) in probs.items():
+    import ctypes
+    from fmdiff import _lib
+    L = _lib.lib()
+    flagsets = [0] + [int(f) for f in a.dbg.split(",") if f]
+    todo = [(name, fl) for name in probs for fl in flagsets]
+    for name, fl in todo:
+        fn, flops = probs[name]
         if a.only and name not in a.only.split(","):
             continue
+        L.fmd_debug_halo_flags(ctypes.c_int(fl))
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -76,7 +84,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
-        print(f"{name:6s} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        print(f"{name:6s} dbg={fl:2d} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+    L.fmd_debug_halo_flags(ctypes.c_int(0))
 
 
 if __name__ == "__main__":
