@@ -19,7 +19,8 @@ LIB = os.path.join(LIB_DIR, "libfmdiff_hip.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("FMD_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
+         *os.environ.get("FMD_EXTRA_FLAGS", "").split()]
 
 
 def _deps_mtime():

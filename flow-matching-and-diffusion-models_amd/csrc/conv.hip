@@ -560,18 +560,18 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->pro_a && !d->pro_b) return -4;
   if (d->splits > 1 && (!d->ws || d->stats)) return -5;
   (void)C;
-  int rc;
-  if (d->splits <= 1 && d->K > 16 && !d->force_generic) {
-    rc = fmd_conv_halo(d, stream);   // 3x3 stride-1 problems with >= 128 16x16 tiles
-    if (rc != 1) return rc;
+  int rc = 1;
+  if (d->K > 16 && !d->force_generic)
+    rc = fmd_conv_halo(d, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
+  if (rc == 1) {
+    if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
+    if (d->K <= 16)
+      rc = launch<16, 256, 1, 4, 64>(d, s);
+    else if (d->K <= 64)
+      rc = launch<64, 128, 2, 2, 64>(d, s);
+    else
+      rc = launch<128, 128, 2, 2, 64>(d, s);
   }
-  if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
-  if (d->K <= 16)
-    rc = launch<16, 256, 1, 4, 64>(d, s);
-  else if (d->K <= 64)
-    rc = launch<64, 128, 2, 2, 64>(d, s);
-  else
-    rc = launch<128, 128, 2, 2, 64>(d, s);
   if (rc) return rc;
   if (d->splits > 1) {
     const int M = d->N * d->Ho * d->Wo;

@@ -46,6 +46,8 @@ struct HArgs {
   int C, C23;
   int tiles_x, tiles_y, ntc;
   int nchunk1, nchunk2;   // main / 1x1-segment chunks
+  int splits, cps;        // split-K over main chunks: split y owns chunks [y*cps, min(nchunk1, (y+1)*cps));
+                          // the 1x1 segment belongs to the last split; fp32 partials go to d.ws
   int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
   const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
@@ -136,7 +138,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
   const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
   const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
-  const int nchunks = A.nchunk1 + A.nchunk2;
 
   // the GN affine of image n for every input channel, and the epilogue's per-cout vectors
   if (PRO != 0) {
@@ -273,15 +274,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   };
 
-  // ---- prologue: the full halo of chunk 0 (always a 3x3 chunk) + the weights of step 0
+  // ---- this workgroup's reduction range (split-K over 3x3 chunks; the 1x1 segment goes to the last split)
+  const int split = blockIdx.y;
+  const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
+  const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
+  const int T1 = A.nchunk1 * 9;
+  const int slot_end = n_seg2 ? T1 + n_seg2 : c_hi * 9;   // one past the last weight slot of this split
+  auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
+
+  // ---- prologue: the full halo of the first chunk (always a 3x3 chunk) + the weights of its first step
   __syncthreads();   // affine + epilogue tables (no DMA in flight yet)
-  setup(0);
-  load_w(0, 0);
-  if (A.nchunk1 * 9 > 1) load_w(1, 1);
+  setup(c_lo);
+  load_w(c_lo * 9, 0);
+  if (c_lo * 9 + 1 < slot_end) load_w(c_lo * 9 + 1, 1);
 #pragma unroll
   for (int k = 0; k < LPRO; ++k) load_main(k, tid + NT * k, tid + NT * k < TOT1);
 #pragma unroll
-  for (int k = 0; k < LPRO; ++k) store(0, k, true, cch);
+  for (int k = 0; k < LPRO; ++k) store(c_lo & 1, k, true, cch);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -293,12 +302,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   //      DMA's counted wait leaves it in flight across the barrier) and transformed + stored in step
   //      i+1.  Waves of the two cout halves share a SIMD pairwise: wco 0 stores before its first tap,
   //      wco 1 after it, so one wave's GroupNorm/SiLU VALU work overlaps the other's MFMAs.
-  const int T1 = A.nchunk1 * 9;
   int wb = 0;   // weight double-buffer of the current step (tiles 2*wb, 2*wb+1)
   int pc = 0;   // affine-table channel of the pending piece
-  for (int chunk = 0; chunk < A.nchunk1; ++chunk) {
-    const int nx = chunk + 1;
-    const bool more = nx < nchunks, nseg2 = nx >= A.nchunk1;
+  for (int chunk = c_lo; chunk < c_hi; ++chunk) {
+    const int nx = next_chunk(chunk);
+    const bool more = nx >= 0, nseg2 = nx >= A.nchunk1;
 #pragma unroll 1
     for (int ps = 0; ps < 5; ++ps) {
       const int slot = chunk * 9 + 2 * ps;
@@ -308,8 +316,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       auto issue_loads = [&]() {
         // weights of the next step: the next pair of this chunk, the first pair of the next chunk,
         // or the first 1x1 slot
-        const int nslot = slot + (two ? 2 : 1);
-        if (nslot < A.nsteps_slots && !HDBG(8)) {
+        const int nslot = two ? slot + 2 : (nx < 0 ? slot_end : nx < A.nchunk1 ? nx * 9 : T1 + (nx - A.nchunk1));
+        if (nslot < slot_end && !HDBG(8)) {
           load_w(nslot, 2 * (wb ^ 1));
           const bool ntwo = nslot < T1 && (nslot - (nslot / 9) * 9) < 8;
           if (ntwo) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
@@ -340,11 +348,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   asm volatile("" ::"v"(rh[0]));
   // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, next chunk staged whole
-  for (int chunk = A.nchunk1; chunk < nchunks; ++chunk) {
+  for (int chunk = A.nchunk1; chunk < A.nchunk1 + n_seg2; ++chunk) {
     const int nx = chunk + 1;
-    const bool more = nx < nchunks;
+    const bool more = nx < A.nchunk1 + n_seg2;
     const int slot = T1 + (chunk - A.nchunk1);
-    if (slot + 1 < A.nsteps_slots) load_w(slot + 1, 2 * (wb ^ 1));
+    if (slot + 1 < slot_end) load_w(slot + 1, 2 * (wb ^ 1));
     if (more) {
       setup(nx);
 #pragma unroll
@@ -363,6 +371,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
   const int Ho = d.Ho, Wo = d.Wo;
+  if (A.splits > 1) {   // fp32 partial sums of this split; splitk_reduce applies the epilogue
+    float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wco * 64 + 16 * i + 4 * lq;
+      if (co >= K) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t p = ((size_t)n * Ho + ty0 + wpx * 4 + j) * Wo + tx0 + l16;
+        if (co + 3 < K) {
+          *(f32x4*)(ws + p * K + co) = acc[i][j];
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (co + r < K) ws[p * K + co + r] = acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
   const bool stats = d.stats != nullptr;
   const bool dep = d.ep_a != nullptr;
   const bool hasx = d.ep_x0 != nullptr;
@@ -431,7 +458,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               xv[r] = f[r];
-              if (dep) v[r] *= silu_grad(ea[r] * f[r] + eb[r]);
+              if (dep && !HDBG(16)) v[r] *= silu_grad(ea[r] * f[r] + eb[r]);
             }
           }
         }
@@ -439,7 +466,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         o[0] = pack2(v[0], v[1]);
         o[1] = pack2(v[2], v[3]);
         *(u32x2*)tp8 = o;
-        if (stats) {
+        if (stats && !HDBG(32)) {
           const float w[4] = {bf_lo(o[0]), bf_hi(o[0]), bf_lo(o[1]), bf_hi(o[1])};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -563,7 +590,8 @@ __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, i
 // Called by fmd_conv when the problem qualifies (3x3, stride 1, pad 1, forward gather,
 // output tile 16x16 inside one image, >= 128 tiles).  Returns 1 if not applicable.
 extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed || d->splits > 1) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed) return 1;
+  if (d->splits > 1 && (!d->ws || d->stats)) return 1;
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
@@ -580,13 +608,16 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.nchunk1 = (A.C + BK - 1) / BK;
   A.nchunk2 = d->src2 ? (A.C23 + BK - 1) / BK : 0;
   A.nsteps_slots = A.nchunk1 * 9 + A.nchunk2;
+  A.splits = d->splits > 1 ? d->splits : 1;
+  A.cps = (A.nchunk1 + A.splits - 1) / A.splits;
+  if (A.splits > 1 && (A.splits - 1) * A.cps >= A.nchunk1) return 1;   // every split owns >= 1 chunk
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
   A.dbg = g_dbg;
   const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
-  if (nwg < 128) return 1;   // too few tiles to fill the chip: the split-K implicit GEMM wins
+  if (nwg * A.splits < 128) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
-  const dim3 g(nwg), blk(NT);
+  const dim3 g(nwg, A.splits), blk(NT);
   hipStream_t st = (hipStream_t)stream;
   if (d->upsample) {
     if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2>), g, blk, 0, st, A);

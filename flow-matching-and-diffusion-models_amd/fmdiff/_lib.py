@@ -8,7 +8,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libfmdiff_hip.so")
+LIB_PATH = os.environ.get("FMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                     "libfmdiff_hip.so")
 
 p = C.c_void_p
 i32 = C.c_int32

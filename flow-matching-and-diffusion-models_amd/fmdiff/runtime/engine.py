@@ -269,7 +269,7 @@ class UNetEngine:
         N_, Hs_, Ws_, _ = x.t.shape
         Ho_ = ops.out_hw(Hs_, 3, stride, 1, upsample)
         halo = stride == 1 and ops.halo_eligible(N_, Hs_, Ho_, ops.out_hw(Ws_, 3, stride, 1, upsample),
-                                                 conv.out_channels, upsample=upsample)
+                                                 conv.out_channels, upsample=upsample, Cin=Cin)
         w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
                            bias=conv.bias, want_stats=True, wgt_tiled=wt)
@@ -328,7 +328,7 @@ class UNetEngine:
         """Data gradient of a 3x3 pad-1 conv.  Stride 1 = forward gather with flipped taps (so it runs on
         the halo-tiled kernel); stride 2 = transposed gather."""
         if stride == 1:
-            halo = ops.halo_eligible(dy.shape[0], H, H, W, Cin)
+            halo = ops.halo_eligible(dy.shape[0], H, H, W, Cin, Cin=dy.shape[-1])
             base, tiled = self._wts(w, 3, halo, Kpad, None)
             return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=(H, W), wgt_tiled=tiled, **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,

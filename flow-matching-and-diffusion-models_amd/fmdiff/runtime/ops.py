@@ -121,15 +121,33 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
 
 
 HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
+HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
+
+
+def halo_splits(N, Ho, Wo, K, Cin) -> int:
+    """Split-K factor the halo kernel uses: 1 when the 16x16 tiles x cout tiles already give >= 128
+    workgroups, else enough chunk-range splits (>= 2 chunks each) to reach ~256; 0 = not eligible."""
+    nwg = N * (Ho // 16) * (Wo // 16) * -(-K // 128)
+    if nwg >= 128:
+        return 1
+    nch = -(-max(Cin, 1) // HALO_BK)
+    sp = min(-(-256 // max(nwg, 1)), nch // 2, 16)
+    if sp < 2 or nwg * sp < 128:
+        return 0
+    cps = -(-nch // sp)
+    while sp > 1 and (sp - 1) * cps >= nch:   # every split owns at least one chunk (mirrors the kernel)
+        sp -= 1
+    return sp if nwg * sp >= 128 else 0
 
 
 def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False, Cin=0,
                   pro=False) -> bool:
     """Mirror of fmd_conv_halo's applicability test (csrc/conv_halo.hip): 3x3 s1 p1 forward gather,
-    16x16 output tiles, K > 16, at least 128 workgroups, GN-prologue inputs of at most HALO_CMAX channels."""
+    16x16 output tiles, K > 16, at least 128 workgroups (with split-K over channel chunks when the
+    level is small), GN-prologue inputs of at most HALO_CMAX channels."""
     return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed and not (pro and Cin > HALO_CMAX)
-            and Ho % 16 == 0 and Wo % 16 == 0 and N * (Ho // 16) * (Wo // 16) * -(-K // 128) >= 128
-            and (Ho == 2 * Hs if upsample else Ho == Hs))
+            and Ho % 16 == 0 and Wo % 16 == 0 and (Ho == 2 * Hs if upsample else Ho == Hs)
+            and halo_splits(N, Ho, Wo, K, Cin) > 0)
 
 
 def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, transposed=False, out_hw_=None,
@@ -173,7 +191,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
                                                   pro is not None)
     d.force_generic = int(force_generic)
     if halo:
-        splits = 1
+        splits = halo_splits(N, Ho, Wo, K, C0 + C1)
         bpx = 256
         if wgt_tiled is None:
             wgt_tiled = tile_weights(wgt)

@@ -474,3 +474,42 @@ def test_conv1x1_gn_apply_vs_torch(C0, C1, Kd):
                        R.to(DEV), d0, 1, d1, 0)
     got = torch.cat([d0, d1], -1) if C1 else d0
     _close(got, ref)
+
+
+@pytest.mark.parametrize("case", ["pro_stats", "skip_seg2", "dgrad_ep", "concat_resid"])
+def test_halo_conv_split_k_matches_generic(case):
+    """Small levels (32x32, 4 images): the halo kernel splits its channel chunks over blockIdx.y, writes fp32
+    partial slabs and splitk_reduce applies the epilogue (bias, per-sample bias, skip, residual, SiLU'),
+    with channel statistics from a separate pass; vs the per-tap implicit GEMM."""
+    O = ops()
+    N, H, W = 4, 32, 32
+    C0, C1, K = 512, 0, 256
+    if case == "concat_resid":
+        C0, C1 = 256, 256
+    x0 = _rand_nhwc(N, H, W, C0, 31).to(DEV)
+    x1 = _rand_nhwc(N, H, W, C1, 32).to(DEV) if C1 else None
+    w = O.prep_weights(_w(K, C0 + C1, 3, 33).to(DEV), 0)
+    kw = dict(bias=(torch.randn(K) * 0.1).to(DEV))
+    if case in ("pro_stats", "concat_resid"):
+        kw["pro"] = ((torch.rand(N, C0 + C1) + 0.5).to(DEV), (torch.randn(N, C0 + C1) * 0.2).to(DEV), True)
+        kw["bias_nc"] = (torch.randn(N, K) * 0.1).to(DEV)
+    if case == "skip_seg2":
+        s2 = _rand_nhwc(N, H, W, 256, 34).to(DEV)
+        s3 = _rand_nhwc(N, H, W, 256, 35).to(DEV)
+        kw.update(src2=s2, src3=s3, wgt2=O.prep_weights(_w(K, 512, 1, 36).to(DEV), 0),
+                  bias2=(torch.randn(K) * 0.1).to(DEV))
+    if case == "concat_resid":
+        kw["resid"] = _rand_nhwc(N, H, W, K, 37).to(DEV)
+    if case == "dgrad_ep":
+        xe = _rand_nhwc(N, H, W, K, 38).to(DEV)
+        kw["ep"] = (xe, None, (torch.rand(N, K) + 0.5).to(DEV), (torch.randn(N, K) * 0.2).to(DEV))
+    sp = O.halo_splits(N, H, W, K, C0 + C1)
+    assert sp > 1 and O.halo_eligible(N, H, H, W, K, Cin=C0 + C1, pro="pro" in kw)
+    want = case != "skip_seg2"
+    a, sa = O.conv(x0, K, w, src1=x1, want_stats=want, **kw)
+    b, sb = O.conv(x0, K, w, src1=x1, want_stats=want, force_generic=True, **kw)
+    torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item())
+    if want:
+        ta = sa.slab.view(N, -1, K, 2).sum(1)
+        tb = sb.slab.view(N, -1, K, 2).sum(1)
+        torch.testing.assert_close(ta, tb, rtol=2e-3, atol=2e-2)
