@@ -336,10 +336,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         hoff[0] = off;
       };
-      asm volatile("" ::"v"(rh[0]));   // the previous step's halo load is consumed here, on every path
-      if (pend) store(nx & 1, 0, !nseg2, pc);
-      issue_loads();
-      compute(chunk & 1, 2 * ps, false, 2 * wb);
+      // Waves w and w+4 share a SIMD: the wco 0 wave stages (GN/SiLU VALU work) before its first tap,
+      // the wco 1 wave after it, so one wave's transform overlaps the other's MFMAs.
+      if (wco == 0) {
+        asm volatile("" ::"v"(rh[0]));   // the previous step's halo load is consumed here, on every path
+        if (pend) store(nx & 1, 0, !nseg2, pc);
+        issue_loads();
+        compute(chunk & 1, 2 * ps, false, 2 * wb);
+      } else {
+        compute(chunk & 1, 2 * ps, false, 2 * wb);
+        asm volatile("" ::"v"(rh[0]));
+        if (pend) store(nx & 1, 0, !nseg2, pc);
+        issue_loads();
+      }
       pc = cch;
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
       step_barrier<1>();

@@ -262,6 +262,37 @@ __global__ void gn_bwd_apply_kernel(const bf16r* __restrict__ dz, const bf16r* _
   }
 }
 
+// t = SiLU(a*x + b) (or the affine alone) over a two-source concat: the GroupNorm(+scale/shift)+SiLU
+// prologue materialised once, so every consumer (conv forward, weight gradient) reads it untransformed
+__global__ void gn_apply_fwd_kernel(const bf16r* __restrict__ x0, const bf16r* __restrict__ x1, int C0, int C1,
+                                    long long M, int HW, const float* __restrict__ a, const float* __restrict__ b,
+                                    int silu, bf16r* __restrict__ t) {
+  const int C = C0 + C1;
+  const int CH = C / 8;
+  const long long total = M * CH;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long p = i / CH;
+    const int c = (int)(i - p * CH) * 8;
+    const int n = (int)(p / HW);
+    const u32x4 v = c < C0 ? *(const u32x4*)(x0 + p * C0 + c) : *(const u32x4*)(x1 + p * C1 + (c - C0));
+    const float* pa = a + (size_t)n * C + c;
+    const float* pb = b + (size_t)n * C + c;
+    const f32x4 a0 = *(const f32x4*)pa, a1 = *(const f32x4*)(pa + 4);
+    const f32x4 b0 = *(const f32x4*)pb, b1 = *(const f32x4*)(pb + 4);
+    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float lo = bf_lo(v[e]) * av[2 * e] + bv[2 * e];
+      float hi = bf_hi(v[e]) * av[2 * e + 1] + bv[2 * e + 1];
+      if (silu) { lo = siluf_(lo); hi = siluf_(hi); }
+      o[e] = pack2(lo, hi);
+    }
+    *(u32x4*)(t + p * C + c) = o;
+  }
+}
+
 inline int grid_for(long long work, int per_block = 256, int cap = 8192) {
   long long b = (work + per_block - 1) / per_block;
   if (b > cap) b = cap;
@@ -319,5 +350,14 @@ extern "C" int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, 
   hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)s, (const bf16r*)dz,
                      (const bf16r*)x0, (const bf16r*)x1, C0, C1, (long long)M, HW, P, Q, R, (const bf16r*)extra,
                      (bf16r*)dx0, acc0, (bf16r*)dx1, acc1);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,
+                                const float* a, const float* b, int32_t silu, void* t, fmd_stream_t s) {
+  if ((C0 % 8) || (C1 % 8) || (C1 && !x1)) return -1;
+  const long long work = M * (long long)((C0 + C1) / 8);
+  hipLaunchKernelGGL(gn_apply_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)s, (const bf16r*)x0,
+                     (const bf16r*)x1, C0, C1, (long long)M, HW, a, b, silu, (bf16r*)t);
   return (int)hipGetLastError();
 }

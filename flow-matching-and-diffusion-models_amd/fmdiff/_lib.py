@@ -61,6 +61,7 @@ SIGNATURES = {
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
+    "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_batch": [p, i32, i32, p],

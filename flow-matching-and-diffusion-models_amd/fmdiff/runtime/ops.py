@@ -82,6 +82,15 @@ def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, be
     return P, Q, R
 
 
+def gn_apply_fwd(x0, x1, a, b, silu=True):
+    """t = SiLU(a*x + b) over the channel concat of x0|x1 (NHWC bf16): the materialised GN prologue."""
+    N, H, W, C0 = x0.shape
+    C1 = x1.shape[-1] if x1 is not None else 0
+    t = torch.empty((N, H, W, C0 + C1), device=x0.device, dtype=BF16)
+    _lib.call("fmd_gn_apply_fwd", _p(x0), _p(x1), C0, C1, N * H * W, H * W, _p(a), _p(b), int(silu), _p(t), stream())
+    return t
+
+
 def gn_bwd_apply(dz, x0, x1, P, Q, R, extra, dx0, acc0, dx1=None, acc1=0):
     N, H, W, Ct = dz.shape
     C0 = x0.shape[-1]

@@ -162,6 +162,10 @@ int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_t HW, int32
                     int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R,
                     float* dgamma, float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st,
                     int32_t fwd_rows, float* ws /* [N][C][2] scratch */, fmd_stream_t s);
+/* t = SiLU(a*x + b) (silu != 0) or a*x + b over the concat x0|x1 (bf16 [M][C0+C1]): the GroupNorm
+ * prologue materialised once for its consumers. */
+int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,
+                     const float* a, const float* b, int32_t silu, void* t, fmd_stream_t s);
 int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,
                      int32_t HW, const float* P, const float* Q, const float* R, const void* extra,
                      void* dx0, int32_t acc0, void* dx1, int32_t acc1, fmd_stream_t s);

@@ -62,7 +62,21 @@ def main():
     def wgrad():
         ops.wgrad(x, x2, dw, pro=(pac, pbc, True), db=db)
 
+    def fwd0():
+        ops.conv(x, K, w, bias=bias, out=out, want_stats=True, wgt_tiled=wt)
+
+    def wgrad0():
+        ops.wgrad(x, x2, dw, db=db)
+
+    def gnapply():
+        ops.gn_apply_fwd(x, None, pac, pbc)
+
+    def gnapply_cat():
+        ops.gn_apply_fwd(x, x2, pa, pb)
+
     probs = dict(fwd=(fwd, 2 * N * H * W * K * C * 9), cat=(cat, 2 * N * H * W * K * 2 * C * 9),
+                 fwd0=(fwd0, 2 * N * H * W * K * C * 9), wgrad0=(wgrad0, 2 * N * H * W * K * C * 9),
+                 gnapply=(gnapply, 4 * N * H * W * C), gnapply_cat=(gnapply_cat, 8 * N * H * W * C),
                  dgrad=(dgrad, 2 * N * H * W * K * C * 9), wgrad=(wgrad, 2 * N * H * W * K * C * 9))
     import ctypes
     from fmdiff import _lib
