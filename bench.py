@@ -79,6 +79,18 @@ def conv_roofline(dev, iters=20):
                 ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC summary
+    (profiles/r*_halo_fwd_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes over the same
+    problem, tools/gpu_pmc.sh); None when no summary is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_halo_fwd_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return float(json.load(f)["traffic_bytes_per_launch"])
+
+
 def cpu_baseline(iters=2):
     """The oracle (fp32 PyTorch-CPU restatement of the reference, proven bit-exact in
     tests/test_oracle_golden.py) timed on this host: one FM train step (fwd+bwd+AdamW) at
@@ -241,7 +253,7 @@ def main():
         "train_mfma_frac": step_tflops / PEAK_BF16_TFLOPS,
         **samp,
         "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": None, "kernel": roof["kernel"],
+                     "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(), "kernel": roof["kernel"],
                      "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]},
         "cpu_baseline": cpu,
     }
