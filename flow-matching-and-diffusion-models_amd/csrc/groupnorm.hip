@@ -82,31 +82,61 @@ __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const f
   const int E0 = HW / rows0;
   const int E1 = C1 ? HW / rows1 : 0;
   double s1 = 0.0, s2 = 0.0;
-  for (int idx = threadIdx.x;; idx += blockDim.x) {
-    // enumerate (channel in group, entry)
-    const int maxE = E0 > E1 ? E0 : E1;
-    if (idx >= Cg * maxE) break;
-    const int cl = idx / maxE, e = idx - cl * maxE;
-    const int c = c_begin + cl;
-    if (c < C0) {
-      if (e < E0) {
-        const float* p = st0 + (((size_t)n * E0 + e) * C0 + c) * 2;
-        s1 += p[0]; s2 += p[1];
+  const bool in0 = c_begin + Cg <= C0, in1 = c_begin >= C0;
+  if ((in0 || in1) && (Cg & 1) == 0) {
+    // the group lies in one source: per slab entry its Cg channels are 2*Cg contiguous floats, read as
+    // 16-byte vectors; fp32 partials per thread (a few entries), double across threads
+    const float* base = in0 ? st0 + (size_t)n * E0 * C0 * 2 + (size_t)c_begin * 2
+                            : st1 + (size_t)n * E1 * C1 * 2 + (size_t)(c_begin - C0) * 2;
+    const int E = in0 ? E0 : E1;
+    const int stride = (in0 ? C0 : C1) * 2;
+    float f1 = 0.f, f2 = 0.f;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+      const float* p = base + (size_t)e * stride;
+      for (int q = 0; q < Cg / 2; ++q) {
+        const f32x4 v = *(const f32x4*)(p + 4 * q);
+        f1 += v[0] + v[2];
+        f2 += v[1] + v[3];
       }
-    } else {
-      if (e < E1) {
-        const float* p = st1 + (((size_t)n * E1 + e) * C1 + (c - C0)) * 2;
-        s1 += p[0]; s2 += p[1];
+    }
+    s1 = f1;
+    s2 = f2;
+  } else {
+    for (int idx = threadIdx.x;; idx += blockDim.x) {
+      // enumerate (channel in group, entry)
+      const int maxE = E0 > E1 ? E0 : E1;
+      if (idx >= Cg * maxE) break;
+      const int cl = idx / maxE, e = idx - cl * maxE;
+      const int c = c_begin + cl;
+      if (c < C0) {
+        if (e < E0) {
+          const float* p = st0 + (((size_t)n * E0 + e) * C0 + c) * 2;
+          s1 += p[0]; s2 += p[1];
+        }
+      } else {
+        if (e < E1) {
+          const float* p = st1 + (((size_t)n * E1 + e) * C1 + (c - C0)) * 2;
+          s1 += p[0]; s2 += p[1];
+        }
       }
     }
   }
-  __shared__ double r1[256], r2[256];
-  r1[threadIdx.x] = s1; r2[threadIdx.x] = s2;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) { r1[threadIdx.x] += r1[threadIdx.x + o]; r2[threadIdx.x] += r2[threadIdx.x + o]; }
-    __syncthreads();
+  // wave reduction (double), then the waves through LDS
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
   }
+  __shared__ double r1[16], r2[16];
+  if ((threadIdx.x & 63) == 0) { r1[threadIdx.x >> 6] = s1; r2[threadIdx.x >> 6] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { t1 += r1[w]; t2 += r2[w]; }
+    r1[0] = t1;
+    r2[0] = t2;
+  }
+  __syncthreads();
   const double cnt = (double)Cg * HW;
   const double mean = r1[0] / cnt;
   double var = r2[0] / cnt - mean * mean;

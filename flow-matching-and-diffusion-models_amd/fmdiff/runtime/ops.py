@@ -46,9 +46,8 @@ def channel_stats(x: torch.Tensor, rows: Optional[int] = None, y: Tuple = None) 
     N, H, W, Cc = x.shape
     HW = H * W
     if rows is None:
-        rows = HW
-        while rows > 1024 and rows % 2 == 0:
-            rows //= 2
+        # 64-pixel slab rows (like the conv epilogues): enough blocks to cover the chip even at 32x32
+        rows = 64 if HW % 64 == 0 else HW
     slab = torch.empty((N * HW // rows, Cc, 2), device=x.device, dtype=F32)
     y0, y1, C0 = (None, None, Cc) if y is None else y
     _lib.call("fmd_channel_stats", _p(x), _p(y0), _p(y1), C0, N, HW, Cc, rows, _p(slab), stream())
