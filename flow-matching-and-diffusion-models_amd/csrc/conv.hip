@@ -593,6 +593,7 @@ extern "C" int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc
   if (d->splits > 1 || d->stats || d->bias || d->bias2 || d->bias_nc || d->resid || d->ep_x0 || d->src2) return -5;
   if (!g || !g->dz || !g->x0 || !g->P || !g->Q || !g->R || !g->dx0 || (g->C0 % 8)) return -7;
   if (g->C0 < d->K && (!g->x1 || !g->dx1)) return -7;
-  if (d->K <= 64) return launch<64, 128, 2, 2, 64, true>(d, s, g);
-  return launch<128, 128, 2, 2, 64, true>(d, s, g);
+  // BK = 32: a 32 KiB LDS footprint keeps 4-5 of these memory-bound workgroups per CU in flight
+  if (d->K <= 64) return launch<64, 128, 2, 2, 32, true>(d, s, g);
+  return launch<128, 128, 2, 2, 32, true>(d, s, g);
 }

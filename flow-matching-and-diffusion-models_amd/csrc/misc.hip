@@ -565,10 +565,21 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
   const int k0 = (b % kt) * PT, c0 = (b / kt) * PT;
   const int T = ks * ks;
   // ---- master tile w[k0:k0+32][c0:c0+32][:] (zero outside K x C)
-  for (int e = threadIdx.x; e < PT * PT * T; e += blockDim.x) {
-    const int kl = e / (PT * T), r = e - kl * (PT * T);   // r = cl * T + tap: contiguous in memory
-    const int k = k0 + kl, c = c0 + r / T;
-    tile[kl * PTS + r] = (k < K && c < C) ? w[((size_t)k * C + c0) * T + r] : 0.f;
+  if (((C * T) & 3) == 0 && c0 + PT <= C && ((size_t)w & 15) == 0) {
+    // full-width tile: 16-byte loads along the contiguous (c, tap) run of each k
+    const int nv = PT * T / 4;
+    for (int e = threadIdx.x; e < PT * nv; e += blockDim.x) {
+      const int kl = e / nv, v = e - kl * nv, k = k0 + kl;
+      const float4 x = k < K ? *(const float4*)(w + ((size_t)k * C + c0) * T + v * 4) : float4{0.f, 0.f, 0.f, 0.f};
+      float* t = tile + kl * PTS + v * 4;
+      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < PT * PT * T; e += blockDim.x) {
+      const int kl = e / (PT * T), r = e - kl * (PT * T);   // r = cl * T + tap: contiguous in memory
+      const int k = k0 + kl, c = c0 + r / T;
+      tile[kl * PTS + r] = (k < K && c < C) ? w[((size_t)k * C + c0) * T + r] : 0.f;
+    }
   }
   __syncthreads();
   for (int o = 0; o < nout; ++o) {
@@ -580,13 +591,34 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
     // tile coordinates in the layout's (row, col) space
     const int r0 = mode == 0 ? k0 : c0, q0 = mode == 0 ? c0 : k0;
     if (kind == 0) {
-      // [R][To][Cc]: for each (row, tap) a run of 32 cols
-      for (int e = threadIdx.x; e < PT * To * PT; e += blockDim.x) {
-        const int ql = e % PT, r = e / PT, tap = r % To, rl = r / To;
-        const int row = r0 + rl, col = q0 + ql;
-        if (row >= R || col >= Cc) continue;
-        const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
-        out[((size_t)row * To + tap) * Cc + col] = (bf16r)f2bf(ptile_value(tile, kl, cl, ks, mode, tap));
+      // [R][To][Cc]: for each (row, tap) a run of 32 cols, written as 16-byte groups of 8
+      const bool vec = (Cc & 7) == 0 && ((size_t)out & 15) == 0;
+      for (int e = threadIdx.x; e < PT * To * (PT / 8); e += blockDim.x) {
+        const int q8 = e % (PT / 8), r = e / (PT / 8), tap = r % To, rl = r / To;
+        const int row = r0 + rl, col8 = q0 + q8 * 8;
+        if (row >= R || col8 >= Cc) continue;
+        bf16r* dst = out + ((size_t)row * To + tap) * Cc + col8;
+        if (vec) {
+          unsigned int pk[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            float v2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int ql = q8 * 8 + 2 * h + u;
+              const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
+              v2[u] = ptile_value(tile, kl, cl, ks, mode, tap);
+            }
+            pk[h] = pack2(v2[0], v2[1]);
+          }
+          *(u32x4*)dst = u32x4{pk[0], pk[1], pk[2], pk[3]};
+        } else {
+          for (int u = 0; u < 8 && col8 + u < Cc; ++u) {
+            const int ql = q8 * 8 + u;
+            const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
+            dst[u] = (bf16r)f2bf(ptile_value(tile, kl, cl, ks, mode, tap));
+          }
+        }
       }
     } else {
       // [R/128][Cc/BK][To][BK/8][128][8]: 16-byte chunks of 8 cols, runs of 32 rows

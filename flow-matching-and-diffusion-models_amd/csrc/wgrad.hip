@@ -22,6 +22,7 @@ constexpr int BCO = 128, BCI = 128, BKP = 32;
 struct WArgs {
   fmd_wgrad_desc d;
   int M, T, C, ntc, nci, per_split, nsteps, ldy;
+  int merged;   // C*T <= BCI: the (tap, cin) pairs share one column tile (a narrow stem conv)
 };
 
 // 8-byte unit swizzle for the [32][128] bf16 tile (256-B rows): conflict-free
@@ -42,7 +43,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   const int tci = bx % A.nci; bx /= A.nci;
   const int tap = bx;
   const int co0 = tco * BCO, ci0 = tci * BCI;
-  const int ky = tap / d.ks, kx = tap - ky * d.ks;
+  // this thread's gather column chunk -> (tap, channel); merged mode spreads the taps over the chunks
+  const int cpt = A.C >> 3;                        // 8-channel chunks per tap
+  const int my_tap = A.merged ? (tid & 15) / cpt : tap;
+  const int my_c = A.merged ? ((tid & 15) - my_tap * cpt) * 8 : ci0 + (tid & 15) * 8;
+  const bool col_ok = A.merged ? my_tap < A.T : my_c < A.C;
+  const int ky = my_tap / d.ks, kx = my_tap - (my_tap / d.ks) * d.ks;
   const int split = blockIdx.y;
   const int s0 = split * A.per_split;
   const int s1 = min(A.nsteps, s0 + A.per_split);
@@ -72,8 +78,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
       if (p < A.M && co < d.K) v = *(const u32x4*)(dy + (size_t)p * A.ldy + co);
       ry[j] = v;
       // gather
-      const int c = ci0 + chunk * 8;
-      bool ok = p < A.M && c < A.C;
+      const int c = my_c;
+      bool ok = p < A.M && col_ok;
       int n = 0;
       const bf16r* ptr = nullptr;
       if (ok) {
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
         }
     }
     if (!pro) return;
-    const int c = ci0 + chunk * 8;
+    const int c = my_c;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (!vg[j]) continue;
@@ -196,12 +202,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int ci = ci0 + wn * 64 + 16 * j + l16;
-      if (ci >= A.C) continue;
+      const int col = wn * 64 + 16 * j + l16;
+      const int ci = A.merged ? col % A.C : ci0 + col;
+      const int ct = A.merged ? col / A.C : tap;
+      if (A.merged ? ct >= A.T : ci >= A.C) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 64 + 16 * i + 4 * lq + r;
-        if (co < d.K) ws[((size_t)co * A.T + tap) * A.C + ci] = acc[i][j][r];
+        if (co < d.K) ws[((size_t)co * A.T + ct) * A.C + ci] = acc[i][j][r];
       }
     }
   }
@@ -303,6 +311,7 @@ WArgs make_args(const fmd_wgrad_desc* d) {
   A.ldy = d->ldy > 0 ? d->ldy : d->K;
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nsteps + splits - 1) / splits;
+  A.merged = A.T > 1 && A.C * A.T <= BCI;
   return A;
 }
 
@@ -323,7 +332,7 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int splits = d->splits > 1 ? d->splits : 1;
   int rc = d->force_generic ? 1 : fmd_wgrad_halo(d, stream);
   if (rc == 1) {
-    dim3 grid(A.ntc * A.nci * A.T, splits);
+    dim3 grid(A.ntc * (A.merged ? 1 : A.nci * A.T), splits);
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, s, A);
     rc = (int)hipGetLastError();
   }

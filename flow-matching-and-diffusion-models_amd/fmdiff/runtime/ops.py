@@ -296,7 +296,8 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             base = (K // 128) * (Ct // 64)
             splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36)))
         else:
-            tiles = -(-K // 128) * -(-Ct // 128) * ks * ks
+            # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
+            tiles = -(-K // 128) * (1 if ks > 1 and Ct * ks * ks <= 128 else -(-Ct // 128) * ks * ks)
             steps = -(-M // 32)
             splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), 256))
     d.splits = splits

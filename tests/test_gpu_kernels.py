@@ -134,13 +134,18 @@ def test_conv_data_gradient(mode):
     _close(got, x.grad.permute(0, 2, 3, 1))
 
 
-@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro", "s1_generic", "pro_generic", "up_generic"])
+@pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "pro", "s1_generic", "pro_generic", "up_generic",
+                                  "stem", "stem_pro", "stem_s2"])
 def test_wgrad(mode):
-    """16x16, C=64, K=128: the 3x3 stride-1 modes run the halo kernel (csrc/wgrad_halo.hip) unless *_generic."""
+    """16x16, C=64, K=128: the 3x3 stride-1 modes run the halo kernel (csrc/wgrad_halo.hip) unless *_generic.
+    stem*: C=8 (the padded 2-channel conv_in): the generic kernel's merged (tap, cin) column tile."""
     O = ops()
     generic = mode.endswith("_generic")
     mode = mode.replace("_generic", "")
     N, H, W, C, K = 2, 16, 16, 64, 128
+    if mode.startswith("stem"):
+        C, K = 8, 96
+        mode = {"stem": "s1", "stem_pro": "pro", "stem_s2": "s2"}[mode]
     ks, s, up = (1, 1, False) if mode == "1x1" else (3, 2 if mode == "s2" else 1, mode == "up")
     pad = ks // 2
     xb = _rand_nhwc(N, H, W, C, 13)
