@@ -519,6 +519,99 @@ __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
   }
 }
 
+// Split-K combine over 16-pixel rows x 64-channel blocks, one pixel x 4 channels per lane (16-byte slab
+// loads), with the same epilogue as splitk_reduce and, when d.stats is set, the channel statistics of the
+// rounded output (sum v, sum v^2 -- or sum v*x with the data-gradient epilogue) written as slab row p/16
+// (FMD_SPLIT_STATS_ROWS), so no separate statistics pass is needed.  Split-K only runs on the small
+// levels: 16-pixel rows give enough blocks there.  Needs K % 4 == 0 and M % 16 == 0.
+__global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d, int M) {
+  const int K = d.K;
+  const int HWo = d.Ho * d.Wo;
+  const size_t total = (size_t)M * K;
+  constexpr int RP = FMD_SPLIT_STATS_ROWS;
+  const int row = blockIdx.x;
+  const int tq = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  static_assert(RP == 16, "one pixel per 16-lane group");
+  const int c = blockIdx.y * 64 + tq * 4;
+  const bool cok = c < K;
+  const bool hasx = d.ep_x0 != nullptr;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (cok) {
+    {
+      const int p = row * RP + pl;
+      const int n = p / HWo;
+      const size_t idx = (size_t)p * K + c;
+      f32x4 v = *(const f32x4*)(d.ws + idx);
+#pragma unroll 4
+      for (int s = 1; s < d.splits; ++s) v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+      if (d.bias) v += *(const f32x4*)(d.bias + c);
+      if (d.bias2) v += *(const f32x4*)(d.bias2 + c);
+      if (d.bias_nc) {   // may be a row view of a wider table: no 16-byte alignment assumed
+        const float* bn = d.bias_nc + (size_t)n * K + c;
+        v += f32x4{bn[0], bn[1], bn[2], bn[3]};
+      }
+      if (d.resid) {
+        const u32x2 r = *(const u32x2*)((const bf16r*)d.resid + idx);
+        v[0] += bf_lo(r[0]); v[1] += bf_hi(r[0]); v[2] += bf_lo(r[1]); v[3] += bf_hi(r[1]);
+      }
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (hasx) {
+        const int C0e = d.ep_C0;
+        const u32x2 r = c < C0e ? *(const u32x2*)((const bf16r*)d.ep_x0 + (size_t)p * C0e + c)
+                                : *(const u32x2*)((const bf16r*)d.ep_x1 + (size_t)p * (K - C0e) + (c - C0e));
+        xv[0] = bf_lo(r[0]); xv[1] = bf_hi(r[0]); xv[2] = bf_lo(r[1]); xv[3] = bf_hi(r[1]);
+        if (d.ep_a) {
+          const f32x4 ea = *(const f32x4*)(d.ep_a + (size_t)n * K + c), eb = *(const f32x4*)(d.ep_b + (size_t)n * K + c);
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) v[r2] *= silu_grad(ea[r2] * xv[r2] + eb[r2]);
+        }
+      }
+      if (d.out_f32) {
+        f32x4* o = (f32x4*)((float*)d.out + idx);
+        *o = d.accumulate ? *o + v : v;
+      } else {
+        u32x2* o = (u32x2*)((bf16r*)d.out + idx);
+        if (d.accumulate) {
+          const u32x2 old = *o;
+          v[0] += bf_lo(old[0]); v[1] += bf_hi(old[0]); v[2] += bf_lo(old[1]); v[3] += bf_hi(old[1]);
+        }
+        u32x2 w;
+        w[0] = pack2(v[0], v[1]);
+        w[1] = pack2(v[2], v[3]);
+        *o = w;
+        const float wr[4] = {bf_lo(w[0]), bf_hi(w[0]), bf_lo(w[1]), bf_hi(w[1])};
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) {
+          s1[r2] += wr[r2];
+          s2[r2] += hasx ? wr[r2] * xv[r2] : wr[r2] * wr[r2];
+        }
+      }
+    }
+  }
+  if (!d.stats) return;
+  // lanes tq, tq+16, tq+32, tq+48 of a wave hold the same channels (4 pixels); then the 4 waves via LDS
+  __shared__ float red[4][64][2];
+#pragma unroll
+  for (int r2 = 0; r2 < 4; ++r2) {
+    s1[r2] += __shfl_xor(s1[r2], 16, 64);
+    s1[r2] += __shfl_xor(s1[r2], 32, 64);
+    s2[r2] += __shfl_xor(s2[r2], 16, 64);
+    s2[r2] += __shfl_xor(s2[r2], 32, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int r2 = 0; r2 < 4; ++r2) { red[wv][tq * 4 + r2][0] = s1[r2]; red[wv][tq * 4 + r2][1] = s2[r2]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int cl = threadIdx.x >> 1, k = threadIdx.x & 1;
+    const int cc = blockIdx.y * 64 + cl;
+    if (cc < K)
+      d.stats[((size_t)row * K + cc) * 2 + k] = (red[0][cl][k] + red[1][cl][k]) + (red[2][cl][k] + red[3][cl][k]);
+  }
+}
+
 template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
 int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = nullptr) {
   KArgs A;
@@ -558,27 +651,35 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->C1 && !d->src1) return -2;
   if (d->src2 && !d->wgt2 && !d->wgt2_tiled) return -3;
   if (d->pro_a && !d->pro_b) return -4;
-  if (d->splits > 1 && (!d->ws || d->stats)) return -5;
+  const int M = d->N * d->Ho * d->Wo;
+  // split-K: the combine kernel produces the channel statistics (64-pixel rows) instead of the main kernel
+  const bool rows_ok = d->K % 4 == 0 && M % FMD_SPLIT_STATS_ROWS == 0 && (d->Ho * d->Wo) % FMD_SPLIT_STATS_ROWS == 0;
+  if (d->splits > 1 && (!d->ws || (d->stats && (!rows_ok || d->out_f32 || d->accumulate)))) return -5;
   (void)C;
+  fmd_conv_desc dm = *d;
+  if (d->splits > 1) dm.stats = nullptr;
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
-    rc = fmd_conv_halo(d, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
+    rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->K <= 16)
-      rc = launch<16, 256, 1, 4, 64>(d, s);
+      rc = launch<16, 256, 1, 4, 64>(&dm, s);
     else if (d->K <= 64)
-      rc = launch<64, 128, 2, 2, 64>(d, s);
+      rc = launch<64, 128, 2, 2, 64>(&dm, s);
     else
-      rc = launch<128, 128, 2, 2, 64>(d, s);
+      rc = launch<128, 128, 2, 2, 64>(&dm, s);
   }
   if (rc) return rc;
   if (d->splits > 1) {
-    const int M = d->N * d->Ho * d->Wo;
-    const size_t total = (size_t)M * d->K;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, s, *d, M);
+    if (rows_ok) {
+      hipLaunchKernelGGL(splitk_reduce_rows, dim3(M / FMD_SPLIT_STATS_ROWS, (d->K + 63) / 64), dim3(256), 0, s, *d, M);
+    } else {
+      const size_t total = (size_t)M * d->K;
+      int blocks = (int)((total + 255) / 256);
+      if (blocks > 8192) blocks = 8192;
+      hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, s, *d, M);
+    }
     rc = (int)hipGetLastError();
   }
   return rc;

@@ -248,6 +248,22 @@ __global__ void gn_bwd_gb_kernel(const float* __restrict__ gb, int N, int C, flo
   if (dbeta) dbeta[c] += b;
 }
 
+// one block per job: dgamma[c] += sum_n ws[n][c][0], dbeta[c] += sum_n ws[n][c][1] (fixed n order)
+struct GbBatch {
+  fmd_gb_job j[FMD_GB_MAX];
+};
+static_assert(sizeof(GbBatch) <= 4096 - 64, "kernel argument segment");
+
+__global__ void gn_gb_fold_kernel(const GbBatch B) {
+  const fmd_gb_job J = B.j[blockIdx.x];
+  for (int c = threadIdx.x; c < J.C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int n = 0; n < J.N; ++n) { a += J.ws[((size_t)n * J.C + c) * 2]; b += J.ws[((size_t)n * J.C + c) * 2 + 1]; }
+    if (J.dgamma) J.dgamma[c] += a;
+    if (J.dbeta) J.dbeta[c] += b;
+  }
+}
+
 // dx = P*dz + Q*x + R (+ extra), split into two destinations at C0
 __global__ void gn_bwd_apply_kernel(const bf16r* __restrict__ dz, const bf16r* __restrict__ x0,
                                     const bf16r* __restrict__ x1, int C0, int C1, long long M, int HW,
@@ -370,6 +386,18 @@ extern "C" int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_
     rc = (int)hipGetLastError();
   }
   return rc;
+}
+
+extern "C" int fmd_gn_gb_fold(const fmd_gb_job* jobs, int32_t njobs, fmd_stream_t s) {
+  if (njobs < 0 || njobs > FMD_GB_MAX || (njobs && !jobs)) return -1;
+  if (njobs == 0) return 0;
+  GbBatch B = {};
+  for (int i = 0; i < njobs; ++i) {
+    if (!jobs[i].ws || jobs[i].N < 1 || jobs[i].C < 1) return -2;
+    B.j[i] = jobs[i];
+  }
+  hipLaunchKernelGGL(gn_gb_fold_kernel, dim3(njobs), dim3(256), 0, (hipStream_t)s, B);
+  return (int)hipGetLastError();
 }
 
 extern "C" int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,

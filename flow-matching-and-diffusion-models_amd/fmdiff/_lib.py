@@ -48,6 +48,14 @@ class GnApplyDesc(C.Structure):
     ]
 
 
+class GbJob(C.Structure):
+    """Mirror of ``fmd_gb_job``."""
+    _fields_ = [("ws", p), ("dgamma", p), ("dbeta", p), ("N", i32), ("C", i32)]
+
+
+GB_MAX = 64   # FMD_GB_MAX
+
+
 # name -> argtypes (restype is int32 unless listed in _RESTYPE)
 SIGNATURES = {
     "fmd_conv": [C.POINTER(ConvDesc), p],
@@ -62,6 +70,7 @@ SIGNATURES = {
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
+    "fmd_gn_gb_fold": [p, i32, p],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_batch": [p, i32, i32, p],

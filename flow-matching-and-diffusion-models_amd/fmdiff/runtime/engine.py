@@ -26,6 +26,7 @@ accumulated straight into ``param.grad`` (fp32, reference layout).
 from __future__ import annotations
 
 import math
+import os
 import weakref
 from typing import List, Optional
 
@@ -42,6 +43,12 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 CPAD = 8      # NHWC channel padding of the model input / output (16-byte rows)
 HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdiff.h)
+# GN+SiLU prologue materialised by fmd_gn_apply_fwd (one streaming pass) instead of recomputed inside the
+# halo conv and its weight gradient, for single-source inputs of at most MAT_CMAX channels at levels of at
+# least MAT_MIN_HW pixels, where the streaming pass costs less than the in-kernel transform it removes
+MAT_PRO = os.environ.get("FMD_MAT_PRO", "0") == "1"   # measured net-negative at batch 8
+MAT_CMAX = 128
+MAT_MIN_HW = 128 * 128
 
 
 class Act:
@@ -75,6 +82,10 @@ def _gdest(a: Optional[Act]):
         a.grad = torch.empty_like(a.t)
         return a.grad, 0
     return a.grad, 1
+
+
+def _materialise(halo: bool, x1, Cin: int, HW: int) -> bool:
+    return MAT_PRO and halo and x1 is None and Cin <= MAT_CMAX and HW >= MAT_MIN_HW
 
 
 class WeightCache:
@@ -374,7 +385,9 @@ class UNetEngine:
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
         w1, w1t = self._wts(c1.weight, 0, halo1)
-        h, hst = ops.conv(x0.t, Cout, w1, src1=x1.t if x1 else None, pro=(a1, b1, True),
+        t1 = ops.gn_apply_fwd(x0.t, None, a1, b1) if _materialise(halo1, x1, Cin, HW) else None
+        h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=x1.t if x1 else None,
+                          pro=None if t1 is not None else (a1, b1, True),
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=True,
                           wgt_tiled=w1t)
         if ss:
@@ -395,7 +408,9 @@ class UNetEngine:
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
         w2, w2t = self._wts(c2.weight, 0, halo2)
-        out, ost = ops.conv(h, Cout, w2, pro=(a2, b2, True), bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
+        t2 = ops.gn_apply_fwd(h, None, a2, b2) if _materialise(halo2, None, Cout, HW) else None
+        out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
+                            bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
         o = Act(out, ost)
         if ctx.tape is None:
             return o
@@ -404,7 +419,10 @@ class UNetEngine:
             dy = o.grad
 
             def wg2():
-                ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
+                if t2 is not None:
+                    ops.wgrad(t2, dy, c2.weight.grad, db=c2.bias.grad)
+                else:
+                    ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
                 if not isinstance(sk, Identity):
                     ops.wgrad(x0.t, dy, sk.conv.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0,
                               db=sk.conv.bias.grad)
@@ -430,8 +448,11 @@ class UNetEngine:
             dh = torch.empty_like(h)
             ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
             del dz2
-            self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
-                                       db=c1.bias.grad))
+            if t1 is not None:
+                self._wg(lambda: ops.wgrad(t1, dh, c1.weight.grad, db=c1.bias.grad))
+            else:
+                self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
+                                           db=c1.bias.grad))
             dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, H, W, ep=(x0.t, x1.t if x1 else None, a1, b1),
                                     want_stats=True)
             P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,
@@ -646,9 +667,13 @@ class UNetEngine:
 
     def backward(self, ctx: Ctx, dpred: torch.Tensor):
         """Run the written-out backward. ``dpred``: bf16 NHWC [N,H,W,Kpad] gradient of the output."""
-        self._head_bwd(dpred)
-        for fn in reversed(ctx.tape):
-            fn()
+        ops.gb_defer()   # GroupNorm gamma/beta folds: one batched launch at the end
+        try:
+            self._head_bwd(dpred)
+            for fn in reversed(ctx.tape):
+                fn()
+        finally:
+            ops.gb_flush()
         self._join()   # every weight gradient has landed before anyone reads .grad
         ctx.tape = None
         self._head_bwd = None

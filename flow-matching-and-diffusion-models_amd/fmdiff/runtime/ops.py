@@ -68,6 +68,29 @@ def gn_prep(st0: Stats, st1: Optional[Stats], N: int, HW: int, C0: int, C1: int,
     return a, b, mr
 
 
+# deferred gamma/beta gradient folds (gb_defer / gb_flush): (ws, N, C, dgamma, dbeta) per GroupNorm backward
+_gb_pending: Optional[list] = None
+
+
+def gb_defer():
+    """Start collecting gn_bwd_prep's gamma/beta folds; gb_flush() applies them in batched launches."""
+    global _gb_pending
+    _gb_pending = []
+
+
+def gb_flush():
+    """Fold every deferred (dgamma, dbeta) contribution (fmd_gn_gb_fold, <= GB_MAX jobs per launch) and stop
+    deferring.  Same sums in the same order as the per-call fold."""
+    global _gb_pending
+    jobs, _gb_pending = _gb_pending or [], None
+    for i in range(0, len(jobs), _lib.GB_MAX):
+        part = jobs[i:i + _lib.GB_MAX]
+        arr = (_lib.GbJob * len(part))()
+        for k, (ws, N, Cc, dg, dbt) in enumerate(part):
+            arr[k].ws, arr[k].dgamma, arr[k].dbeta, arr[k].N, arr[k].C = _p(ws), _p(dg), _p(dbt), N, Cc
+        _lib.call("fmd_gn_gb_fold", arr, len(part), stream())
+
+
 def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, beta, dgamma, dbeta,
                 emb=None, emb_stride=0, emb_mode=0, demb=None, demb_stride=0, fwd: Optional[Stats] = None):
     dev = s12.slab.device
@@ -75,6 +98,9 @@ def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, be
     Q = torch.empty((N, Ct), device=dev, dtype=F32)
     R = torch.empty((N, Ct), device=dev, dtype=F32)
     ws = torch.empty((N, Ct, 2), device=dev, dtype=F32)
+    if _gb_pending is not None and (dgamma is not None or dbeta is not None):
+        _gb_pending.append((ws, N, Ct, dgamma, dbeta))   # ws stays referenced until the fold is issued
+        dgamma = dbeta = None
     _lib.call("fmd_gn_bwd_prep", _p(s12.slab), s12.rows, N, HW, Ct, groups, _p(mr), _p(gamma), _p(beta), _p(emb),
               emb_stride, emb_mode, _p(P), _p(Q), _p(R), _p(dgamma), _p(dbeta), _p(demb), demb_stride,
               _p(fwd.slab) if fwd else None, fwd.rows if fwd else 1, _p(ws), stream())
@@ -130,6 +156,7 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
 
 HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
 HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
+SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
 
 
 def halo_splits(N, Ho, Wo, K, Cin) -> int:
@@ -215,11 +242,14 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     else:
         d.splits = 1
     st = None
-    fused_stats = want_stats and splits == 1 and (Ho * Wo) % 64 == 0 and M % bpx == 0
+    # statistics from the conv epilogue (no split) or from the split-K combine (csrc/conv.hip splitk_reduce_rows)
+    fused_stats = want_stats and (Ho * Wo) % 64 == 0 and (
+        (splits == 1 and M % bpx == 0) or (splits > 1 and K % 4 == 0 and not out_f32 and not accumulate))
     if fused_stats:
-        slab = torch.empty((M // 64, K, 2), device=dev, dtype=F32)
+        rows = 64 if splits == 1 else SPLIT_STATS_ROWS
+        slab = torch.empty((M // rows, K, 2), device=dev, dtype=F32)
         d.stats = _p(slab)
-        st = Stats(slab, 64)
+        st = Stats(slab, rows)
     _lib.call("fmd_conv", C.byref(d), stream())
     if want_stats and not fused_stats:
         if ep is not None:
@@ -299,7 +329,9 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
             tiles = -(-K // 128) * (1 if ks > 1 and Ct * ks * ks <= 128 else -(-Ct // 128) * ks * ks)
             steps = -(-M // 32)
-            splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), 256))
+            # up to 4 workgroups per CU (the kernel is latency-bound at one), partial slabs <= 48 MB
+            cap = max(256, min(1024, (48 << 20) // (K * Ct * ks * ks * 4)))
+            splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), cap))
     d.splits = splits
     ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
     d.ws = _p(ws)

@@ -59,7 +59,8 @@ typedef struct fmd_conv_desc {
   void* out;                /* bf16 (or fp32 if out_f32) [N][Ho][Wo][K] */
   int32_t out_f32;
   int32_t accumulate;       /* out += result */
-  float* stats;             /* slab [M/64][K][2] of per-64-pixel partial sums, or NULL */
+  float* stats;             /* slab [M/64][K][2] of per-64-pixel partial sums, or NULL; with splits > 1
+                               [M/FMD_SPLIT_STATS_ROWS][K][2] (written by the split-K combine) */
   const void* ep_x0;        /* data-gradient epilogue: x = forward GN input at (p, c); if ep_a: */
                             /*   out *= silu'(ep_a*x+ep_b); stats become (sum out, sum out*x) */
   const void* ep_x1;
@@ -98,6 +99,7 @@ typedef struct fmd_gn_apply_desc {
 int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_stream_t s);
 
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
+#define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);
@@ -162,6 +164,17 @@ int fmd_gn_bwd_prep(const float* s12, int32_t rows, int32_t N, int32_t HW, int32
                     int32_t emb_stride, int32_t emb_mode, float* P, float* Q, float* R,
                     float* dgamma, float* dbeta, float* demb, int32_t demb_stride, const float* fwd_st,
                     int32_t fwd_rows, float* ws /* [N][C][2] scratch */, fmd_stream_t s);
+/* Deferred gamma/beta gradients: fmd_gn_bwd_prep called with dgamma = dbeta = NULL leaves the per-(n,c)
+ * partials in its ws; one fmd_gn_gb_fold launch (<= FMD_GB_MAX jobs) then adds sum_n of every job's
+ * partials to its dgamma/dbeta -- one launch per backward pass instead of one per GroupNorm. */
+#define FMD_GB_MAX 64
+typedef struct {
+  const float* ws;   /* [N][C][2] (dgamma, dbeta) partials */
+  float* dgamma;     /* [C] += , may be NULL */
+  float* dbeta;      /* [C] += , may be NULL */
+  int32_t N, C;
+} fmd_gb_job;
+int fmd_gn_gb_fold(const fmd_gb_job* jobs, int32_t njobs, fmd_stream_t s);
 /* t = SiLU(a*x + b) (silu != 0) or a*x + b over the concat x0|x1 (bf16 [M][C0+C1]): the GroupNorm
  * prologue materialised once for its consumers. */
 int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,

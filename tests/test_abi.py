@@ -46,7 +46,7 @@ def test_struct_mirrors_match_header_field_order():
     from fmdiff import _lib
     src = open(HEADER).read()
     for cname, py in (("fmd_conv_desc", _lib.ConvDesc), ("fmd_wgrad_desc", _lib.WgradDesc),
-                      ("fmd_gn_apply_desc", _lib.GnApplyDesc)):
+                      ("fmd_gn_apply_desc", _lib.GnApplyDesc), ("fmd_gb_job", _lib.GbJob)):
         m = re.search(r"typedef\s+struct\s*(?:\w+\s*)?\{([^{}]*)\}\s*" + cname + r"\s*;", src, flags=re.S)
         assert m, cname
         body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)

@@ -109,6 +109,31 @@ def test_conv_splitk_matches():
     _close(b, a.float(), rel=8e-3)
 
 
+@pytest.mark.parametrize("ep", [False, True])
+def test_conv_splitk_fused_stats(ep):
+    """Split-K combine with the channel statistics fused (splitk_reduce_rows): output and (sum v, sum v^2)
+    / (sum v, sum v*x) slab rows vs fmd_channel_stats of the same output, plus bias / per-sample bias /
+    SiLU'-epilogue handling vs the unsplit conv."""
+    O = ops()
+    N, H, W, C, K = 2, 16, 16, 256, 192
+    x = _rand_nhwc(N, H, W, C, 41).to(DEV)
+    wp = O.prep_weights(_w(K, C, 3, 42).to(DEV), 0)
+    g = torch.Generator().manual_seed(43)
+    bias = (torch.randn(K, generator=g) * 0.1).to(DEV)
+    bnc = (torch.randn(N, K, generator=g) * 0.1).to(DEV)
+    kw = dict(bias=bias, bias_nc=bnc, want_stats=True, force_generic=True)
+    if ep:
+        xe = _rand_nhwc(N, H, W, K, 44).to(DEV)
+        kw.update(ep=(xe, None, (torch.rand(N, K, generator=g) + 0.5).to(DEV),
+                      (torch.randn(N, K, generator=g) * 0.2).to(DEV)))
+    a, sa = O.conv(x, K, wp, splits=1, **kw)
+    b, sb = O.conv(x, K, wp, splits=4, **kw)
+    _close(b, a.float(), rel=8e-3)
+    assert sb.rows == O.SPLIT_STATS_ROWS
+    ref = O.channel_stats(b, rows=sb.rows, y=(kw["ep"][0], None, K) if ep else None)
+    torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "s2_split"])
 def test_conv_data_gradient(mode):
     """Data gradients through the generic implicit GEMM; s2 runs the parity-class decomposition of the
@@ -239,6 +264,37 @@ def test_groupnorm_forward_backward():
     ref_ds = (dz * F.group_norm(x.detach(), G, gamma.detach(), beta.detach(), 1e-5)).sum((2, 3))
     torch.testing.assert_close(demb[:, :C].cpu(), ref_ds, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(demb[:, C:].cpu(), dz.sum((2, 3)), rtol=1e-3, atol=1e-3)
+
+
+def test_groupnorm_deferred_gamma_beta_fold():
+    """gb_defer/gb_flush (fmd_gn_gb_fold, one launch for many GroupNorms, incl. > FMD_GB_MAX jobs and
+    dgamma-only jobs) == the per-call fold of fmd_gn_bwd_prep, bit for bit."""
+    O = ops()
+    N, HW, G = 2, 64, 8
+    shapes = [(32 + 16 * (i % 5)) for i in range(70)]
+    g = torch.Generator().manual_seed(5)
+    cases = []
+    for i, Cc in enumerate(shapes):
+        slab = torch.randn(N * HW // 64, Cc, 2, generator=g).to(DEV)
+        mr = torch.stack([torch.randn(N, G, generator=g), torch.rand(N, G, generator=g) + 0.5], -1).to(DEV)
+        gamma = (torch.rand(Cc, generator=g) + 0.5).to(DEV)
+        beta = torch.randn(Cc, generator=g).to(DEV)
+        init = torch.randn(2, Cc, generator=g).to(DEV)
+        cases.append((O.Stats(slab, 64), Cc, mr, gamma, beta, init, i % 7 == 3))
+    ref, got = [], []
+    for st, Cc, mr, gamma, beta, init, no_beta in cases:
+        dg, db = init[0].clone(), init[1].clone()
+        O.gn_bwd_prep(st, N, HW, Cc, G, mr, gamma, beta, dg, None if no_beta else db)
+        ref.append((dg, db))
+    O.gb_defer()
+    for st, Cc, mr, gamma, beta, init, no_beta in cases:
+        dg, db = init[0].clone(), init[1].clone()
+        O.gn_bwd_prep(st, N, HW, Cc, G, mr, gamma, beta, dg, None if no_beta else db)
+        got.append((dg, db))
+    O.gb_flush()
+    torch.cuda.synchronize()
+    for (a0, b0), (a1, b1) in zip(ref, got):
+        assert torch.equal(a0, a1) and torch.equal(b0, b1)
 
 
 @pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32), (1, 64, 2, 16)])
