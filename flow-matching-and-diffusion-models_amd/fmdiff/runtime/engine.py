@@ -85,7 +85,12 @@ def _gdest(a: Optional[Act]):
 
 
 def _materialise(halo: bool, x1, Cin: int, HW: int) -> bool:
-    return MAT_PRO and halo and x1 is None and Cin <= MAT_CMAX and HW >= MAT_MIN_HW
+    """Materialise the GN+SiLU prologue (fmd_gn_apply_fwd) instead of fusing it into the conv: always on
+    the generic implicit-GEMM path (small levels), whose gather would redo the transform once per tap
+    (9x, VALU-bound at the low occupancy of those levels); on the halo path only if MAT_PRO."""
+    if not halo:
+        return True
+    return MAT_PRO and x1 is None and Cin <= MAT_CMAX and HW >= MAT_MIN_HW
 
 
 class WeightCache:
@@ -385,8 +390,9 @@ class UNetEngine:
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
         w1, w1t = self._wts(c1.weight, 0, halo1)
-        t1 = ops.gn_apply_fwd(x0.t, None, a1, b1) if _materialise(halo1, x1, Cin, HW) else None
-        h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=x1.t if x1 else None,
+        t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if _materialise(halo1, x1, Cin, HW) else None
+        src1 = x1.t if (x1 is not None and t1 is None) else None
+        h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=True,
                           wgt_tiled=w1t)
