@@ -389,8 +389,11 @@ class UNetEngine:
             es = eo.shape[1]
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
+        mat1 = _materialise(halo1, x1, Cin, HW)
+        if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
+            halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin)
         w1, w1t = self._wts(c1.weight, 0, halo1)
-        t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if _materialise(halo1, x1, Cin, HW) else None
+        t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
         src1 = x1.t if (x1 is not None and t1 is None) else None
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
@@ -410,11 +413,14 @@ class UNetEngine:
         else:
             _check_conv(sk.conv, 1, 1, 0)
         halo2 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cout, pro=True)
+        mat2 = _materialise(halo2, None, Cout, HW)
+        if mat2 and not halo2:
+            halo2 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cout)
         if not isinstance(sk, Identity):
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
         w2, w2t = self._wts(c2.weight, 0, halo2)
-        t2 = ops.gn_apply_fwd(h, None, a2, b2) if _materialise(halo2, None, Cout, HW) else None
+        t2 = ops.gn_apply_fwd(h, None, a2, b2) if mat2 else None
         out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
                             bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
         o = Act(out, ost)
