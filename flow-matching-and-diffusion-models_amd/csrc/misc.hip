@@ -381,6 +381,13 @@ __global__ void fill_from_table_kernel(const float* __restrict__ table, const in
   if (i < N) out[i] = table[index[0]];
 }
 
+// out[0:n] = table[index[0]*n : index[0]*n + n]  (one row of a per-step table, chosen on the device)
+__global__ void gather_row_kernel(const float* __restrict__ table, const int* __restrict__ index, long long n,
+                                  float* __restrict__ out) {
+  const float* src = table + (long long)index[0] * n;
+  GRID_STRIDE(i, n) out[i] = src[i];
+}
+
 __global__ void counter_add_kernel(int* c, int v) {
   if (threadIdx.x == 0) c[0] += v;
 }
@@ -796,6 +803,11 @@ int fmd_fill_from_table(const float* table, const int32_t* index, float* out, in
 }
 
 int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s) { LAUNCH(counter_add_kernel, 1, c, v); }
+
+int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s) {
+  if (n < 1 || !table || !index || !out) return -1;
+  LAUNCH(gather_row_kernel, grid_for(n), table, index, (long long)n, out);
+}
 
 int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc,
                   fmd_stream_t s) {

@@ -94,6 +94,7 @@ SIGNATURES = {
     "fmd_flow_euler": [p, p, i32, p, p, i32, i32, i32, p, i32, i32, p, p],
     "fmd_ddpm_step": [p, p, i32, p, p, p, i32, i32, i32, p, i32, i32, p, p],
     "fmd_fill_from_table": [p, p, p, i32, p],
+    "fmd_gather_row": [p, p, i64, p, p],
     "fmd_counter_add": [p, i32, p],
     "fmd_head_fwd": [p, i32, i32, i32, i32, p, p, p, p, i32, p, p],
     "fmd_head_dgrad": [p, p, i32, p, p, p, i32, i32, i32, i32, p, p, p],

@@ -250,6 +250,7 @@ class UNetEngine:
         else:
             raise TypeError(type(model))
         self.wc = WeightCache()
+        self._tt = None   # precomputed per-step time embeddings (set_time_table)
         self.gl, self.gl_slot = self._group_emb_layers(model)
         # weight gradients (+ their split-K reductions) may run on a second HIP stream beside the
         # data-gradient chain (they are off its critical path until the optimizer step).  Off by default:
@@ -577,8 +578,37 @@ class UNetEngine:
             self._head_bwd = bwd
         return out
 
+    def set_time_table(self, t_steps: Optional[torch.Tensor], N: int = 0, index: Optional[torch.Tensor] = None):
+        """Precompute the time embedding (+ grouped ResBlock projections) of every step of a fixed sampling
+        schedule ``t_steps`` [S] (each for a batch of N); forward(save=False) then copies row ``index[0]``
+        (device step counter) instead of running the time MLP -- one launch per step instead of four.
+        ``None`` clears the table."""
+        self._tt = None
+        if t_steps is None:
+            return
+        S = t_steps.shape[0]
+        t_all = t_steps.float().repeat_interleave(N)      # row i*N + n = step i, sample n
+        embs, eos = [], []
+        for r0 in range(0, S * N, 32):                    # the linear kernels take <= 32 rows per launch
+            ctx = self.time_mlp(t_all[r0:r0 + 32].contiguous(), False, min(32, S * N - r0))
+            embs.append(ctx.emb)
+            eos.append(ctx.eo_all)
+        emb = torch.cat(embs).view(S, -1)
+        eo = torch.cat(eos).view(S, -1) if eos[0] is not None else None
+        self._tt = dict(N=N, index=index, emb=emb, eo=eo, emb_cols=embs[0].shape[1],
+                        eo_cols=eos[0].shape[1] if eo is not None else 0)
+
     def time_mlp(self, t, ctx_save, N, t_scale=1.0, t_trunc=False):
         m = self.m
+        tt = getattr(self, "_tt", None)
+        if tt is not None and not ctx_save and N == tt["N"] and t_scale == 1.0 and not t_trunc:
+            emb = torch.empty((N, tt["emb_cols"]), device=tt["emb"].device, dtype=tt["emb"].dtype)
+            ops.gather_row(tt["emb"], tt["index"], emb)
+            ctx = Ctx(emb, False, N)
+            if tt["eo"] is not None:
+                ctx.eo_all = torch.empty((N, tt["eo_cols"]), device=emb.device, dtype=tt["eo"].dtype)
+                ops.gather_row(tt["eo"], tt["index"], ctx.eo_all)
+            return ctx
         if self.kind == "efficient":
             l1, l2 = m.time_embed[0], m.time_embed[2]
             feats = ops.timestep_embedding(t, m.model_channels, False, 0, t_scale=t_scale, t_trunc=t_trunc)

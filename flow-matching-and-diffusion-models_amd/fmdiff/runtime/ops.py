@@ -535,6 +535,11 @@ def fill_from_table(table, index, out):
     _lib.call("fmd_fill_from_table", _p(table), _p(index), _p(out), out.numel(), stream())
 
 
+def gather_row(table, index, out):
+    """out = table[index[0]] (row of ``out.numel()`` fp32 elements; ``index`` is a device int32 counter)."""
+    _lib.call("fmd_gather_row", _p(table), _p(index), out.numel(), _p(out), stream())
+
+
 def flow_euler(x, v_nhwc, sigmas, index, cond, next_inp):
     N, Cx = x.shape[:2]
     HW = x[0, 0].numel()

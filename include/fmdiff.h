@@ -260,6 +260,9 @@ int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, c
                   const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
                   void* next, fmd_stream_t s);
 int fmd_fill_from_table(const float* table, const int32_t* index, float* out, int32_t N, fmd_stream_t s);
+/* out[0:n] = table[index[0]*n : (index[0]+1)*n] -- a per-step row (e.g. precomputed time embeddings of a
+ * sampling schedule) selected by a device-side step counter, so the step stays graph-replayable. */
+int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s);
 int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s);
 
 #ifdef __cplusplus

@@ -90,3 +90,33 @@ def test_train_step_gradients_vs_oracle(golden):
     print(f"grad rel L2 {rel:.3e}, worst cosine {worst}")
     assert rel < 5e-2
     assert worst[0] > 0.99, worst
+
+
+def test_fused_sampler_matches_plain_euler_loop(golden):
+    """FusedFlowSampler (hipGraph-replayed step, per-schedule time-embedding table selected by the device
+    step counter) == the plain FlowMatchEuler loop x += (sigma[i+1] - sigma[i]) * model(x | cond, t_i)
+    through the module API (src/pipelines/utils.py:163-220 sampling order)."""
+    from fmdiff.pipelines.schedulers import FlowMatchEulerDiscreteScheduler
+    from fmdiff.pipelines.train.fused import FusedFlowSampler
+    T, M = golden
+    name = "ldct_fm_test"
+    meta = M[name]
+    model = _build(meta).to(DEV)
+    _load_seeded(model, meta)
+    g = torch.Generator().manual_seed(7)
+    init = torch.randn(T[f"{name}/x"].shape, generator=g).to(DEV)
+    cond = T[f"{name}/cond"].to(DEV)
+    steps = 6
+    sch = FlowMatchEulerDiscreteScheduler(1000)
+    sch.set_timesteps(steps)
+    x = init.clone()
+    with torch.no_grad():
+        for i in range(steps):
+            t = sch.timesteps[i].float().expand(x.shape[0]).to(DEV)
+            v = model(x, t, context=cond)
+            x = x + (sch.sigmas[i + 1] - sch.sigmas[i]).item() * v.float()
+    for use_graph in (True, False):
+        got = FusedFlowSampler(model, steps).sample(init, cond, use_graph=use_graph)
+        err = _rel(got, x)
+        print(f"graph={use_graph}: rel L2 {err:.3e}")
+        assert err < 2e-3
