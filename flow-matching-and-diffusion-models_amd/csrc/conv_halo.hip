@@ -33,12 +33,12 @@ constexpr int TH = 16, TW = 16;           // output tile
 constexpr int BCO = 128;                  // output channels per tile
 constexpr int BK = FMD_HALO_BK;           // input channels per chunk (32)
 constexpr int KC = BK / 8;                // 16-byte chunks per position (4)
-constexpr int NT = 512;
+// Workgroup: NT = 512 (8 waves of 64 couts x 4 rows, 128 VGPRs, 4 waves/SIMD) or NT = 256 (4 waves of
+// 64 couts x 8 rows: twice the MFMAs per fragment read and 256 VGPRs for addresses / prefetch, 2 waves/SIMD).
 constexpr int HALO = (TH + 2) * (TW + 2); // 324 positions
 constexpr int HPAD = 336;                 // plane stride (rows): == 0 mod 16 bank slots
 constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer (21 KiB)
 constexpr int WBUF = KC * BCO * 8;        // bf16 elements per weight tile (8 KiB = one 16 B DMA per thread)
-static_assert(WBUF == NT * 8, "one weight DMA per thread");
 static_assert(2 * HBUF + 4 * WBUF >= TH * TW * BCO, "epilogue tile fits in the staging LDS");
 
 struct HArgs {
@@ -62,6 +62,7 @@ struct HArgs {
 #endif
 
 static int g_dbg = 0;
+static int g_nt = 512;   // workgroup size of the halo conv (fmd_halo_set_workgroup; FMD_HALO_NT at load)
 
 // staged piece h (16 bytes) of a chunk: blocks of 32 = 8 consecutive positions x KC channel groups
 FMD_DEV int piece_pos(int h) { return (h >> 5) * 8 + (h & 7); }
@@ -82,7 +83,8 @@ static_assert(SM_BYTES <= 163840 / 2, "two workgroups per CU");
 // would drain the halo prefetch that is meant to stay in flight across the barrier.
 template <int KEEP>
 FMD_DEV void step_barrier() {
-  if (KEEP) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+  if constexpr (KEEP == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+  else if constexpr (KEEP == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -99,8 +101,20 @@ FMD_DEV void glds16(const void* gsrc, unsigned lds_dst) {
 }
 
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
-template <bool UP, int PRO>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo(const HArgs A) {
+template <int NT>
+struct HaloCfg {
+  static constexpr int NW = NT / 64;           // waves
+  static constexpr int WR = 16 / (NW / 2);     // output rows per wave (4 | 8)
+  static constexpr int EPW = NT == 512 ? 4 : 2;
+};
+
+template <bool UP, int PRO, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(HaloCfg<NT>::EPW, HaloCfg<NT>::EPW)))
+void conv3x3_halo(const HArgs A) {
+  constexpr int WR = HaloCfg<NT>::WR;
+  constexpr int NWH = HaloCfg<NT>::NW / 2;                 // waves per cout half
+  constexpr int WDMA = WBUF / (NT * 8);                    // 16-byte weight DMAs per thread per tap
+  static_assert(WDMA * NT * 8 == WBUF, "weight tile DMA split");
   constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
   constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk (100 | 324)
   constexpr int TOT1 = ((HPOS + 7) / 8) * 8 * KC;          // staged pieces of a main chunk
@@ -108,7 +122,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int LPT = (PC1 + NT - 1) / NT;                 // loads per thread per staging step (1)
   constexpr int LPRO = (TOT1 + NT - 1) / NT;               // loads per thread for the prologue's full chunk
   constexpr int SEG2 = TH * TW * KC;                       // pieces of a 1x1 chunk (1024)
-  static_assert(LPT == 1, "one staged piece per thread and step");
+  static_assert(LPT >= 1 && LPT <= 2, "staged pieces per thread and step");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
   bf16r* const lds = (bf16r*)smem;
   bf16r* const hbuf = (bf16r*)(smem + SM_H);
@@ -119,7 +133,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
   const fmd_conv_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid >> 2, wpx = wid & 3;   // 2 x 4 waves: 64 couts x 4 pixel rows each
+  const int wco = wid / NWH, wpx = wid % NWH;   // 2 x NWH waves: 64 couts x WR pixel rows each
   const int l16 = lane & 15, lq = lane >> 4;
   const int kc = piece_kc(tid);              // staged pieces start at multiples of 32: the channel group is fixed
 
@@ -165,12 +179,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     } else {
       src = A.wt2 + ((size_t)tco * A.nchunk2 + (slot - A.nchunk1 * 9)) * WBUF;
     }
-    const unsigned dst = lds_base + SM_W + (unsigned)(wtile * WBUF + wid * 64 * 8) * 2;
-    glds16(src + tid * 8, __builtin_amdgcn_readfirstlane(dst));
+#pragma unroll
+    for (int k = 0; k < WDMA; ++k) {
+      const unsigned dst = lds_base + SM_W + (unsigned)(wtile * WBUF + (wid * 64 + k * NT) * 8) * 2;
+      glds16(src + (tid + k * NT) * 8, __builtin_amdgcn_readfirstlane(dst));
+    }
   };
 
   // ---- halo staging through registers (the GN/SiLU transform happens between load and LDS store)
-  constexpr int LMAX = LPRO > 2 ? LPRO : 2;
+  constexpr int LMAX = LPRO > SEG2 / NT ? (LPRO > 2 ? LPRO : 2) : (SEG2 / NT > 2 ? SEG2 / NT : 2);
   u32x4 rh[LMAX];
   int hoff[LMAX];            // LDS element offset; -1: no store; bit 30: store zeros (padding)
   const bf16r* cbase = s0;   // this thread's channel group of the chunk being staged
@@ -248,7 +265,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (o >= 0) *(u32x4*)(hbuf + buf * HBUF + (o & ~(1 << 30))) = v;
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][WR];
 
   auto compute = [&](int hb_i, int tap, bool seg2, int wb_i) {
     const bf16r* hb = hbuf + hb_i * HBUF;
@@ -257,9 +274,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     bf16x8 af[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(wb + (lq * BCO + wco * 64 + 16 * i + l16) * 8);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int py = wpx * 4 + j;
+    auto bfrag = [&](int j) -> bf16x8 {
+      const int py = wpx * WR + j;
       int pos;
       if (UP && !seg2) {
         const int ly = ((ty0 + py + ky - 1) >> 1) - hy0;
@@ -268,9 +284,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         pos = (py + ky) * (TW + 2) + l16 + kx;
       }
-      const bf16x8 bv = *(const bf16x8*)(hb + (lq * HPAD + pos) * 8);
+      return *(const bf16x8*)(hb + (lq * HPAD + pos) * 8);
+    };
+    if constexpr (NT == 256) {
+      // all WR row fragments read up front (256-VGPR variant): their LDS latency overlaps the MFMAs
+      bf16x8 bv[WR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
+      for (int j = 0; j < WR; ++j) bv[j] = bfrag(j);
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them)
+#pragma unroll
+      for (int j = 0; j < WR; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);   // and keep later waits (halo consume) out of the MFMA block
+    } else {
+#pragma unroll
+      for (int j = 0; j < WR; ++j) {
+        const bf16x8 bv = bfrag(j);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
+      }
     }
   };
 
@@ -294,7 +327,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   step_barrier<0>();
 
   // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8).  The next chunk's halo is staged in
@@ -325,37 +358,52 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         // one halo load per step, always (a dummy in-bounds read when nothing is staged): the register
         // then has the same load -> consume pattern on every path, so hipcc's waits stay counted
         if (issue && ps == 0) setup(nx);
-        const int h = ps * (nseg2 ? SEG2 / 4 : PC1) + tid;
-        const bool act = issue && (nseg2 ? tid < SEG2 / 4 : (tid < PC1 && h < TOT1));
-        int off;
-        const bf16r* src = piece_src(h, act, nseg2, off);
-        if (HDBG(1)) {
-          rh[0] = u32x4{0u, 0u, 0u, 0u};
-        } else {
-          rh[0] = *(const u32x4*)src;
+#pragma unroll
+        for (int k = 0; k < LPT; ++k) {
+          const int t = tid + NT * k;
+          const int h = ps * (nseg2 ? SEG2 / 4 : PC1) + t;
+          const bool act = issue && (nseg2 ? t < SEG2 / 4 : (t < PC1 && h < TOT1));
+          int off;
+          const bf16r* src = piece_src(h, act, nseg2, off);
+          if (HDBG(1)) {
+            rh[k] = u32x4{0u, 0u, 0u, 0u};
+          } else {
+            rh[k] = *(const u32x4*)src;
+          }
+          hoff[k] = off;
         }
-        hoff[0] = off;
+      };
+      auto consume = [&]() {   // the previous step's halo loads are consumed here, on every path
+#pragma unroll
+        for (int k = 0; k < LPT; ++k) asm volatile("" ::"v"(rh[k]));
+      };
+      auto store_pending = [&]() {
+        if (pend) {
+#pragma unroll
+          for (int k = 0; k < LPT; ++k) store(nx & 1, k, !nseg2, pc);
+        }
       };
       // Waves w and w+4 share a SIMD: the wco 0 wave stages (GN/SiLU VALU work) before its first tap,
       // the wco 1 wave after it, so one wave's transform overlaps the other's MFMAs.
       if (wco == 0) {
-        asm volatile("" ::"v"(rh[0]));   // the previous step's halo load is consumed here, on every path
-        if (pend) store(nx & 1, 0, !nseg2, pc);
+        consume();
+        store_pending();
         issue_loads();
         compute(chunk & 1, 2 * ps, false, 2 * wb);
       } else {
         compute(chunk & 1, 2 * ps, false, 2 * wb);
-        asm volatile("" ::"v"(rh[0]));
-        if (pend) store(nx & 1, 0, !nseg2, pc);
+        consume();
+        store_pending();
         issue_loads();
       }
       pc = cch;
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
-      step_barrier<1>();
+      step_barrier<LPT>();
       wb ^= 1;
     }
   }
-  asm volatile("" ::"v"(rh[0]));
+#pragma unroll
+  for (int k = 0; k < LPT; ++k) asm volatile("" ::"v"(rh[k]));
   // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, next chunk staged whole
   for (int chunk = A.nchunk1; chunk < A.nchunk1 + n_seg2; ++chunk) {
     const int nx = chunk + 1;
@@ -387,8 +435,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int co = co0 + wco * 64 + 16 * i + 4 * lq;
       if (co >= K) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t p = ((size_t)n * Ho + ty0 + wpx * 4 + j) * Wo + tx0 + l16;
+      for (int j = 0; j < WR; ++j) {
+        const size_t p = ((size_t)n * Ho + ty0 + wpx * WR + j) * Wo + tx0 + l16;
         if (co + 3 < K) {
           *(f32x4*)(ws + p * K + co) = acc[i][j];
         } else {
@@ -403,9 +451,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const bool dep = d.ep_a != nullptr;
   const bool hasx = d.ep_x0 != nullptr;
   // per-channel sums of this lane's 4 pixels, reduced over the wave's 16 pixel lanes per cout block:
-  // slab row = one wave's 64 pixels (4 rows x 16) of one image; any bijection works for GN
-  const int srow = tile * 4 + wpx;
-  auto flush_stats = [&](int i, const float* a4, const float* q4) {
+  // slab row = 64 pixels (4 tile rows x 16) of one image; any bijection works for GN
+  auto flush_stats = [&](int i, int j0, const float* a4, const float* q4) {
+    const int srow = tile * 4 + (wpx * WR + j0) / 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float a = row16_sum_to_last(a4[r]), q = row16_sum_to_last(q4[r]);
@@ -425,9 +473,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const bool side = d.resid != nullptr || hasx;
     if (side) {
       // the whole 64 KiB side tile in flight at once (the main loop's fragments are dead here)
-      u32x4 sv[8];
+      constexpr int SK = TH * TW * BCO / 8 / NT;   // 16-byte pieces per thread (8 | 16)
+      u32x4 sv[SK];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < SK; ++k) {
         const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
         const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
         const int c = co0 + c16 * 8;
@@ -437,7 +486,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         sv[k] = *(const u32x4*)src;
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < SK; ++k) {
         const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
         *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
       }
@@ -451,8 +500,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const f32x4 ea = *(const f32x4*)(epi + BCO + cl), eb = *(const f32x4*)(epi + 2 * BCO + cl);
       float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int pi = (wpx * 4 + j) * 16 + l16;
+      for (int j = 0; j < WR; ++j) {
+        const int pi = (wpx * WR + j) * 16 + l16;
         bf16r* tp8 = tileb + pi * BCO + (((cl >> 3) ^ (pi & 15)) * 8) + (cl & 7);
         float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -483,12 +532,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             st2[r] += hasx ? w[r] * xv[r] : w[r] * w[r];
           }
         }
+        if (stats && (j & 3) == 3) {   // one slab row per 4 tile rows
+          flush_stats(i, j - 3, st1, st2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { st1[r] = 0.f; st2[r] = 0.f; }
+        }
       }
-      if (stats) flush_stats(i, st1, st2);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < TH * TW * BCO / 8 / NT; ++k) {
       const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
       const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
       *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) =
@@ -510,8 +563,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
       float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
   #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int y = ty0 + wpx * 4 + j, x = tx0 + l16;
+      for (int j = 0; j < WR; ++j) {
+        const int y = ty0 + wpx * WR + j, x = tx0 + l16;
         const size_t p = ((size_t)n * Ho + y) * Wo + x;
         float v[4];
   #pragma unroll
@@ -569,9 +622,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             st1[r] += v[r];
             st2[r] += hasx ? v[r] * xv[r] : v[r] * v[r];
           }
+          if ((j & 3) == 3) {
+            flush_stats(i, j - 3, st1, st2);
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) { st1[r] = 0.f; st2[r] = 0.f; }
+          }
         }
       }
-      if (stats) flush_stats(i, st1, st2);
     }
   }
 }
@@ -626,16 +683,30 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < 128) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
-  const dim3 g(nwg, A.splits), blk(NT);
   hipStream_t st = (hipStream_t)stream;
+  const dim3 g(nwg, A.splits);
+  if (g_nt == 256) {
+    const dim3 blk(256);
+    if (d->upsample) {
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2, 256>), g, blk, 0, st, A);
+      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1, 256>), g, blk, 0, st, A);
+      else hipLaunchKernelGGL((conv3x3_halo<true, 0, 256>), g, blk, 0, st, A);
+    } else {
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2, 256>), g, blk, 0, st, A);
+      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1, 256>), g, blk, 0, st, A);
+      else hipLaunchKernelGGL((conv3x3_halo<false, 0, 256>), g, blk, 0, st, A);
+    }
+    return (int)hipGetLastError();
+  }
+  const dim3 blk(512);
   if (d->upsample) {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo<true, 0>), g, blk, 0, st, A);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2, 512>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1, 512>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<true, 0, 512>), g, blk, 0, st, A);
   } else {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo<false, 0>), g, blk, 0, st, A);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2, 512>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1, 512>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<false, 0, 512>), g, blk, 0, st, A);
   }
   return (int)hipGetLastError();
 }
@@ -643,6 +714,12 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
 // Debug hook (not part of the public ABI): ablation flags of the next launches (see HArgs::dbg).
 extern "C" int fmd_debug_halo_flags(int flags) {
   g_dbg = flags;
+  return 0;
+}
+
+extern "C" int fmd_halo_set_workgroup(int32_t nt) {
+  if (nt != 256 && nt != 512) return -1;
+  g_nt = nt;
   return 0;
 }
 

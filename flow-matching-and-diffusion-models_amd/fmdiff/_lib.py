@@ -71,6 +71,7 @@ SIGNATURES = {
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
     "fmd_gn_gb_fold": [p, i32, p],
+    "fmd_halo_set_workgroup": [i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_batch": [p, i32, i32, p],
@@ -119,6 +120,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, i32)
+        if os.environ.get("FMD_HALO_NT"):
+            check(L.fmd_halo_set_workgroup(int(os.environ["FMD_HALO_NT"])), "fmd_halo_set_workgroup")
         _lib = L
     return _lib
 

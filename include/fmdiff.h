@@ -100,6 +100,9 @@ int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_st
 
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
+/* Halo conv workgroup size: 512 (8 waves x 64 pixels each, default) or 256 (4 waves x 128 pixels,
+ * 256 VGPRs per wave).  Returns -1 for other values.  Also settable with FMD_HALO_NT at load time. */
+int fmd_halo_set_workgroup(int32_t nt);
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);

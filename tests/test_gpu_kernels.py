@@ -574,3 +574,42 @@ def test_halo_conv_split_k_matches_generic(case):
         ta = sa.slab.view(N, -1, K, 2).sum(1)
         tb = sb.slab.view(N, -1, K, 2).sum(1)
         torch.testing.assert_close(ta, tb, rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("case", ["pro_stats", "skip_seg2", "dgrad_ep", "upsample", "split"])
+def test_halo_workgroup_256_matches_512(case):
+    """fmd_halo_set_workgroup(256) (4 waves x 8 rows, 256 VGPRs) computes exactly what the default
+    512-thread kernel computes: same per-element reduction order, so outputs and statistics are equal."""
+    import ctypes
+    from fmdiff import _lib
+    O = ops()
+    N, H, W, C, K = 4, 128, 128, 128, 128
+    if case == "split":
+        N, H, W, C, K = 4, 32, 32, 512, 256
+    x = _rand_nhwc(N, H // 2 if case == "upsample" else H, W // 2 if case == "upsample" else W, C, 51).to(DEV)
+    w = O.prep_weights(_w(K, C, 3, 52).to(DEV), 0)
+    kw = dict(bias=(torch.randn(K) * 0.1).to(DEV), want_stats=case != "split")
+    if case in ("pro_stats", "upsample", "split"):
+        kw["pro"] = ((torch.rand(N, C) + 0.5).to(DEV), (torch.randn(N, C) * 0.2).to(DEV), True)
+    if case == "upsample":
+        kw["upsample"] = True
+    if case == "skip_seg2":
+        kw.update(src2=_rand_nhwc(N, H, W, 64, 53).to(DEV), wgt2=O.prep_weights(_w(K, 64, 1, 54).to(DEV), 0))
+    if case == "dgrad_ep":
+        kw["ep"] = (_rand_nhwc(N, H, W, K, 55).to(DEV), None, (torch.rand(N, K) + 0.5).to(DEV),
+                    (torch.randn(N, K) * 0.2).to(DEV))
+    assert O.halo_eligible(N, x.shape[1], H, W, K, upsample=case == "upsample", Cin=C, pro="pro" in kw)
+    L = _lib.lib()
+    outs = []
+    try:
+        for nt in (512, 256):
+            assert L.fmd_halo_set_workgroup(ctypes.c_int32(nt)) == 0
+            wt = O.tile_weights(w)
+            w2t = O.tile_weights(kw["wgt2"]) if "wgt2" in kw else None
+            o, st = O.conv(x, K, w, wgt_tiled=wt, wgt2_tiled=w2t, **kw)
+            outs.append((o, st))
+    finally:
+        L.fmd_halo_set_workgroup(ctypes.c_int32(512))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1].slab, outs[1][1].slab)
