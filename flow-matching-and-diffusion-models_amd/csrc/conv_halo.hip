@@ -90,16 +90,6 @@ FMD_DEV void step_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// 16-byte LDS-DMA (global_load_lds_dwordx4) issued through inline asm: hipcc neither counts it nor
-// makes later ds_reads wait for it (its builtin form drains vmcnt before every following LDS read),
-// so the pipeline's own counted waits in step_barrier() are the only ones.  lds_dst: wave-uniform
-// LDS byte address; lane i lands at lds_dst + 16 i.
-FMD_DEV void glds16(const void* gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
 template <int NT>
 struct HaloCfg {

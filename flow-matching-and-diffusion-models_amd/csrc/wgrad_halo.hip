@@ -49,6 +49,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   __shared__ __attribute__((aligned(16))) bf16r lds[2 * XBUF + 2 * DBUF];
   bf16r* xb = lds;
   bf16r* db_ = lds + 2 * XBUF;
+  const unsigned db_base = (unsigned)(size_t)(__attribute__((address_space(3))) bf16r*)db_;
   const fmd_wgrad_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid >> 2, wci = wid & 3;
@@ -114,7 +115,9 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
     }
   };
-  // dY needs no transform: gathered global -> LDS by DMA (lane = one pixel's 16-byte channel group)
+  // dY needs no transform: gathered global -> LDS by DMA (lane = one pixel's 16-byte channel group).
+  // Issued through inline asm (glds16): the builtin form makes hipcc drain vmcnt before every later
+  // LDS read, i.e. the next tile's loads would be waited for inside this tile's MFMA loop.
   auto dma_dy = [&](int t, int buf) {
     int n, ty0, tx0;
     tile_org(t, n, ty0, tx0);
@@ -123,10 +126,8 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       const int idx = wid * 4 + j, plane = idx >> 1, half = idx & 1;
       const int pos = half * 64 + lane;
       const int pix = (n * d.Ho + ty0 + (pos >> 4)) * d.Wo + tx0 + (pos & 15);
-      __builtin_amdgcn_global_load_lds((const void*)(dy + (size_t)pix * A.ldy + co0 + plane * 8),
-                                       (__attribute__((address_space(3))) void*)(db_ + buf * DBUF +
-                                                                                 (plane * DPAD + half * 64) * 8),
-                                       16, 0, 0);
+      const unsigned dst = db_base + (unsigned)(buf * DBUF + (plane * DPAD + half * 64) * 8) * 2;
+      glds16(dy + (size_t)pix * A.ldy + co0 + plane * 8, __builtin_amdgcn_readfirstlane(dst));
     }
   };
   auto store_tile = [&](int buf) {
@@ -194,6 +195,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
     dma_dy(t0, 0);
     load_tile(t0);
     store_tile(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the asm DMAs are not tracked by hipcc
     __syncthreads();
     int buf = 0;
     for (int t = t0; t < t1; ++t) {
@@ -204,6 +206,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       }
       compute(buf);
       if (more) store_tile(buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's dY DMA landed before the barrier
       __syncthreads();
       buf ^= 1;
     }
