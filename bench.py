@@ -171,7 +171,7 @@ def main():
     ldct = (clean + 0.05 * torch.randn(B, 1, HW, HW, device=dev, generator=g)).clamp(0, 1)
 
     trainer = FusedTrainStep(model, lr=1e-4, warmup=500, total_steps=100 * 1000, num_train_timesteps=1000)
-    use_graph = (not args.no_graph) and world == 1
+    use_graph = not args.no_graph   # N > 1: forward + backward replayed, all-reduce + AdamW issued eagerly
     if use_graph:
         trainer.capture(clean, ldct, warmup_iters=2)
         run = trainer.replay

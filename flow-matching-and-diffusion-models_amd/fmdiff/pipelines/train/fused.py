@@ -77,6 +77,7 @@ class FusedTrainStep:
             self.acp = ddpm_scheduler.alphas_cumprod.to(dev, torch.float32)
         self._graph = None
         self._static = None
+        self._split = False
 
     # ---------------------------------------------------------------- body
     def _chunk(self, clean, ldct, noise, t_or_ts):
@@ -103,6 +104,19 @@ class FusedTrainStep:
 
     def step(self, clean, ldct, noise=None, t=None):
         """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss."""
+        loss = self._fwd_bwd(clean, ldct, noise, t)
+        self._allreduce()
+        self._adamw()
+        return loss
+
+    def _adamw(self):
+        b1, b2 = self.hp["betas"]
+        ops.adamw_sched(self.flat.data, self.flat.grad, self.m, self.v, self.step_ctr, self.hp["lr"], self.hp["warmup"],
+                        self.hp["total"], b1, b2, self.hp["eps"], self.hp["wd"], 1.0 / self.world)
+        ops.counter_add(self.step_ctr)
+
+    def _fwd_bwd(self, clean, ldct, noise=None, t=None):
+        """Weight refresh, gradient zeroing and forward + backward of every grad-accumulation chunk."""
         self.eng.invalidate_weights()            # bf16 kernel weights re-derived from the updated masters
         self.flat.grad.zero_()
         N = clean.shape[0]
@@ -118,16 +132,15 @@ class FusedTrainStep:
                 tt = t[c0:c0 + chunk] if t is not None else torch.randint(0, self.N_train, (cl.shape[0],),
                                                                            device=cl.device)
             loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt)
-        self._allreduce()
-        b1, b2 = self.hp["betas"]
-        ops.adamw_sched(self.flat.data, self.flat.grad, self.m, self.v, self.step_ctr, self.hp["lr"], self.hp["warmup"],
-                        self.hp["total"], b1, b2, self.hp["eps"], self.hp["wd"], 1.0 / self.world)
-        ops.counter_add(self.step_ctr)
         return loss
 
     # ---------------------------------------------------------- hipGraph
-    def capture(self, clean, ldct, warmup_iters: int = 2):
-        """Capture one full step (RNG, forward, loss, backward, [all-reduce], AdamW) into a hipGraph."""
+    def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None):
+        """Capture one step into a hipGraph.  Single process: the whole step (RNG, forward, loss, backward,
+        AdamW).  With several ranks (``split_collectives``, default: world > 1) the graph holds RNG +
+        forward + backward, and each replay is followed by the bucketed RCCL all-reduce and the AdamW
+        launch issued eagerly: no collective is ever recorded into a graph."""
+        self._split = self.world > 1 if split_collectives is None else bool(split_collectives)
         self._static = (clean.clone(), ldct.clone() if ldct is not None else None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -137,7 +150,10 @@ class FusedTrainStep:
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._graph_loss = self.step(*self._static)
+            if self._split:
+                self._graph_loss = self._fwd_bwd(*self._static)
+            else:
+                self._graph_loss = self.step(*self._static)
         self._graph = g
 
     def replay(self, clean=None, ldct=None):
@@ -146,6 +162,9 @@ class FusedTrainStep:
         if ldct is not None:
             self._static[1].copy_(ldct)
         self._graph.replay()
+        if self._split:
+            self._allreduce()
+            self._adamw()
         return self._graph_loss
 
 

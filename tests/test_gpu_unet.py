@@ -120,3 +120,28 @@ def test_fused_sampler_matches_plain_euler_loop(golden):
         err = _rel(got, x)
         print(f"graph={use_graph}: rel L2 {err:.3e}")
         assert err < 2e-3
+
+
+def test_fused_train_step_split_capture_matches_full_graph(golden):
+    """FusedTrainStep.capture(split_collectives=True) -- the multi-rank form: forward+backward graph,
+    then the (bucketed) all-reduce and AdamW issued eagerly -- reproduces the single-graph step."""
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    T, M = golden
+    name = "ldct_fm_test"
+    meta = M[name]
+    x, cond = T[f"{name}/x"].to(DEV), T[f"{name}/cond"].to(DEV)
+    clean = x.clamp(0, 1)
+    res = []
+    for split in (False, True):
+        model = _build(meta).to(DEV)
+        _load_seeded(model, meta)
+        tr = FusedTrainStep(model, lr=1e-3, warmup=1)
+        torch.manual_seed(11)
+        tr.capture(clean, cond, warmup_iters=2, split_collectives=split)
+        losses = [float(tr.replay().item()) for _ in range(2)]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().clone()))
+    (la, pa), (lb, pb) = res
+    assert all(math.isfinite(v) for v in la + lb)
+    assert la == lb
+    assert torch.equal(pa, pb)
