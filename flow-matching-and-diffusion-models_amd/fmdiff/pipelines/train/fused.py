@@ -24,15 +24,20 @@ from typing import Optional
 import torch
 
 from ...runtime import ops
-from ...runtime.dp import bucketed_allreduce, world_size
+from ...runtime.dp import bucketed_allreduce, bucketed_allreduce_async, world_size
 from ...runtime.engine import get_engine
 
 
 class FlatParams:
-    """Re-point every parameter (and its .grad) into one flat fp32 buffer."""
+    """Re-point every parameter (and its .grad) into one flat fp32 buffer.  ``first``: parameters laid out
+    at the front (``split_at`` elements), e.g. those whose gradients are final early in the backward."""
 
-    def __init__(self, model: torch.nn.Module):
+    def __init__(self, model: torch.nn.Module, first=None):
         params = [p for p in model.parameters()]
+        if first:
+            ids = {id(p) for p in first}
+            params = list(first) + [p for p in params if id(p) not in ids]
+        self.split_at = sum(p.numel() for p in first) if first else 0
         dev = params[0].device
         total = sum(p.numel() for p in params)
         self.data = torch.empty(total, device=dev, dtype=torch.float32)
@@ -54,10 +59,14 @@ class FusedTrainStep:
     def __init__(self, model, *, objective: str = "flow_matching", lr: float = 1e-4, weight_decay: float = 0.0,
                  warmup: int = 500, total_steps: int = 10 ** 9, num_train_timesteps: int = 1000,
                  grad_accum: int = 1, betas=(0.9, 0.999), eps: float = 1e-8, ddpm_scheduler=None,
-                 process_group=None, allreduce_buckets: int = 4):
+                 process_group=None, allreduce_buckets: int = 4, overlap_allreduce: Optional[bool] = None):
         self.model = model
         self.eng = get_engine(model)
-        self.flat = FlatParams(model)
+        world = world_size(process_group)
+        # data parallel: the decoder's gradients (final after backward part 1) go first in the flat buffer
+        # and are all-reduced while the encoder's backward runs
+        self.overlap = (world > 1 if overlap_allreduce is None else bool(overlap_allreduce)) and grad_accum <= 1
+        self.flat = FlatParams(model, self.eng.decoder_params() if self.overlap else None)
         dev = self.flat.data.device
         self.m = torch.zeros_like(self.flat.data)
         self.v = torch.zeros_like(self.flat.data)
@@ -96,8 +105,16 @@ class FusedTrainStep:
             ta, tb, sign = noise, None, 0.0                                        # target eps
         dpred = torch.empty(out.shape, device=out.device, dtype=torch.bfloat16)
         ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
-        self.eng.backward(ctx, dpred)
+        if self.overlap:
+            self.eng.backward(ctx, dpred, part=1)   # part 2 in _bwd_rest, after the decoder all-reduce starts
+            self._ctx = ctx
+        else:
+            self.eng.backward(ctx, dpred)
         return self.loss
+
+    def _bwd_rest(self):
+        self.eng.backward(self._ctx, None, part=2)
+        self._ctx = None
 
     def _allreduce(self):
         bucketed_allreduce(self.flat.grad, self.buckets, self.pg)
@@ -105,9 +122,21 @@ class FusedTrainStep:
     def step(self, clean, ldct, noise=None, t=None):
         """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss."""
         loss = self._fwd_bwd(clean, ldct, noise, t)
-        self._allreduce()
+        if self.overlap:
+            self._overlapped_tail(self._bwd_rest)
+        else:
+            self._allreduce()
         self._adamw()
         return loss
+
+    def _overlapped_tail(self, rest):
+        """Decoder gradients all-reduced (async) while ``rest`` (the encoder backward) runs, then the rest."""
+        k = self.flat.split_at
+        works = bucketed_allreduce_async(self.flat.grad[:k], max(1, self.buckets // 2), self.pg)
+        rest()
+        bucketed_allreduce(self.flat.grad[k:], max(1, self.buckets // 2), self.pg)
+        for w in works:
+            w.wait()
 
     def _adamw(self):
         b1, b2 = self.hp["betas"]
@@ -155,6 +184,12 @@ class FusedTrainStep:
             else:
                 self._graph_loss = self.step(*self._static)
         self._graph = g
+        self._graph2 = None
+        if self._split and self.overlap:   # the encoder backward as a second graph in the same pool
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=g.pool()):
+                self._bwd_rest()
+            self._graph2 = g2
 
     def replay(self, clean=None, ldct=None):
         if clean is not None:
@@ -163,7 +198,10 @@ class FusedTrainStep:
             self._static[1].copy_(ldct)
         self._graph.replay()
         if self._split:
-            self._allreduce()
+            if self._graph2 is not None:
+                self._overlapped_tail(self._graph2.replay)
+            else:
+                self._allreduce()
             self._adamw()
         return self._graph_loss
 

@@ -34,3 +34,13 @@ def bucketed_allreduce(flat: torch.Tensor, buckets: int = 4, group=None) -> None
         return
     for lo, hi in bucket_bounds(flat.numel(), buckets):
         dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=group)
+
+
+def bucketed_allreduce_async(flat: torch.Tensor, buckets: int = 2, group=None) -> list:
+    """Start in-place SUM all-reduces of ``flat`` (bucket by bucket) without making the current stream wait:
+    compute issued afterwards overlaps them; call ``.wait()`` on every returned work before reading ``flat``."""
+    if world_size(group) <= 1:
+        return []
+    return [dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True)
+            for lo, hi in bucket_bounds(flat.numel(), buckets)]
+

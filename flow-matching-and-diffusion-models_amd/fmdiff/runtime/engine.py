@@ -220,7 +220,7 @@ class WeightCache:
 
 
 class Ctx:
-    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all")
+    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark")
 
     def __init__(self, emb, save, N):
         self.emb = emb
@@ -229,6 +229,7 @@ class Ctx:
         self.N = N
         self.eo_all = None      # [N][sum O] grouped emb projections of all ResBlocks
         self.demb_all = None
+        self.mark = 0           # tape length when the decoder started (backward part 1 = tape[mark:])
 
 
 def _check_conv(c: Conv, ks, stride, pad):
@@ -654,6 +655,8 @@ class UNetEngine:
                 hs.append(h)
             for layer in m.middle_block:
                 h = self._apply(layer, h, ctx)
+            if ctx.tape is not None:
+                ctx.mark = len(ctx.tape)
             for blk in m.output_blocks:
                 skip = hs.pop()
                 layers = list(blk)
@@ -678,6 +681,8 @@ class UNetEngine:
                 if m.mid_block.attentions is not None:
                     h = self.attention(m.mid_block.attentions[0], h, ctx)
                 h = self.res_block(m.mid_block.resnets[1], [h], ctx)
+            if ctx.tape is not None:
+                ctx.mark = len(ctx.tape)
             for blk in m.up_blocks:
                 for j, r in enumerate(blk.resnets):
                     h = self.res_block(r, [h, res.pop()], ctx)
@@ -707,18 +712,55 @@ class UNetEngine:
             raise NotImplementedError("SpatialCrossAttention is not yet on the fmdiff engine")
         raise NotImplementedError(type(layer).__name__)
 
-    def backward(self, ctx: Ctx, dpred: torch.Tensor):
-        """Run the written-out backward. ``dpred``: bf16 NHWC [N,H,W,Kpad] gradient of the output."""
-        ops.gb_defer()   # GroupNorm gamma/beta folds: one batched launch at the end
-        try:
-            self._head_bwd(dpred)
-            for fn in reversed(ctx.tape):
-                fn()
-        finally:
-            ops.gb_flush()
+    def backward(self, ctx: Ctx, dpred: torch.Tensor, part: int = 0):
+        """Run the written-out backward. ``dpred``: bf16 NHWC [N,H,W,Kpad] gradient of the output.
+
+        ``part`` 1 runs the head and the decoder (tape[mark:]) and folds their GroupNorm gamma/beta, so
+        every ``decoder_params()`` gradient is final when it returns; ``part`` 2 runs the rest (middle,
+        encoder, grouped emb projections, time MLP).  A data-parallel step all-reduces the decoder's
+        gradients while part 2 runs.  ``part`` 0 = both."""
+        if part in (0, 1):
+            ops.gb_defer()   # GroupNorm gamma/beta folds: batched launches
+            try:
+                self._head_bwd(dpred)
+                for fn in reversed(ctx.tape[ctx.mark:] if part == 1 else ctx.tape):
+                    fn()
+            finally:
+                ops.gb_flush()
+            if part == 1:
+                self._join()
+                return
+        if part == 2:
+            ops.gb_defer()
+            try:
+                for fn in reversed(ctx.tape[:ctx.mark]):
+                    fn()
+            finally:
+                ops.gb_flush()
         self._join()   # every weight gradient has landed before anyone reads .grad
         ctx.tape = None
         self._head_bwd = None
+
+    def decoder_params(self) -> List[torch.nn.Parameter]:
+        """Parameters whose gradients are final after ``backward(part=1)``: the decoder blocks and the
+        output head, minus the ResBlock emb projections (their gradients come from the grouped linear
+        backward, which runs last)."""
+        m = self.m
+        mods = ([m.output_blocks, m.out] if self.kind == "efficient"
+                else [m.up_blocks, m.conv_norm_out, m.conv_out])
+        late = set()
+        if self.gl is not None:
+            for mod in mods:
+                for sub in mod.modules():
+                    if isinstance(sub, ResBlockND) and id(sub) in self.gl_slot and sub.emb_layers is not None:
+                        late.update(id(p) for p in sub.emb_layers.parameters())
+        out, seen = [], set()
+        for mod in mods:
+            for p in mod.parameters():
+                if id(p) not in late and id(p) not in seen:
+                    seen.add(id(p))
+                    out.append(p)
+        return out
 
     # ----------------------------------------------------------- utilities
     def stage_input(self, x: torch.Tensor, context: Optional[torch.Tensor]):

@@ -124,7 +124,9 @@ def test_fused_sampler_matches_plain_euler_loop(golden):
 
 def test_fused_train_step_split_capture_matches_full_graph(golden):
     """FusedTrainStep.capture(split_collectives=True) -- the multi-rank form: forward+backward graph,
-    then the (bucketed) all-reduce and AdamW issued eagerly -- reproduces the single-graph step."""
+    then the (bucketed) all-reduce and AdamW issued eagerly -- reproduces the single-graph step; so does
+    the overlapped form (decoder gradients first in the flat buffer, backward in two graphs with the
+    decoder all-reduce issued between them)."""
     from fmdiff.pipelines.train.fused import FusedTrainStep
     T, M = golden
     name = "ldct_fm_test"
@@ -132,16 +134,19 @@ def test_fused_train_step_split_capture_matches_full_graph(golden):
     x, cond = T[f"{name}/x"].to(DEV), T[f"{name}/cond"].to(DEV)
     clean = x.clamp(0, 1)
     res = []
-    for split in (False, True):
+    for split, overlap in ((False, False), (True, False), (True, True)):
         model = _build(meta).to(DEV)
         _load_seeded(model, meta)
-        tr = FusedTrainStep(model, lr=1e-3, warmup=1)
+        tr = FusedTrainStep(model, lr=1e-3, warmup=1, overlap_allreduce=overlap)
+        assert (tr.flat.split_at > 0) == overlap
         torch.manual_seed(11)
         tr.capture(clean, cond, warmup_iters=2, split_collectives=split)
         losses = [float(tr.replay().item()) for _ in range(2)]
         torch.cuda.synchronize()
-        res.append((losses, tr.flat.data.detach().clone()))
-    (la, pa), (lb, pb) = res
-    assert all(math.isfinite(v) for v in la + lb)
-    assert la == lb
-    assert torch.equal(pa, pb)
+        res.append((losses, {k: p.detach().clone() for k, p in model.named_parameters()}))
+    la, pa = res[0]
+    assert all(math.isfinite(v) for v in la)
+    for lb, pb in res[1:]:
+        assert la == lb
+        for k in pa:
+            assert torch.equal(pa[k], pb[k]), k

@@ -161,7 +161,12 @@ def _dp_worker(rank, world, port, meta, tensors, q):
                            tensors["t"][sl], meta["num_train_timesteps"])
         sc.backward()
         flat = torch.cat([p.grad.reshape(-1) for p in sd.values()])
-        dp.bucketed_allreduce(flat, buckets=3)
+        # the trainer's overlapped form: the front (decoder) part async, the rest blocking, then wait
+        k = flat.numel() // 3
+        works = dp.bucketed_allreduce_async(flat[:k], buckets=2)
+        dp.bucketed_allreduce(flat[k:], buckets=3)
+        for w in works:
+            w.wait()
         flat /= world                                                     # grad_scale folded into AdamW on GPU
         if rank == 0:
             q.put(flat)
