@@ -173,7 +173,12 @@ def main():
     trainer = FusedTrainStep(model, lr=1e-4, warmup=500, total_steps=100 * 1000, num_train_timesteps=1000)
     use_graph = not args.no_graph   # N > 1: forward + backward replayed, all-reduce + AdamW issued eagerly
     if use_graph:
-        trainer.capture(clean, ldct, warmup_iters=2)
+        try:
+            trainer.capture(clean, ldct, warmup_iters=2)
+        except RuntimeError as e:   # keep the N-rank run alive if this stack refuses the capture
+            log(f"[bench] hipGraph capture failed ({e}); running the step eagerly")
+            use_graph = False
+    if use_graph:
         run = trainer.replay
     else:
         def run():

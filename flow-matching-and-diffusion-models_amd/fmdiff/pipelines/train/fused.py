@@ -178,7 +178,10 @@ class FusedTrainStep:
                 self.step(*self._static)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # multi-rank: thread-local capture, so the process group's watchdog thread may keep querying its
+        # (already completed) events while this thread records
+        mode = "thread_local" if self._split else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             if self._split:
                 self._graph_loss = self._fwd_bwd(*self._static)
             else:
@@ -187,7 +190,7 @@ class FusedTrainStep:
         self._graph2 = None
         if self._split and self.overlap:   # the encoder backward as a second graph in the same pool
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=g.pool()):
+            with torch.cuda.graph(g2, pool=g.pool(), capture_error_mode=mode):
                 self._bwd_rest()
             self._graph2 = g2
 
@@ -250,7 +253,8 @@ class FusedFlowSampler:
         self.eng.invalidate_weights()
         self._one()   # step 0 eagerly: re-derives the bf16 weights and warms the allocator
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):   # capture records, does not execute: the counter stays at 1
+        mode = "thread_local" if torch.distributed.is_available() and torch.distributed.is_initialized() else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):   # records, does not execute: the counter stays at 1
             self._one()
         for _ in range(self.S - 1):
             g.replay()
