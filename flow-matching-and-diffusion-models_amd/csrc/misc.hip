@@ -388,6 +388,26 @@ __global__ void gather_row_kernel(const float* __restrict__ table, const int* __
   GRID_STRIDE(i, n) out[i] = src[i];
 }
 
+// out = sum_k c[k] * in[k] over n fp32 elements (k < nin <= FMD_LINCOMB_MAX): the multistep solver
+// updates (DPM-Solver++, UniPC) with their per-step scalar coefficients folded on the host
+__global__ void lincomb_kernel(const fmd_lincomb_desc D) {
+  const long long n4 = D.n / 4;
+  const bool vec = (D.n & 3) == 0;
+  if (vec) {
+    GRID_STRIDE(i, n4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < D.nin; ++k) acc += D.c[k] * ((const f32x4*)D.in[k])[i];
+      ((f32x4*)D.out)[i] = acc;
+    }
+  } else {
+    GRID_STRIDE(i, D.n) {
+      float acc = 0.f;
+      for (int k = 0; k < D.nin; ++k) acc += D.c[k] * D.in[k][i];
+      D.out[i] = acc;
+    }
+  }
+}
+
 __global__ void counter_add_kernel(int* c, int v) {
   if (threadIdx.x == 0) c[0] += v;
 }
@@ -803,6 +823,19 @@ int fmd_fill_from_table(const float* table, const int32_t* index, float* out, in
 }
 
 int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s) { LAUNCH(counter_add_kernel, 1, c, v); }
+
+int fmd_lincomb(const fmd_lincomb_desc* d, fmd_stream_t s) {
+  if (!d || !d->out || d->nin < 1 || d->nin > FMD_LINCOMB_MAX || d->n < 0) return -1;
+  for (int k = 0; k < d->nin; ++k)
+    if (!d->in[k]) return -2;
+  if ((d->n & 3) == 0) {
+    if (((size_t)d->out & 15) != 0) return -3;
+    for (int k = 0; k < d->nin; ++k)
+      if (((size_t)d->in[k] & 15) != 0) return -3;
+  }
+  if (d->n == 0) return 0;
+  LAUNCH(lincomb_kernel, grid_for((d->n & 3) == 0 ? d->n / 4 : d->n), *d);
+}
 
 int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s) {
   if (n < 1 || !table || !index || !out) return -1;

@@ -48,6 +48,14 @@ class GnApplyDesc(C.Structure):
     ]
 
 
+LINCOMB_MAX = 6   # FMD_LINCOMB_MAX
+
+
+class LincombDesc(C.Structure):
+    """Mirror of ``fmd_lincomb_desc``."""
+    _fields_ = [("out", p), ("in_", p * LINCOMB_MAX), ("c", C.c_float * LINCOMB_MAX), ("nin", i32), ("n", i64)]
+
+
 class GbJob(C.Structure):
     """Mirror of ``fmd_gb_job``."""
     _fields_ = [("ws", p), ("dgamma", p), ("dbeta", p), ("N", i32), ("C", i32)]
@@ -71,6 +79,7 @@ SIGNATURES = {
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
     "fmd_gn_gb_fold": [p, i32, p],
+    "fmd_lincomb": [C.POINTER(LincombDesc), p],
     "fmd_halo_set_workgroup": [i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],

@@ -227,3 +227,275 @@ class DDIMScheduler(DDPMScheduler):
         ops.ddpm_step(x, _nhwc_view(model_output.float()), coef, idx, None, None, None)
         out = x.to(model_output.dtype)
         return SchedulerOutput(out) if return_dict else (out,)
+
+
+# --------------------------------------------------------------------------------------------------
+# Multistep solvers: diffusers DPMSolverMultistepScheduler / UniPCMultistepScheduler protocol (called by the
+# reference at src/pipelines/utils.py:218 through SCHEDULER_REGISTRY "dpm_multistep" / "unipc", and the
+# run_model CLI aliases dpmsolver1/2/++).  Host bookkeeping (timesteps, sigmas, step index, warm-up order)
+# follows the upstream float32 / int64 / float64 types; every per-step scalar is folded on the host into
+# the coefficients of one fused device update ``out = sum_k c_k * t_k`` (fmd_lincomb) over the sample and
+# the model-output history, so a step is 2 launches (data-prediction conversion + update).
+
+
+class _MultistepBase:
+    order_max = 3
+
+    def __init__(self, num_train_timesteps, beta_start, beta_end, beta_schedule, solver_order, prediction_type,
+                 timestep_spacing, steps_offset, final_sigmas_type, use_karras_sigmas, thresholding):
+        if prediction_type != "epsilon":
+            raise NotImplementedError("fmdiff multistep solvers: epsilon prediction (the reference's DDPM models)")
+        if use_karras_sigmas or thresholding:
+            raise NotImplementedError("fmdiff multistep solvers: karras sigmas / thresholding")
+        if not 1 <= int(solver_order) <= self.order_max:
+            raise ValueError(f"solver_order {solver_order}")
+        if final_sigmas_type not in ("zero", "sigma_min"):
+            raise ValueError(final_sigmas_type)
+        N = int(num_train_timesteps)
+        self.betas = _betas(N, beta_start, beta_end, beta_schedule)
+        self.alphas_cumprod = torch.cumprod(1.0 - self.betas, dim=0)
+        self.init_noise_sigma = 1.0
+        self.timesteps = torch.from_numpy(np.linspace(0, N - 1, N, dtype=np.float32)[::-1].copy())
+        self.num_inference_steps = None
+        self._set_common()
+
+    def _set_common(self):
+        self.model_outputs = [None] * self.config.solver_order
+        self.lower_order_nums = 0
+        self._step_index = None
+
+    @property
+    def step_index(self):
+        return self._step_index
+
+    def set_timesteps(self, num_inference_steps: int, device=None):
+        N = self.config.num_train_timesteps
+        n = int(num_inference_steps)
+        sp = self.config.timestep_spacing
+        if sp == "linspace":
+            ts = np.linspace(0, N - 1, n + 1).round()[::-1][:-1].copy().astype(np.int64)
+        elif sp == "leading":
+            ts = (np.arange(0, n + 1) * (N // (n + 1))).round()[::-1][:-1].copy().astype(np.int64)
+            ts += self.config.steps_offset
+        elif sp == "trailing":
+            ts = np.arange(N, 0, -N / n).round().copy().astype(np.int64) - 1
+        else:
+            raise ValueError(sp)
+        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
+        sig = np.interp(ts, np.arange(0, len(sig)), sig)
+        last = (((1 - self.alphas_cumprod[0]) / self.alphas_cumprod[0]) ** 0.5).item() \
+            if self.config.final_sigmas_type == "sigma_min" else 0
+        self.sigmas = torch.from_numpy(np.concatenate([sig, [last]]).astype(np.float32))
+        self.timesteps = torch.from_numpy(ts).to(device=device, dtype=torch.int64) if device is not None \
+            else torch.from_numpy(ts).to(torch.int64)
+        self.num_inference_steps = len(ts)
+        self._set_common()
+
+    def _init_step_index(self, timestep):
+        cand = (self.timesteps.cpu() == int(timestep)).nonzero()
+        self._step_index = len(self.timesteps) - 1 if len(cand) == 0 else int(cand[1 if len(cand) > 1 else 0])
+
+    @staticmethod
+    def _alpha_sigma(sigma):
+        alpha_t = 1 / ((sigma ** 2 + 1) ** 0.5)
+        return alpha_t, sigma * alpha_t
+
+    def _lam(self, i):
+        a, s = self._alpha_sigma(self.sigmas[i])
+        return torch.log(a) - torch.log(s)
+
+    def _to_x0(self, eps, x):
+        """x0 = (x - sigma_t * eps) / alpha_t at the current step (fmd_lincomb)."""
+        a, s = self._alpha_sigma(self.sigmas[self._step_index])
+        return ops.lincomb(torch.empty_like(x), [x, eps], [1.0 / a, -(s / a)])
+
+    @staticmethod
+    def _prep(model_output, sample):
+        ops._need_cuda(sample, "scheduler.step")
+        return model_output.float().contiguous(), sample.float().contiguous()
+
+
+class DPMSolverMultistepScheduler(_MultistepBase):
+    """Defaults as upstream: solver_order 2, dpmsolver++, midpoint, lower_order_final, final_sigmas_type
+    zero (rejected for algorithm_type dpmsolver, like upstream), linspace spacing."""
+
+    def __init__(self, num_train_timesteps: int = 1000, beta_start: float = 0.0001, beta_end: float = 0.02,
+                 beta_schedule: str = "linear", solver_order: int = 2, prediction_type: str = "epsilon",
+                 algorithm_type: str = "dpmsolver++", solver_type: str = "midpoint", lower_order_final: bool = True,
+                 euler_at_final: bool = False, use_karras_sigmas: bool = False, final_sigmas_type: str = "zero",
+                 timestep_spacing: str = "linspace", steps_offset: int = 0, thresholding: bool = False,
+                 **_unused):
+        if algorithm_type not in ("dpmsolver++", "dpmsolver"):
+            raise NotImplementedError(f"fmdiff DPM-Solver: algorithm_type {algorithm_type}")
+        if solver_type not in ("midpoint", "heun"):
+            raise ValueError(solver_type)
+        if algorithm_type == "dpmsolver" and final_sigmas_type == "zero":
+            raise ValueError(f"`final_sigmas_type` {final_sigmas_type} is not supported for `algorithm_type` "
+                             f"{algorithm_type}. Please choose `sigma_min` instead.")
+        self.config = _flat_cfg(num_train_timesteps=int(num_train_timesteps), beta_start=beta_start,
+                                beta_end=beta_end, beta_schedule=beta_schedule, solver_order=int(solver_order),
+                                prediction_type=prediction_type, algorithm_type=algorithm_type,
+                                solver_type=solver_type, lower_order_final=lower_order_final,
+                                euler_at_final=euler_at_final, final_sigmas_type=final_sigmas_type,
+                                timestep_spacing=timestep_spacing, steps_offset=steps_offset)
+        super().__init__(num_train_timesteps, beta_start, beta_end, beta_schedule, solver_order, prediction_type,
+                         timestep_spacing, steps_offset, final_sigmas_type, use_karras_sigmas, thresholding)
+
+    def _coefs(self, order):
+        """(coefficient of the sample, [coefficients of model_outputs[-1], [-2], [-3]]) of one update."""
+        i = self._step_index
+        pp = self.config.algorithm_type == "dpmsolver++"
+        heun = self.config.solver_type == "heun"
+        a_t, s_t = self._alpha_sigma(self.sigmas[i + 1])
+        a_0, s_0 = self._alpha_sigma(self.sigmas[i])
+        h = self._lam(i + 1) - self._lam(i)
+        cx = s_t / s_0 if pp else a_t / a_0
+        c0 = -(a_t * (torch.exp(-h) - 1.0)) if pp else -(s_t * (torch.exp(h) - 1.0))
+        if order == 1:
+            return cx, [c0]
+        if pp:
+            cd1 = (a_t * ((torch.exp(-h) - 1.0) / h + 1.0)) if heun else -0.5 * (a_t * (torch.exp(-h) - 1.0))
+        else:
+            cd1 = -(s_t * ((torch.exp(h) - 1.0) / h - 1.0)) if heun else -0.5 * (s_t * (torch.exp(h) - 1.0))
+        h_0 = self._lam(i) - self._lam(i - 1)
+        r0 = h_0 / h
+        if order == 2:   # D1 = (m0 - m1) / r0
+            return cx, [c0 + cd1 / r0, -cd1 / r0]
+        # third order: D1 = D1_0 + r0/(r0+r1) (D1_0 - D1_1), D2 = (D1_0 - D1_1)/(r0+r1)
+        cd1 = (a_t * ((torch.exp(-h) - 1.0) / h + 1.0)) if pp else -(s_t * ((torch.exp(h) - 1.0) / h - 1.0))
+        cd2 = (-(a_t * ((torch.exp(-h) - 1.0 + h) / h ** 2 - 0.5)) if pp
+               else -(s_t * ((torch.exp(h) - 1.0 - h) / h ** 2 - 0.5)))
+        r1 = (self._lam(i - 1) - self._lam(i - 2)) / h
+        k = r0 / (r0 + r1)
+        # D1_0 = (m0 - m1)/r0, D1_1 = (m1 - m2)/r1
+        d10 = [1.0 / r0, -1.0 / r0, 0.0]
+        d11 = [0.0, 1.0 / r1, -1.0 / r1]
+        diff = [x - y for x, y in zip(d10, d11)]
+        d1 = [x + k * y for x, y in zip(d10, diff)]
+        d2 = [y / (r0 + r1) for y in diff]
+        return cx, [c0 + cd1 * d1[0] + cd2 * d2[0], cd1 * d1[1] + cd2 * d2[1], cd1 * d1[2] + cd2 * d2[2]]
+
+    def step(self, model_output, timestep, sample, generator=None, variance_noise=None, return_dict: bool = True,
+             **_kw):
+        eps, x = self._prep(model_output, sample)
+        if self._step_index is None:
+            self._init_step_index(timestep)
+        n = len(self.timesteps)
+        i = self._step_index
+        lof = i == n - 1 and (self.config.euler_at_final or (self.config.lower_order_final and n < 15)
+                              or self.config.final_sigmas_type == "zero")
+        los = i == n - 2 and self.config.lower_order_final and n < 15
+        m = self._to_x0(eps, x) if self.config.algorithm_type == "dpmsolver++" else eps.clone()
+        self.model_outputs = self.model_outputs[1:] + [m]
+        if self.config.solver_order == 1 or self.lower_order_nums < 1 or lof:
+            order = 1
+        elif self.config.solver_order == 2 or self.lower_order_nums < 2 or los:
+            order = 2
+        else:
+            order = 3
+        cx, cm = self._coefs(order)
+        hist = [self.model_outputs[-1 - k] for k in range(order)]
+        prev = ops.lincomb(torch.empty_like(x), [x] + hist, [cx] + cm)
+        if self.lower_order_nums < self.config.solver_order:
+            self.lower_order_nums += 1
+        self._step_index += 1
+        out = prev.to(model_output.dtype)
+        return SchedulerOutput(out) if return_dict else (out,)
+
+
+class UniPCMultistepScheduler(_MultistepBase):
+    """Defaults as upstream: solver_order 2, bh2, predict_x0, lower_order_final, corrector on every step after
+    the first (disable_corrector = []), final_sigmas_type zero, linspace spacing."""
+
+    def __init__(self, num_train_timesteps: int = 1000, beta_start: float = 0.0001, beta_end: float = 0.02,
+                 beta_schedule: str = "linear", solver_order: int = 2, prediction_type: str = "epsilon",
+                 predict_x0: bool = True, solver_type: str = "bh2", lower_order_final: bool = True,
+                 disable_corrector=(), use_karras_sigmas: bool = False, timestep_spacing: str = "linspace",
+                 steps_offset: int = 0, final_sigmas_type: str = "zero", thresholding: bool = False, **_unused):
+        if not predict_x0:
+            raise NotImplementedError("fmdiff UniPC: predict_x0 (upstream default)")
+        if solver_type not in ("bh1", "bh2"):
+            raise ValueError(solver_type)
+        self.config = _flat_cfg(num_train_timesteps=int(num_train_timesteps), beta_start=beta_start,
+                                beta_end=beta_end, beta_schedule=beta_schedule, solver_order=int(solver_order),
+                                prediction_type=prediction_type, predict_x0=predict_x0, solver_type=solver_type,
+                                lower_order_final=lower_order_final, disable_corrector=list(disable_corrector),
+                                timestep_spacing=timestep_spacing, steps_offset=steps_offset,
+                                final_sigmas_type=final_sigmas_type)
+        super().__init__(num_train_timesteps, beta_start, beta_end, beta_schedule, solver_order, prediction_type,
+                         timestep_spacing, steps_offset, final_sigmas_type, use_karras_sigmas, thresholding)
+
+    def _set_common(self):
+        super()._set_common()
+        self.last_sample = None
+        self.this_order = None
+
+    def _rb(self, h, rks, order):
+        hh = -h
+        h_phi_1 = torch.expm1(hh)
+        h_phi_k = h_phi_1 / hh - 1
+        fact = 1
+        B_h = hh if self.config.solver_type == "bh1" else torch.expm1(hh)
+        R, b = [], []
+        for i in range(1, order + 1):
+            R.append(torch.pow(rks, i - 1))
+            b.append(h_phi_k * fact / B_h)
+            fact *= i + 1
+            h_phi_k = h_phi_k / hh - 1 / fact
+        return torch.stack(R), torch.tensor(b), h_phi_1, B_h
+
+    def _update(self, corrector: bool, order: int):
+        """Coefficients of x, model_outputs[-1], [-2], ..., (and model_t for the corrector)."""
+        i = self._step_index
+        it, i0 = (i, i - 1) if corrector else (i + 1, i)
+        a_t, s_t = self._alpha_sigma(self.sigmas[it])
+        a_0, s_0 = self._alpha_sigma(self.sigmas[i0])
+        l_0 = self._lam(i0)
+        h = self._lam(it) - l_0
+        rks = [(self._lam(i0 - k) - l_0) / h for k in range(1, order)]
+        R, b, h_phi_1, B_h = self._rb(h, torch.tensor(rks + [1.0]), order)
+        cx = s_t / s_0
+        cm = [-(a_t * h_phi_1)] + [0.0] * (order - 1)
+        if corrector:
+            rhos = torch.tensor([0.5]) if order == 1 else torch.linalg.solve(R, b)
+            lin = rhos[:-1]
+        else:
+            rhos = None
+            lin = (torch.tensor([0.5]) if order == 2 else torch.linalg.solve(R[:-1, :-1], b[:-1])) \
+                if order > 1 else torch.tensor([])
+        # x_t -= a_t B_h * (sum_k lin_k (m_k - m0) / rk  [+ rho_last (model_t - m0)])
+        g = a_t * B_h
+        for k in range(1, order):
+            w = lin[k - 1] / rks[k - 1]
+            cm[k] = cm[k] - g * w
+            cm[0] = cm[0] + g * w
+        cmt = None
+        if corrector:
+            cmt = -(g * rhos[-1])
+            cm[0] = cm[0] + g * rhos[-1]
+        return cx, cm, cmt
+
+    def step(self, model_output, timestep, sample, return_dict: bool = True, generator=None, **_kw):
+        eps, x = self._prep(model_output, sample)
+        if self._step_index is None:
+            self._init_step_index(timestep)
+        m = self._to_x0(eps, x)
+        i = self._step_index
+        if i > 0 and (i - 1) not in self.config.disable_corrector and self.last_sample is not None:
+            cx, cm, cmt = self._update(True, self.this_order)
+            hist = [self.model_outputs[-1 - k] for k in range(self.this_order)]
+            x = ops.lincomb(torch.empty_like(x), [self.last_sample] + hist + [m], [cx] + cm + [cmt])
+        self.model_outputs = self.model_outputs[1:] + [m]
+        n = len(self.timesteps)
+        order = min(self.config.solver_order, n - i) if self.config.lower_order_final else self.config.solver_order
+        self.this_order = min(order, self.lower_order_nums + 1)
+        self.last_sample = x
+        cx, cm, _ = self._update(False, self.this_order)
+        hist = [self.model_outputs[-1 - k] for k in range(self.this_order)]
+        prev = ops.lincomb(torch.empty_like(x), [x] + hist, [cx] + cm)
+        if self.lower_order_nums < self.config.solver_order:
+            self.lower_order_nums += 1
+        self._step_index += 1
+        out = prev.to(model_output.dtype)
+        return SchedulerOutput(out) if return_dict else (out,)
+

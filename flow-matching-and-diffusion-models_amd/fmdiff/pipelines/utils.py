@@ -19,7 +19,8 @@ from typing import Dict, Tuple
 
 import torch
 
-from .schedulers import DDIMScheduler, DDPMScheduler, FlowMatchEulerDiscreteScheduler
+from .schedulers import (DDIMScheduler, DDPMScheduler, DPMSolverMultistepScheduler,
+                         FlowMatchEulerDiscreteScheduler, UniPCMultistepScheduler)
 
 
 class _NotBuiltScheduler:
@@ -30,23 +31,8 @@ class _NotBuiltScheduler:
         raise NotImplementedError(f"scheduler '{self.name}' has no HIP step implementation in fmdiff yet")
 
 
-class DPMSolverMultistepScheduler(_NotBuiltScheduler):
-    name = "dpm_multistep"
-
-    def __init__(self, num_train_timesteps: int = 1000, solver_order: int = 2, algorithm_type: str = "dpmsolver++",
-                 **params):
-        super().__init__(num_train_timesteps)
-
-
 class DPMSolverSDEScheduler(_NotBuiltScheduler):
-    name = "dpm_sde"
-
-
-class UniPCMultistepScheduler(_NotBuiltScheduler):
-    name = "unipc"
-
-    def __init__(self, num_train_timesteps: int = 1000, solver_order: int = 2, **params):
-        super().__init__(num_train_timesteps)
+    name = "dpm_sde"   # Brownian-tree SDE sampler (torchsde upstream): not on the BASELINE configs
 
 
 SCHEDULER_REGISTRY: Dict[str, type] = {

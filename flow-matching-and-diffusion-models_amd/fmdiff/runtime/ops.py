@@ -535,6 +535,22 @@ def fill_from_table(table, index, out):
     _lib.call("fmd_fill_from_table", _p(table), _p(index), _p(out), out.numel(), stream())
 
 
+def lincomb(out, inputs, coefs):
+    """out = sum_k coefs[k] * inputs[k] (fp32 device tensors of out's size; out may be one of the inputs)."""
+    _need_cuda(out, "lincomb")
+    if not 1 <= len(inputs) <= _lib.LINCOMB_MAX or len(inputs) != len(coefs):
+        raise ValueError("lincomb: 1..6 inputs, one coefficient each")
+    d = _lib.LincombDesc()
+    d.out, d.nin, d.n = _p(out), len(inputs), out.numel()
+    for k, (t, c) in enumerate(zip(inputs, coefs)):
+        if t.dtype != F32 or not t.is_contiguous() or t.numel() != out.numel():
+            raise ValueError("lincomb: contiguous fp32 inputs of the output's size")
+        d.in_[k] = _p(t)
+        d.c[k] = float(c)
+    _lib.call("fmd_lincomb", C.byref(d), stream())
+    return out
+
+
 def gather_row(table, index, out):
     """out = table[index[0]] (row of ``out.numel()`` fp32 elements; ``index`` is a device int32 counter)."""
     _lib.call("fmd_gather_row", _p(table), _p(index), out.numel(), _p(out), stream())

@@ -263,6 +263,18 @@ int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, c
                   const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
                   void* next, fmd_stream_t s);
 int fmd_fill_from_table(const float* table, const int32_t* index, float* out, int32_t N, fmd_stream_t s);
+/* out = sum_k c[k] * in[k] over n fp32 elements: the multistep scheduler updates (DPM-Solver / UniPC,
+ * replaces diffusers' DPMSolverMultistepScheduler.step / UniPCMultistepScheduler.step tensor arithmetic,
+ * called at src/pipelines/utils.py:218).  out may alias an input.  n % 4 == 0 needs 16-byte alignment. */
+#define FMD_LINCOMB_MAX 6
+typedef struct {
+  float* out;
+  const float* in[FMD_LINCOMB_MAX];
+  float c[FMD_LINCOMB_MAX];
+  int32_t nin;
+  int64_t n;
+} fmd_lincomb_desc;
+int fmd_lincomb(const fmd_lincomb_desc* d, fmd_stream_t s);
 /* out[0:n] = table[index[0]*n : (index[0]+1)*n] -- a per-step row (e.g. precomputed time embeddings of a
  * sampling schedule) selected by a device-side step counter, so the step stays graph-replayable. */
 int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s);

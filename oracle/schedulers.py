@@ -4,7 +4,8 @@ The reference calls third-party ``diffusers`` schedulers
 (``src/pipelines/utils.py:13-30``; ``requirements.txt:18`` pins only
 ``diffusers>=0.24.0``).  diffusers is not installed offline, so this is a
 restatement of its published algorithms (FlowMatchEulerDiscreteScheduler,
-DDPMScheduler, DDIMScheduler with their default constructor arguments),
+DDPMScheduler, DDIMScheduler, DPMSolverMultistepScheduler, UniPCMultistepScheduler with their default
+constructor arguments),
 pinned only by the closed-form known-answer values in SURVEY.md Appendix B /
 8(c): **parity unpinned** beyond those KATs.
 
@@ -186,6 +187,240 @@ class DDIM(DDPM):
         if eta > 0:
             prev = prev + std * (noise if noise is not None else torch.randn_like(eps))
         return StepOut(prev)
+
+
+# --------------------------------------------------------------------------------------------------
+# Multistep solvers (diffusers DPMSolverMultistepScheduler / UniPCMultistepScheduler, default constructor
+# arguments: linspace spacing, final_sigmas_type "zero", lower_order_final, epsilon prediction; no
+# thresholding, karras or lu-lambda sigmas).  Restated from the published algorithms (DPM-Solver++,
+# arXiv:2211.01095 multistep update; UniPC, arXiv:2302.04867 B(h) predictor/corrector); parity unpinned.
+
+
+class _SigmaSchedule:
+    def _init_sched(self, N, beta_start, beta_end, beta_schedule, order, final_sigmas_type="zero"):
+        self.N = int(N)
+        self.final_sigmas_type = final_sigmas_type
+        self.betas = _betas(self.N, beta_start, beta_end, beta_schedule)
+        self.alphas_cumprod = torch.cumprod(1.0 - self.betas, dim=0)
+        self.order = int(order)
+        self.timesteps = None
+        self.sigmas = None
+
+    def set_timesteps(self, n, spacing="linspace", steps_offset=0):
+        N = self.N
+        if spacing == "linspace":
+            ts = np.linspace(0, N - 1, n + 1).round()[::-1][:-1].copy().astype(np.int64)
+        elif spacing == "leading":
+            r = N // (n + 1)
+            ts = (np.arange(0, n + 1) * r).round()[::-1][:-1].copy().astype(np.int64) + steps_offset
+        elif spacing == "trailing":
+            r = N / n
+            ts = np.arange(N, 0, -r).round().copy().astype(np.int64) - 1
+        else:
+            raise ValueError(spacing)
+        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
+        last = (((1 - self.alphas_cumprod[0]) / self.alphas_cumprod[0]) ** 0.5).item() \
+            if self.final_sigmas_type == "sigma_min" else 0
+        sig = np.interp(ts, np.arange(0, len(sig)), sig)
+        self.sigmas = torch.from_numpy(np.concatenate([sig, [last]]).astype(np.float32))
+        self.timesteps = torch.from_numpy(ts).to(torch.int64)
+        self.model_outputs = [None] * self.order
+        self.lower_order_nums = 0
+        self.step_index = None
+
+    @staticmethod
+    def alpha_sigma(sigma):
+        alpha_t = 1 / ((sigma ** 2 + 1) ** 0.5)
+        return alpha_t, sigma * alpha_t
+
+    def lam(self, i):
+        a, s = self.alpha_sigma(self.sigmas[i])
+        return torch.log(a) - torch.log(s)
+
+    def init_index(self, t):
+        cand = (self.timesteps == int(t)).nonzero()
+        if len(cand) == 0:
+            self.step_index = len(self.timesteps) - 1
+        else:
+            self.step_index = int(cand[1 if len(cand) > 1 else 0])
+
+    def to_x0(self, eps, x):
+        a, s = self.alpha_sigma(self.sigmas[self.step_index])
+        return (x - s * eps) / a
+
+
+class DPMSolverMultistep(_SigmaSchedule):
+    """DPMSolverMultistepScheduler: algorithm dpmsolver++ | dpmsolver, solver_order 1 | 2 | 3, solver_type
+    midpoint | heun, lower_order_final."""
+
+    def __init__(self, num_train_timesteps=1000, beta_start=0.0001, beta_end=0.02, beta_schedule="linear",
+                 solver_order=2, algorithm_type="dpmsolver++", solver_type="midpoint", lower_order_final=True,
+                 final_sigmas_type="zero"):
+        if algorithm_type == "dpmsolver" and final_sigmas_type == "zero":
+            raise ValueError("final_sigmas_type zero is not supported for algorithm_type dpmsolver")
+        self._init_sched(num_train_timesteps, beta_start, beta_end, beta_schedule, solver_order, final_sigmas_type)
+        self.algo = algorithm_type
+        self.solver_type = solver_type
+        self.lower_order_final = lower_order_final
+
+    def first(self, m, x):
+        i = self.step_index
+        a_t, s_t = self.alpha_sigma(self.sigmas[i + 1])
+        a_s, s_s = self.alpha_sigma(self.sigmas[i])
+        h = (torch.log(a_t) - torch.log(s_t)) - (torch.log(a_s) - torch.log(s_s))
+        if self.algo == "dpmsolver++":
+            return (s_t / s_s) * x - (a_t * (torch.exp(-h) - 1.0)) * m
+        return (a_t / a_s) * x - (s_t * (torch.exp(h) - 1.0)) * m
+
+    def second(self, x):
+        i = self.step_index
+        a_t, s_t = self.alpha_sigma(self.sigmas[i + 1])
+        a_0, s_0 = self.alpha_sigma(self.sigmas[i])
+        l_t, l_0, l_1 = self.lam(i + 1), self.lam(i), self.lam(i - 1)
+        m0, m1 = self.model_outputs[-1], self.model_outputs[-2]
+        h, h_0 = l_t - l_0, l_0 - l_1
+        r0 = h_0 / h
+        D0, D1 = m0, (1.0 / r0) * (m0 - m1)
+        if self.algo == "dpmsolver++":
+            if self.solver_type == "midpoint":
+                return ((s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * D0
+                        - 0.5 * (a_t * (torch.exp(-h) - 1.0)) * D1)
+            return ((s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * D0
+                    + (a_t * ((torch.exp(-h) - 1.0) / h + 1.0)) * D1)
+        if self.solver_type == "midpoint":
+            return ((a_t / a_0) * x - (s_t * (torch.exp(h) - 1.0)) * D0
+                    - 0.5 * (s_t * (torch.exp(h) - 1.0)) * D1)
+        return ((a_t / a_0) * x - (s_t * (torch.exp(h) - 1.0)) * D0
+                - (s_t * ((torch.exp(h) - 1.0) / h - 1.0)) * D1)
+
+    def third(self, x):
+        i = self.step_index
+        a_t, s_t = self.alpha_sigma(self.sigmas[i + 1])
+        a_0, s_0 = self.alpha_sigma(self.sigmas[i])
+        l_t, l_0, l_1, l_2 = self.lam(i + 1), self.lam(i), self.lam(i - 1), self.lam(i - 2)
+        m0, m1, m2 = self.model_outputs[-1], self.model_outputs[-2], self.model_outputs[-3]
+        h, h_0, h_1 = l_t - l_0, l_0 - l_1, l_1 - l_2
+        r0, r1 = h_0 / h, h_1 / h
+        D0 = m0
+        D1_0, D1_1 = (1.0 / r0) * (m0 - m1), (1.0 / r1) * (m1 - m2)
+        D1 = D1_0 + (r0 / (r0 + r1)) * (D1_0 - D1_1)
+        D2 = (1.0 / (r0 + r1)) * (D1_0 - D1_1)
+        if self.algo == "dpmsolver++":
+            return ((s_t / s_0) * x - (a_t * (torch.exp(-h) - 1.0)) * D0
+                    + (a_t * ((torch.exp(-h) - 1.0) / h + 1.0)) * D1
+                    - (a_t * ((torch.exp(-h) - 1.0 + h) / h ** 2 - 0.5)) * D2)
+        return ((a_t / a_0) * x - (s_t * (torch.exp(h) - 1.0)) * D0
+                - (s_t * ((torch.exp(h) - 1.0) / h - 1.0)) * D1
+                - (s_t * ((torch.exp(h) - 1.0 - h) / h ** 2 - 0.5)) * D2)
+
+    def step(self, eps, t, x):
+        if self.step_index is None:
+            self.init_index(t)
+        n = len(self.timesteps)
+        lof = self.step_index == n - 1 and (self.final_sigmas_type == "zero" or (self.lower_order_final and n < 15))
+        los = self.step_index == n - 2 and self.lower_order_final and n < 15
+        m = self.to_x0(eps, x) if self.algo == "dpmsolver++" else eps
+        self.model_outputs = self.model_outputs[1:] + [m]
+        x = x.to(torch.float32)
+        if self.order == 1 or self.lower_order_nums < 1 or lof:
+            prev = self.first(m, x)
+        elif self.order == 2 or self.lower_order_nums < 2 or los:
+            prev = self.second(x)
+        else:
+            prev = self.third(x)
+        if self.lower_order_nums < self.order:
+            self.lower_order_nums += 1
+        self.step_index += 1
+        return StepOut(prev.to(eps.dtype))
+
+
+class UniPCMultistep(_SigmaSchedule):
+    """UniPCMultistepScheduler: predict_x0, solver_type bh1 | bh2, solver_order 1..3, corrector on every
+    step after the first, lower_order_final."""
+
+    def __init__(self, num_train_timesteps=1000, beta_start=0.0001, beta_end=0.02, beta_schedule="linear",
+                 solver_order=2, solver_type="bh2", lower_order_final=True, final_sigmas_type="zero"):
+        self._init_sched(num_train_timesteps, beta_start, beta_end, beta_schedule, solver_order, final_sigmas_type)
+        self.solver_type = solver_type
+        self.lower_order_final = lower_order_final
+
+    def set_timesteps(self, n, spacing="linspace", steps_offset=0):
+        super().set_timesteps(n, spacing, steps_offset)
+        self.last_sample = None
+        self.this_order = None
+
+    def _rb(self, h, rks, order):
+        hh = -h
+        h_phi_1 = torch.expm1(hh)
+        h_phi_k = h_phi_1 / hh - 1
+        fact = 1
+        B_h = hh if self.solver_type == "bh1" else torch.expm1(hh)
+        R, b = [], []
+        for i in range(1, order + 1):
+            R.append(torch.pow(rks, i - 1))
+            b.append(h_phi_k * fact / B_h)
+            fact *= i + 1
+            h_phi_k = h_phi_k / hh - 1 / fact
+        return torch.stack(R), torch.tensor(b), h_phi_1, B_h
+
+    def predictor(self, x, order):
+        i = self.step_index
+        m0 = self.model_outputs[-1]
+        a_t, s_t = self.alpha_sigma(self.sigmas[i + 1])
+        a_0, s_0 = self.alpha_sigma(self.sigmas[i])
+        l_0 = self.lam(i)
+        h = self.lam(i + 1) - l_0
+        rks, D1s = [], []
+        for k in range(1, order):
+            mi = self.model_outputs[-(k + 1)]
+            rk = (self.lam(i - k) - l_0) / h
+            rks.append(rk)
+            D1s.append((mi - m0) / rk)
+        rks.append(1.0)
+        R, b, h_phi_1, B_h = self._rb(h, torch.tensor(rks), order)
+        x_t_ = s_t / s_0 * x - a_t * h_phi_1 * m0
+        if D1s:
+            rhos = torch.tensor([0.5]) if order == 2 else torch.linalg.solve(R[:-1, :-1], b[:-1])
+            pred_res = sum(rhos[k] * D1s[k] for k in range(len(D1s)))
+            return x_t_ - a_t * B_h * pred_res
+        return x_t_
+
+    def corrector(self, model_t, x, order):
+        i = self.step_index
+        m0 = self.model_outputs[-1]
+        a_t, s_t = self.alpha_sigma(self.sigmas[i])
+        a_0, s_0 = self.alpha_sigma(self.sigmas[i - 1])
+        l_0 = self.lam(i - 1)
+        h = self.lam(i) - l_0
+        rks, D1s = [], []
+        for k in range(1, order):
+            mi = self.model_outputs[-(k + 1)]
+            rk = (self.lam(i - (k + 1)) - l_0) / h
+            rks.append(rk)
+            D1s.append((mi - m0) / rk)
+        rks.append(1.0)
+        R, b, h_phi_1, B_h = self._rb(h, torch.tensor(rks), order)
+        rhos = torch.tensor([0.5]) if order == 1 else torch.linalg.solve(R, b)
+        x_t_ = s_t / s_0 * x - a_t * h_phi_1 * m0
+        corr = sum(rhos[k] * D1s[k] for k in range(len(D1s))) if D1s else 0
+        return x_t_ - a_t * B_h * (corr + rhos[-1] * (model_t - m0))
+
+    def step(self, eps, t, x):
+        if self.step_index is None:
+            self.init_index(t)
+        m = self.to_x0(eps, x)
+        if self.step_index > 0 and self.last_sample is not None:
+            x = self.corrector(m, self.last_sample, self.this_order)
+        self.model_outputs = self.model_outputs[1:] + [m]
+        n = len(self.timesteps)
+        order = min(self.order, n - self.step_index) if self.lower_order_final else self.order
+        self.this_order = min(order, self.lower_order_nums + 1)
+        self.last_sample = x
+        prev = self.predictor(x, self.this_order)
+        if self.lower_order_nums < self.order:
+            self.lower_order_nums += 1
+        self.step_index += 1
+        return StepOut(prev.to(eps.dtype))
 
 
 def cosine_with_warmup(step: int, warmup: int, total: int, num_cycles: float = 0.5) -> float:

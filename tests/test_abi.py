@@ -46,7 +46,8 @@ def test_struct_mirrors_match_header_field_order():
     from fmdiff import _lib
     src = open(HEADER).read()
     for cname, py in (("fmd_conv_desc", _lib.ConvDesc), ("fmd_wgrad_desc", _lib.WgradDesc),
-                      ("fmd_gn_apply_desc", _lib.GnApplyDesc), ("fmd_gb_job", _lib.GbJob)):
+                      ("fmd_gn_apply_desc", _lib.GnApplyDesc), ("fmd_gb_job", _lib.GbJob),
+                      ("fmd_lincomb_desc", _lib.LincombDesc)):
         m = re.search(r"typedef\s+struct\s*(?:\w+\s*)?\{([^{}]*)\}\s*" + cname + r"\s*;", src, flags=re.S)
         assert m, cname
         body = re.sub(r"/\*.*?\*/", "", m.group(1), flags=re.S)
@@ -54,8 +55,8 @@ def test_struct_mirrors_match_header_field_order():
         fields = []
         for decl in body.split(";"):
             parts = [p for p in decl.strip().split(",") if p.strip()]
-            fields += [re.findall(r"[A-Za-z_]\w*", p)[-1] for p in parts]
-        assert fields == [f for f, _ in py._fields_], cname
+            fields += [re.findall(r"[A-Za-z_]\w*", re.sub(r"\[[^\]]*\]", "", p))[-1] for p in parts]
+        assert fields == [f.rstrip("_") for f, _ in py._fields_], cname
 
 
 def test_product_path_has_no_cpu_fallback():

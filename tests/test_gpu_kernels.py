@@ -613,3 +613,36 @@ def test_halo_workgroup_256_matches_512(case):
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1].slab, outs[1][1].slab)
+
+
+@pytest.mark.parametrize("kind,order,variant,betas", [
+    ("dpm", 1, "dpmsolver++", "default"), ("dpm", 2, "dpmsolver++", "default"), ("dpm", 3, "dpmsolver++", "ldct"),
+    ("dpm", 2, "heun", "default"), ("dpm", 2, "dpmsolver", "ldct"), ("unipc", 1, "bh2", "default"),
+    ("unipc", 2, "bh2", "ldct"), ("unipc", 3, "bh2", "default"), ("unipc", 2, "bh1", "default")])
+def test_multistep_schedulers_vs_oracle(kind, order, variant, betas):
+    """DPMSolverMultistepScheduler / UniPCMultistepScheduler (host coefficients + fmd_lincomb) vs the CPU
+    restatement in oracle/schedulers.py over a 12-step loop with arbitrary model outputs.  ldct betas =
+    configs/diffusion/ldct_ddpm.json (linear 0.00085 -> 0.012).  Tolerance 1e-5 relative (fp32 with the
+    scalar products folded in a different order)."""
+    from oracle import schedulers as OS
+    from fmdiff.pipelines.schedulers import DPMSolverMultistepScheduler, UniPCMultistepScheduler
+    bk = dict(beta_start=0.00085, beta_end=0.012) if betas == "ldct" else {}
+    if kind == "dpm":
+        algo = "dpmsolver" if variant == "dpmsolver" else "dpmsolver++"
+        kw = dict(solver_order=order, algorithm_type=algo, final_sigmas_type="sigma_min" if algo == "dpmsolver"
+                  else "zero", solver_type="heun" if variant == "heun" else "midpoint", **bk)
+        ref, got = OS.DPMSolverMultistep(1000, **kw), DPMSolverMultistepScheduler(1000, **kw)
+    else:
+        kw = dict(solver_order=order, solver_type=variant, **bk)
+        ref, got = OS.UniPCMultistep(1000, **kw), UniPCMultistepScheduler(1000, **kw)
+    ref.set_timesteps(12)
+    got.set_timesteps(12)
+    g = torch.Generator().manual_seed(4)
+    xr = torch.randn(2, 1, 16, 16, generator=g)
+    xg = xr.clone().to(DEV)
+    for t in ref.timesteps:
+        eps = torch.randn(2, 1, 16, 16, generator=g) * 0.8 + 0.1 * xr
+        xr = ref.step(eps, t, xr).prev_sample
+        xg = got.step(eps.to(DEV), t, xg).prev_sample
+        torch.testing.assert_close(xg.cpu(), xr, rtol=1e-5, atol=1e-5 * xr.abs().max().item())
+

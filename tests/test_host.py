@@ -72,6 +72,51 @@ def test_beta_schedules(sched):
 
 
 # ------------------------------------------------------------------ registry / loop host logic
+@pytest.mark.parametrize("kind,order,variant", [
+    ("dpm", 1, "dpmsolver++"), ("dpm", 2, "dpmsolver++"), ("dpm", 3, "dpmsolver++"), ("dpm", 2, "heun"),
+    ("dpm", 2, "dpmsolver"), ("dpm", 3, "dpmsolver"), ("unipc", 1, "bh2"), ("unipc", 2, "bh2"),
+    ("unipc", 3, "bh2"), ("unipc", 2, "bh1")])
+def test_multistep_oracle_follows_exact_denoiser(kind, order, variant):
+    """KAT for the restated DPM-Solver(++) / UniPC (parity otherwise unpinned: diffusers is absent): fed the
+    exact epsilon of a fixed x0, every solver order integrates the probability-flow ODE exactly, so the final
+    sample is alpha_T x0 + sigma_T eps0 (eps0 = the initial noise) to fp32 rounding."""
+    from oracle import schedulers as OS
+    if kind == "dpm":
+        algo = "dpmsolver" if variant == "dpmsolver" else "dpmsolver++"
+        fs = "sigma_min" if algo == "dpmsolver" else "zero"
+        sch = OS.DPMSolverMultistep(solver_order=order, algorithm_type=algo, final_sigmas_type=fs,
+                                    solver_type="heun" if variant == "heun" else "midpoint")
+    else:
+        sch = OS.UniPCMultistep(solver_order=order, solver_type=variant)
+    sch.set_timesteps(20)
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.rand(2, 1, 4, 4, generator=g) * 2 - 1
+    e0 = torch.randn(2, 1, 4, 4, generator=g)
+    a, sg = sch.alpha_sigma(sch.sigmas[0])
+    x = a * x0 + sg * e0
+    for i, t in enumerate(sch.timesteps):
+        a, sg = sch.alpha_sigma(sch.sigmas[i])
+        x = sch.step((x - a * x0) / sg, t, x).prev_sample
+    a, sg = sch.alpha_sigma(sch.sigmas[-1])
+    assert (x - (a * x0 + sg * e0)).abs().max().item() < 2e-6
+
+
+def test_multistep_timesteps_kat():
+    """linspace spacing (upstream default) for 50 steps over 1000: 999, 979, ..., 20; final sigma 0."""
+    from oracle import schedulers as OS
+    from fmdiff.pipelines.schedulers import DPMSolverMultistepScheduler, UniPCMultistepScheduler
+    o = OS.DPMSolverMultistep()
+    o.set_timesteps(50)
+    assert o.timesteps[:3].tolist() == [999, 979, 959] and o.timesteps[-1].item() == 20
+    assert o.sigmas[-1].item() == 0.0 and len(o.sigmas) == 51
+    for cls in (DPMSolverMultistepScheduler, UniPCMultistepScheduler):
+        sch = cls(1000)
+        sch.set_timesteps(50)
+        assert torch.equal(sch.timesteps, o.timesteps) and torch.equal(sch.sigmas, o.sigmas)
+    with pytest.raises(ValueError):
+        DPMSolverMultistepScheduler(1000, algorithm_type="dpmsolver")   # final_sigmas_type zero, like upstream
+
+
 def test_build_scheduler_and_overrides():
     s, n = PU.build_scheduler({"name": "flow_match_euler", "params": {"shift": 1.0, "bogus": 3}}, {})
     assert isinstance(s, FS.FlowMatchEulerDiscreteScheduler) and n == 1000
