@@ -70,7 +70,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   const int kk0 = split * per_split;
   const int kk1 = min(nkt, kk0 + per_split);
   const int Wq = A.par ? d.Wo >> 1 : d.Wo;
-  const int HWq = A.par ? (d.Ho >> 1) * Wq : d.Ho * d.Wo;
+  const int Dz = d.Do > 0 ? d.Do : 1;                       // output depth (3-D problems), 1 in 2-D
+  const int HWq = A.par ? (d.Ho >> 1) * Wq : Dz * d.Ho * d.Wo;
   // pixel index of the layout (output tensor / split-K slab) for tile pixel p
   auto pmap = [&](int p) -> int {
     if (!A.par) return p;
@@ -78,26 +79,30 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
     return (n * d.Ho + 2 * qy + cy) * d.Wo + 2 * qx + cx;
   };
 
-  const int HWo = d.Ho * d.Wo;
+  const int HWo = Dz * d.Ho * d.Wo;
   const int cch = tid % CH;      // this thread's 16B chunk within a BK slice
   const int rbase = tid / CH;
 
   // per-thread pixel rows
-  int pn[AX], poy[AX], pox[AX];
+  int pn[AX], poz[AX], poy[AX], pox[AX];
+  const int HWp = A.par ? HWq : d.Ho * d.Wo;   // pixels per output depth slice
 #pragma unroll
   for (int j = 0; j < AX; ++j) {
     const int p = px0 + rbase + j * RPP;
     if (p < A.M) {
       const int n = p / HWq;
-      const int rem = p - n * HWq;
+      int rem = p - n * HWq;
       pn[j] = n;
+      poz[j] = rem / HWp;
+      rem -= poz[j] * HWp;
       poy[j] = rem / Wq;
       pox[j] = rem - poy[j] * Wq;
       if (A.par) { poy[j] = 2 * poy[j] + cy; pox[j] = 2 * pox[j] + cx; }
     } else {
-      pn[j] = -1; poy[j] = 0; pox[j] = 0;
+      pn[j] = -1; poz[j] = 0; poy[j] = 0; pox[j] = 0;
     }
   }
+  const int Dsz = d.Ds > 0 ? d.Ds : 1;   // stored input depth
 
   const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
   const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
@@ -129,7 +134,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
     }
     cur_c = c;
     cur_seg = seg;
-    const int ky = tap / d.ks, kx = tap - (tap / d.ks) * d.ks;
+    const int kk2 = d.ks * d.ks;
+    const int kz = tap / kk2, t2 = tap - kz * kk2;   // kz = 0 in 2-D (T = ks*ks)
+    const int ky = t2 / d.ks, kx = t2 - (t2 / d.ks) * d.ks;
     // weights
 #pragma unroll
     for (int j = 0; j < AW; ++j) {
@@ -152,32 +159,35 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
       bool ok = n >= 0;
       const bf16r* ptr = nullptr;
       if (seg == 0) {
-        int sy, sx;
+        int sz = 0, sy, sx;
+        const bool d3 = d.Do > 0;
         if (!d.transposed) {
+          const int iz = d3 ? poz[j] * d.stride + kz - d.pad : 0;
           const int iy = poy[j] * d.stride + ky - d.pad;
           const int ix = pox[j] * d.stride + kx - d.pad;
           if (d.upsample) {
-            ok = ok && iy >= 0 && iy < 2 * d.Hs && ix >= 0 && ix < 2 * d.Ws;
-            sy = iy >> 1; sx = ix >> 1;
+            ok = ok && iy >= 0 && iy < 2 * d.Hs && ix >= 0 && ix < 2 * d.Ws && iz >= 0 && iz < 2 * Dsz;
+            sz = iz >> 1; sy = iy >> 1; sx = ix >> 1;
           } else {
-            ok = ok && iy >= 0 && iy < d.Hs && ix >= 0 && ix < d.Ws;
-            sy = iy; sx = ix;
+            ok = ok && iy >= 0 && iy < d.Hs && ix >= 0 && ix < d.Ws && iz >= 0 && iz < Dsz;
+            sz = iz; sy = iy; sx = ix;
           }
         } else {
+          const int nz = d3 ? poz[j] + d.pad - kz : 0;
           const int ny = poy[j] + d.pad - ky;
           const int nx = pox[j] + d.pad - kx;
-          ok = ok && ny >= 0 && nx >= 0;
+          ok = ok && ny >= 0 && nx >= 0 && nz >= 0;
           if (d.stride == 2) {
-            ok = ok && !(ny & 1) && !(nx & 1);
-            sy = ny >> 1; sx = nx >> 1;
+            ok = ok && !(ny & 1) && !(nx & 1) && !(nz & 1);
+            sz = nz >> 1; sy = ny >> 1; sx = nx >> 1;
           } else {
-            sy = ny; sx = nx;
+            sz = nz; sy = ny; sx = nx;
           }
-          ok = ok && sy < d.Hs && sx < d.Ws;
+          ok = ok && sy < d.Hs && sx < d.Ws && sz < Dsz;
         }
         ok = ok && c < A.C;
         if (ok) {
-          const size_t pix = ((size_t)n * d.Hs + sy) * d.Ws + sx;
+          const size_t pix = (((size_t)n * Dsz + sz) * d.Hs + sy) * d.Ws + sx;
           ptr = (c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0);
         }
       } else {
@@ -491,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
 
 __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
   const int K = d.K;
-  const int HWo = d.Ho * d.Wo;
+  const int HWo = (d.Do > 0 ? d.Do : 1) * d.Ho * d.Wo;
   const size_t total = (size_t)M * K;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
     const int p = (int)(idx / K);
@@ -526,7 +536,7 @@ __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
 // levels: 16-pixel rows give enough blocks there.  Needs K % 4 == 0 and M % 16 == 0.
 __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d, int M) {
   const int K = d.K;
-  const int HWo = d.Ho * d.Wo;
+  const int HWo = (d.Do > 0 ? d.Do : 1) * d.Ho * d.Wo;
   const size_t total = (size_t)M * K;
   constexpr int RP = FMD_SPLIT_STATS_ROWS;
   const int row = blockIdx.x;
@@ -617,15 +627,16 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   KArgs A;
   A.d = *d;
   if (g) A.g = *g;
-  A.M = d->N * d->Ho * d->Wo;
-  A.T = d->ks * d->ks;
+  const int Dz = d->Do > 0 ? d->Do : 1;
+  A.M = d->N * Dz * d->Ho * d->Wo;
+  A.T = d->ks * d->ks * (d->Do > 0 ? d->ks : 1);
   A.C = d->C0 + d->C1;
   A.nk1 = ((A.C + BK - 1) / BK) * A.T;
   A.nk = A.nk1 + (d->src2 ? (d->C2 + d->C3 + BK - 1) / BK : 0);
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nk + splits - 1) / splits;
   A.Mfull = A.M;
-  A.par = d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
+  A.par = d->Do == 0 && d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
           !d->stats && !d->src2 && !GNA;
   if (A.par) A.M = d->N * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
   A.ntp = (A.M + BPX - 1) / BPX;
@@ -634,7 +645,7 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   if (d->stats) {
     // every wave's pixel range must be one image and full
     const int wrows = BPX / WN;
-    if (wrows != 64 || (d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
+    if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
   }
   dim3 grid(A.ntp * A.ntc, splits, A.par ? 4 : 1);
   hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);
@@ -651,9 +662,10 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->C1 && !d->src1) return -2;
   if (d->src2 && !d->wgt2 && !d->wgt2_tiled) return -3;
   if (d->pro_a && !d->pro_b) return -4;
-  const int M = d->N * d->Ho * d->Wo;
-  // split-K: the combine kernel produces the channel statistics (64-pixel rows) instead of the main kernel
-  const bool rows_ok = d->K % 4 == 0 && M % FMD_SPLIT_STATS_ROWS == 0 && (d->Ho * d->Wo) % FMD_SPLIT_STATS_ROWS == 0;
+  const int M = d->N * (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  const int HWo = (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  // split-K: the combine kernel produces the channel statistics (16-pixel rows) instead of the main kernel
+  const bool rows_ok = d->K % 4 == 0 && M % FMD_SPLIT_STATS_ROWS == 0 && HWo % FMD_SPLIT_STATS_ROWS == 0;
   if (d->splits > 1 && (!d->ws || (d->stats && (!rows_ok || d->out_f32 || d->accumulate)))) return -5;
   (void)C;
   fmd_conv_desc dm = *d;

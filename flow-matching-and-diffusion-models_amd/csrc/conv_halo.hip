@@ -646,7 +646,7 @@ __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, i
 // Called by fmd_conv when the problem qualifies (3x3, stride 1, pad 1, forward gather,
 // output tile 16x16 inside one image, >= 128 tiles).  Returns 1 if not applicable.
 extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed || d->Do > 0 || d->Ds > 0) return 1;
   if (d->splits > 1 && (!d->ws || d->stats)) return 1;
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;

@@ -20,9 +20,9 @@ inline int grid_for(long long work, int per_block = 256, int cap = 16384) {
 // mode 0: forward  out[k][tap][c] (rows k >= K and channels c >= C zero; Kpad x T x Cpad)
 // mode 1: data-grad out[c][tap][k] (Cpad rows, Kpad inner)
 // mode 2: data-grad of nearest-x2 upsample + 3x3 conv: 4x4 effective taps, out[c][16][k]
-__global__ void prep_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode, int Kpad, int Cpad,
-                                    bf16r* __restrict__ out) {
-  const int T = ks * ks;
+// T: taps of the kernel (ks*ks in 2-D, ks^3 in 3-D); ks is read by mode 2 only (2-D up-dgrad)
+__global__ void prep_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int T, int mode, int Kpad,
+                                    int Cpad, bf16r* __restrict__ out) {
   if (mode == 0) {
     const long long total = (long long)Kpad * T * Cpad;
     GRID_STRIDE(i, total) {
@@ -430,6 +430,27 @@ __global__ void sum_pool2_kernel(const bf16r* __restrict__ src, int N, int H, in
   }
 }
 
+__global__ void sum_pool2_3d_kernel(const bf16r* __restrict__ src, int N, int D, int H, int W, int C,
+                                    bf16r* __restrict__ dst, int acc) {
+  // dst[n][z][y][x][c] (+)= sum of the 2x2x2 block of src (dst D x H x W, src 2D x 2H x 2W)
+  const long long total = (long long)N * D * H * W * C;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int x = (int)(r % W); r /= W;
+    const int y = (int)(r % H); r /= H;
+    const int z = (int)(r % D);
+    const int n = (int)(r / D);
+    float s = 0.f;
+    for (int dz = 0; dz < 2; ++dz)
+      for (int dy = 0; dy < 2; ++dy)
+        for (int dx = 0; dx < 2; ++dx)
+          s += bf2f(src[((((size_t)n * 2 * D + 2 * z + dz) * 2 * H + 2 * y + dy) * 2 * W + 2 * x + dx) * C + c]);
+    if (acc) s += bf2f(dst[i]);
+    dst[i] = (bf16r)f2bf(s);
+  }
+}
+
 __global__ void add_bf16_kernel(const bf16r* __restrict__ a, bf16r* __restrict__ dst, long long n) {
   GRID_STRIDE(i, n) dst[i] = (bf16r)f2bf(bf2f(dst[i]) + bf2f(a[i]));
 }
@@ -688,7 +709,15 @@ extern "C" {
 int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t Kpad, int32_t Cpad,
                       void* out, fmd_stream_t s) {
   const long long total = (long long)Kpad * Cpad * (mode == 2 ? 16 : ks * ks);
-  LAUNCH(prep_weights_kernel, grid_for(total), w, K, C, ks, mode, Kpad, Cpad, (bf16r*)out);
+  LAUNCH(prep_weights_kernel, grid_for(total), w, K, C, ks, ks * ks, mode, Kpad, Cpad, (bf16r*)out);
+}
+
+int fmd_prep_weights_t(const float* w, int32_t K, int32_t C, int32_t T, int32_t mode, int32_t Kpad, int32_t Cpad,
+                       void* out, fmd_stream_t s) {
+  if (mode != 0 && mode != 1 && mode != 3) return -1;
+  if (T < 1 || K > Kpad || C > Cpad) return -2;
+  const long long total = (long long)Kpad * Cpad * T;
+  LAUNCH(prep_weights_kernel, grid_for(total), w, K, C, 0, T, mode, Kpad, Cpad, (bf16r*)out);
 }
 
 
@@ -845,6 +874,12 @@ int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* o
 int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc,
                   fmd_stream_t s) {
   LAUNCH(sum_pool2_kernel, grid_for((long long)N * H * W * C), (const bf16r*)src, N, H, W, C, (bf16r*)dst, acc);
+}
+
+int fmd_sum_pool2_3d(const void* src, int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, void* dst,
+                     int32_t acc, fmd_stream_t s) {
+  LAUNCH(sum_pool2_3d_kernel, grid_for((long long)N * D * H * W * C), (const bf16r*)src, N, D, H, W, C,
+         (bf16r*)dst, acc);
 }
 
 int fmd_add_bf16(const void* a, void* dst, int64_t n, fmd_stream_t s) {

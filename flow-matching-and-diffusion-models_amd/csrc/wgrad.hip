@@ -48,13 +48,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   const int my_tap = A.merged ? (tid & 15) / cpt : tap;
   const int my_c = A.merged ? ((tid & 15) - my_tap * cpt) * 8 : ci0 + (tid & 15) * 8;
   const bool col_ok = A.merged ? my_tap < A.T : my_c < A.C;
-  const int ky = my_tap / d.ks, kx = my_tap - (my_tap / d.ks) * d.ks;
+  const int kk2 = d.ks * d.ks;
+  const int kz = my_tap / kk2, t2 = my_tap - (my_tap / kk2) * kk2;   // kz = 0 in 2-D
+  const int ky = t2 / d.ks, kx = t2 - (t2 / d.ks) * d.ks;
+  const bool d3 = d.Do > 0;
+  const int Dsz = d.Ds > 0 ? d.Ds : 1, Dz = d.Do > 0 ? d.Do : 1;
   const int split = blockIdx.y;
   const int s0 = split * A.per_split;
   const int s1 = min(A.nsteps, s0 + A.per_split);
   const bool do_bias = d.db && tap == 0 && tci == 0;
 
-  const int HWo = d.Ho * d.Wo;
+  const int HWo = Dz * d.Ho * d.Wo, HWs = d.Ho * d.Wo;
   const int chunk = tid & 15;     // 8-channel chunk
   const int rb = tid >> 4;        // row (pixel) 0..15, +16
   const bf16r* __restrict__ dy = (const bf16r*)d.dy;
@@ -84,19 +88,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
       const bf16r* ptr = nullptr;
       if (ok) {
         n = p / HWo;
-        const int rem = p - n * HWo;
+        int rem = p - n * HWo;
+        const int oz = rem / HWs;
+        rem -= oz * HWs;
         const int oy = rem / d.Wo, ox = rem - (rem / d.Wo) * d.Wo;
+        const int iz = d3 ? oz * d.stride + kz - d.pad : 0;
         const int iy = oy * d.stride + ky - d.pad, ix = ox * d.stride + kx - d.pad;
-        int sy, sx;
+        int sz, sy, sx;
         if (d.upsample) {
-          ok = iy >= 0 && iy < 2 * d.Hs && ix >= 0 && ix < 2 * d.Ws;
-          sy = iy >> 1; sx = ix >> 1;
+          ok = iy >= 0 && iy < 2 * d.Hs && ix >= 0 && ix < 2 * d.Ws && iz >= 0 && iz < 2 * Dsz;
+          sz = iz >> 1; sy = iy >> 1; sx = ix >> 1;
         } else {
-          ok = iy >= 0 && iy < d.Hs && ix >= 0 && ix < d.Ws;
-          sy = iy; sx = ix;
+          ok = iy >= 0 && iy < d.Hs && ix >= 0 && ix < d.Ws && iz >= 0 && iz < Dsz;
+          sz = iz; sy = iy; sx = ix;
         }
         if (ok) {
-          const size_t pix = ((size_t)n * d.Hs + sy) * d.Ws + sx;
+          const size_t pix = (((size_t)n * Dsz + sz) * d.Hs + sy) * d.Ws + sx;
           ptr = (c < d.C0) ? x0 + pix * d.C0 + c : x1 + pix * d.C1 + (c - d.C0);
         }
       }
@@ -268,7 +275,7 @@ constexpr int RC = 64;
 
 __global__ __launch_bounds__(256) void wgrad_reduce(const WArgs A, int splits, int nsl, int sstride) {
   const fmd_wgrad_desc& d = A.d;
-  __shared__ float res[RC * 25 + 1];   // [c][tap], T <= 25
+  __shared__ float res[RC * 27 + 1];   // [c][tap], T <= 27 (3x3x3)
   const size_t per = (size_t)d.K * A.T * A.C;
   const int k = blockIdx.x, c0 = blockIdx.y * RC;
   const int nc = min(RC, A.C - c0);
@@ -302,8 +309,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const WArgs A, int splits, i
 WArgs make_args(const fmd_wgrad_desc* d) {
   WArgs A;
   A.d = *d;
-  A.M = d->N * d->Ho * d->Wo;
-  A.T = d->ks * d->ks;
+  A.M = d->N * (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  A.T = d->ks * d->ks * (d->Do > 0 ? d->ks : 1);
   A.C = d->C0 + d->C1;
   A.ntc = (d->K + BCO - 1) / BCO;
   A.nci = (A.C + BCI - 1) / BCI;
@@ -320,7 +327,8 @@ WArgs make_args(const fmd_wgrad_desc* d) {
 extern "C" int64_t fmd_wgrad_workspace(const fmd_wgrad_desc* d) {
   const int splits = d->splits > 1 ? d->splits : 1;
   const int64_t C = d->C0 + d->C1;
-  return (int64_t)splits * d->K * d->ks * d->ks * C + (int64_t)splits * d->K;
+  const int64_t T = (int64_t)d->ks * d->ks * (d->Do > 0 ? d->ks : 1);
+  return (int64_t)splits * d->K * T * C + (int64_t)splits * d->K;
 }
 
 extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
@@ -349,7 +357,7 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
     if (rc) return rc;
   }
-  if (A.T > 25) return -4;
+  if (A.T > 27) return -4;
   hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl, sstride);
   return (int)hipGetLastError();
 }

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 // 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
 // Returns 1 (nothing launched) when the problem does not qualify.  d->splits = pixel-tile splits.
 extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->Do > 0 || d->Ds > 0) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (d->Ho % WTH || d->Wo % WTW) return 1;
   const int C = d->C0 + d->C1;

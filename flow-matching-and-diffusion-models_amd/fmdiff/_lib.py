@@ -27,6 +27,7 @@ class ConvDesc(C.Structure):
         ("bias", p), ("bias2", p), ("bias_nc", p), ("resid", p), ("out", p), ("out_f32", i32), ("accumulate", i32),
         ("stats", p), ("ep_x0", p), ("ep_x1", p), ("ep_C0", i32), ("ep_a", p), ("ep_b", p),
         ("ws", p), ("splits", i32), ("force_generic", i32), ("wgt_tiled", p), ("wgt2_tiled", p),
+        ("Ds", i32), ("Do", i32),
     ]
 
 
@@ -36,7 +37,7 @@ class WgradDesc(C.Structure):
         ("N", i32), ("Hs", i32), ("Ws", i32), ("C0", i32), ("C1", i32), ("Ho", i32), ("Wo", i32), ("K", i32),
         ("ks", i32), ("stride", i32), ("pad", i32), ("upsample", i32),
         ("src0", p), ("src1", p), ("pro_a", p), ("pro_b", p), ("pro_silu", i32), ("dy", p), ("ldy", i32), ("dw", p), ("db", p),
-        ("accumulate", i32), ("ws", p), ("splits", i32), ("force_generic", i32),
+        ("accumulate", i32), ("ws", p), ("splits", i32), ("force_generic", i32), ("Ds", i32), ("Do", i32),
     ]
 
 
@@ -83,10 +84,12 @@ SIGNATURES = {
     "fmd_halo_set_workgroup": [i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
+    "fmd_prep_weights_t": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_batch": [p, i32, i32, p],
     "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
     "fmd_nhwc_to_nchw": [p, i32, i32, i32, i32, i32, p, p],
     "fmd_sum_pool2": [p, i32, i32, i32, i32, p, i32, p],
+    "fmd_sum_pool2_3d": [p, i32, i32, i32, i32, i32, p, i32, p],
     "fmd_add_bf16": [p, p, i64, p],
     "fmd_timestep_embedding": [p, i32, i32, i32, i32, f32, f32, i32, p, p],
     "fmd_adamw_sched": [p, p, p, p, i64, p, f32, i32, i32, f32, f32, f32, f32, f32, p],

@@ -43,8 +43,8 @@ class Stats:
 
 def channel_stats(x: torch.Tensor, rows: Optional[int] = None, y: Tuple = None) -> Stats:
     """(sum x, sum x^2) per (n, channel, row-block), or (sum x, sum x*y) when ``y=(y0, y1, C0)`` is given."""
-    N, H, W, Cc = x.shape
-    HW = H * W
+    N, Cc = x.shape[0], x.shape[-1]
+    HW = x[0, ..., 0].numel()   # pixels per image (H*W, or D*H*W for NDHWC)
     if rows is None:
         # 64-pixel slab rows (like the conv epilogues): enough blocks to cover the chip even at 32x32
         rows = 64 if HW % 64 == 0 else HW
@@ -192,18 +192,27 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
          wgt2_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
     """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``."""
     _need_cuda(src0, "conv")
-    N, Hs, Ws, C0 = src0.shape
+    # 3-D (spatial_dims = 3): NDHWC tensors, cubic kernels; ``out_hw_`` is then (Do, Ho, Wo)
+    d3 = src0.dim() == 5
+    if d3:
+        N, Ds, Hs, Ws, C0 = src0.shape
+    else:
+        N, Hs, Ws, C0 = src0.shape
+        Ds = 0
     C1 = src1.shape[-1] if src1 is not None else 0
     if out_hw_ is not None:
-        Ho, Wo = out_hw_
+        Do, Ho, Wo = out_hw_ if d3 else (0, *out_hw_)
     else:
         Ho, Wo = out_hw(Hs, ks, stride, pad, upsample), out_hw(Ws, ks, stride, pad, upsample)
-    M = N * Ho * Wo
+        Do = out_hw(Ds, ks, stride, pad, upsample) if d3 else 0
+    M = N * max(Do, 1) * Ho * Wo
     dev = src0.device
     if out is None:
-        out = torch.empty((N, Ho, Wo, K), device=dev, dtype=F32 if out_f32 else BF16)
+        shape = (N, Do, Ho, Wo, K) if d3 else (N, Ho, Wo, K)
+        out = torch.empty(shape, device=dev, dtype=F32 if out_f32 else BF16)
     d = ConvDesc()
     d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, Hs, Ws, C0, C1, Ho, Wo, K
+    d.Ds, d.Do = Ds, Do
     d.ks, d.stride, d.pad, d.upsample, d.transposed = ks, stride, pad, int(upsample), int(transposed)
     d.src0, d.src1 = _p(src0), _p(src1)
     if pro is not None:
@@ -218,12 +227,12 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.ep_x0, d.ep_x1, d.ep_C0, d.ep_a, d.ep_b = _p(x0), _p(x1), x0.shape[-1], _p(ea), _p(eb)
         if x1 is None and x0.shape[-1] != K:
             raise ValueError("epilogue tensor channels must match the conv output channels")
-    T = ks * ks
+    T = ks * ks * (ks if d3 else 1)
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
     bpx = 256 if K <= 16 else 128
-    halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
-                                                  pro is not None)
+    halo = not d3 and not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
+                                                            C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
     if halo:
         splits = halo_splits(N, Ho, Wo, K, C0 + C1)
@@ -243,7 +252,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.splits = 1
     st = None
     # statistics from the conv epilogue (no split) or from the split-K combine (csrc/conv.hip splitk_reduce_rows)
-    fused_stats = want_stats and (Ho * Wo) % 64 == 0 and (
+    fused_stats = want_stats and (max(Do, 1) * Ho * Wo) % 64 == 0 and (
         (splits == 1 and M % bpx == 0) or (splits > 1 and K % 4 == 0 and not out_f32 and not accumulate))
     if fused_stats:
         rows = 64 if splits == 1 else SPLIT_STATS_ROWS
@@ -304,14 +313,21 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     """dW (+)= conv weight gradient in the reference [K][C][kh][kw] fp32 layout (and db).
 
     ``dy_offset``: use channels [dy_offset, dy_offset + dw.shape[0]) of a wider dY (fused q/k/v)."""
-    N, Hs, Ws, C0 = src0.shape
+    d3 = src0.dim() == 5
+    if d3:
+        N, Ds, Hs, Ws, C0 = src0.shape
+        _, Do, Ho, Wo, ldy = dy.shape
+    else:
+        N, Hs, Ws, C0 = src0.shape
+        _, Ho, Wo, ldy = dy.shape
+        Ds = Do = 0
     C1 = src1.shape[-1] if src1 is not None else 0
-    _, Ho, Wo, ldy = dy.shape
     K = dw.shape[0]
-    M = N * Ho * Wo
+    M = N * max(Do, 1) * Ho * Wo
     Ct = C0 + C1
     d = WgradDesc()
     d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, Hs, Ws, C0, C1, Ho, Wo, K
+    d.Ds, d.Do = Ds, Do
     d.ks, d.stride, d.pad, d.upsample = ks, stride, pad, int(upsample)
     d.src0, d.src1 = _p(src0), _p(src1)
     if pro is not None:
@@ -319,7 +335,8 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
     d.force_generic = int(force_generic)
     if splits is None:
-        if not force_generic and wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample, ldy):
+        if not d3 and not force_generic and wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample,
+                                                                 ldy):
             # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk, pixel-tile split);
             # partial slabs capped at ~96 MB (their write + reduce read)
             tiles = N * (Ho // 8) * (Wo // 16)
@@ -327,10 +344,11 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36)))
         else:
             # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
-            tiles = -(-K // 128) * (1 if ks > 1 and Ct * ks * ks <= 128 else -(-Ct // 128) * ks * ks)
+            T = ks * ks * (ks if d3 else 1)
+            tiles = -(-K // 128) * (1 if T > 1 and Ct * T <= 128 else -(-Ct // 128) * T)
             steps = -(-M // 32)
             # up to 4 workgroups per CU (the kernel is latency-bound at one), partial slabs <= 48 MB
-            cap = max(256, min(1024, (48 << 20) // (K * Ct * ks * ks * 4)))
+            cap = max(256, min(1024, (48 << 20) // (K * Ct * T * 4)))
             splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), cap))
     d.splits = splits
     ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
@@ -341,9 +359,16 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
 def prep_weights(w: torch.Tensor, mode: int, Kpad: Optional[int] = None, Cpad: Optional[int] = None, out=None):
     """fp32 [K][C][kh][kw] -> bf16 kernel layout (mode 0 fwd [Kpad][T][Cpad]; 1 dgrad [Cpad][T][Kpad]; 2 up-dgrad)."""
     K, Cc = w.shape[0], w.shape[1]
-    ks = w.shape[2] if w.dim() == 4 else 1
+    ks = w.shape[2] if w.dim() >= 4 else 1
     Kpad = Kpad or K
     Cpad = Cpad or Cc
+    if w.dim() == 5:   # 3-D: ks^3 taps (modes 0, 1, 3)
+        T = ks ** 3
+        shape = (Kpad, T, Cpad) if mode == 0 else (Cpad, T, Kpad)
+        if out is None:
+            out = torch.empty(shape, device=w.device, dtype=BF16)
+        _lib.call("fmd_prep_weights_t", _p(w.contiguous()), K, Cc, T, mode, Kpad, Cpad, _p(out), stream())
+        return out
     T = 16 if mode == 2 else ks * ks
     shape = (Kpad, T, Cpad) if mode == 0 else (Cpad, T, Kpad)
     if out is None:
@@ -495,6 +520,12 @@ def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
 def sum_pool2(src, dst, acc):
     N, H, W, Cc = dst.shape
     _lib.call("fmd_sum_pool2", _p(src), N, H, W, Cc, _p(dst), int(acc), stream())
+
+
+def sum_pool2_3d(src, dst, acc=False):
+    """dst (+)= 2x2x2 block sums of src (bf16 NDHWC): the data gradient of a nearest-x2 3-D upsample."""
+    N, D, H, W, Cc = dst.shape
+    _lib.call("fmd_sum_pool2_3d", _p(src), N, D, H, W, Cc, _p(dst), int(acc), stream())
 
 
 def add_(dst, a):

@@ -72,6 +72,8 @@ typedef struct fmd_conv_desc {
   int32_t force_generic;    /* 1: never take the halo-tiled 3x3 path (testing) */
   const void* wgt_tiled;    /* wgt re-tiled by fmd_tile_weights_halo (enables the halo path) */
   const void* wgt2_tiled;   /* wgt2 re-tiled likewise (T = 1) */
+  int32_t Ds, Do;           /* 3-D problems (spatial_dims = 3, NDHWC): stored / output depth; 0 = 2-D.
+                               Cubic kernel (ks^3 taps, wgt [K][ks^3][C]); implicit-GEMM path only */
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the
@@ -140,6 +142,7 @@ typedef struct fmd_wgrad_desc {
   float* ws;                /* fp32 workspace, size fmd_wgrad_workspace() floats */
   int32_t splits;           /* split-K over pixels (halo path: over 8x16-pixel tiles) */
   int32_t force_generic;    /* 1: never use the halo-tiled kernel (tests) */
+  int32_t Ds, Do;           /* 3-D: stored / output depth (0 = 2-D); dw [K][C][ks][ks][ks] */
 } fmd_wgrad_desc;
 
 /* Dispatches 3x3 stride-1 problems (K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0) to the
@@ -192,6 +195,10 @@ int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0,
  * [Cpad][16][Kpad] data gradient of nearest-x2 upsample + 3x3 conv (4x4 taps). */
 int fmd_prep_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t Kpad, int32_t Cpad,
                      void* out, fmd_stream_t s);
+/* Same for any tap count T (w [K][C][T], e.g. T = 27 for a 3x3x3 kernel); modes 0, 1 and 3 (3 = mode 1
+ * with the taps reversed: the stride-1 data gradient as a forward gather). */
+int fmd_prep_weights_t(const float* w, int32_t K, int32_t C, int32_t T, int32_t mode, int32_t Kpad, int32_t Cpad,
+                       void* out, fmd_stream_t s);
 /* All bf16 weight layouts of a model in one launch (after each optimizer step).  jobs: device int64
  * [njobs][16], one per fp32 master w[K][C][ks*ks] = {w, K | C<<32, ks | nout<<32, first block | ktiles<<32,
  * then nout (<= 6) pairs {out, mode | kind<<8 | R<<16 | Cc<<40}}; kind 0 = the fmd_prep_weights layout
@@ -202,6 +209,10 @@ int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t C
 int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
                      fmd_stream_t s);
 int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc, fmd_stream_t s);
+/* dst[n][z][y][x][c] (+)= sum of the 2x2x2 block of src (bf16 NDHWC, src 2D x 2H x 2W): the data gradient
+ * of a nearest-x2 3-D upsample. */
+int fmd_sum_pool2_3d(const void* src, int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, void* dst,
+                     int32_t acc, fmd_stream_t s);
 int fmd_add_bf16(const void* a, void* dst, int64_t n, fmd_stream_t s);
 
 /* ------------------------------------------------------ time embedding

@@ -646,3 +646,102 @@ def test_multistep_schedulers_vs_oracle(kind, order, variant, betas):
         xg = got.step(eps.to(DEV), t, xg).prev_sample
         torch.testing.assert_close(xg.cpu(), xr, rtol=1e-5, atol=1e-5 * xr.abs().max().item())
 
+
+
+def _to_ncdhw(x):
+    return x.float().permute(0, 4, 1, 2, 3).contiguous()
+
+
+def _rand_ndhwc(N, D, H, W, C, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(N, D, H, W, C, generator=g) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("mode", ["s1_pro_stats", "s2", "up_concat", "1x1"])
+def test_conv3d_forward_vs_torch(mode):
+    """3-D implicit GEMM (NDHWC, 3x3x3 / 1x1x1, config E's EfficientUNetND(spatial_dims=3) convs) vs F.conv3d."""
+    O = ops()
+    N, D, H, W, C0, C1, K = 2, 6, 8, 8, 32, 0, 48
+    if mode == "up_concat":
+        C1 = 16
+    ks, s = (1, 1) if mode == "1x1" else (3, 2 if mode == "s2" else 1)
+    pad = ks // 2
+    x0 = _rand_ndhwc(N, D, H, W, C0, 61)
+    x1 = _rand_ndhwc(N, D, H, W, C1, 62) if C1 else None
+    g = torch.Generator().manual_seed(63)
+    w = torch.randn(K, C0 + C1, ks, ks, ks, generator=g) / math.sqrt((C0 + C1) * ks ** 3)
+    b = torch.randn(K, generator=g) * 0.1
+    kw = dict(bias=b.to(DEV), ks=ks, stride=s, pad=pad)
+    x = _to_ncdhw(torch.cat([x0, x1], -1) if C1 else x0)
+    if mode == "s1_pro_stats":
+        a = torch.rand(N, C0) + 0.5
+        bb = torch.randn(N, C0) * 0.2
+        kw["pro"] = (a.to(DEV), bb.to(DEV), True)
+        x = F.silu(x * a[:, :, None, None, None] + bb[:, :, None, None, None]).to(torch.bfloat16).float()
+        kw["want_stats"] = True
+    if mode == "up_concat":
+        kw["upsample"] = True
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+    out, st = O.conv(x0.to(DEV), K, O.prep_weights(w.to(DEV), 0), src1=x1.to(DEV) if C1 else None, **kw)
+    ref = F.conv3d(x, _bfw(w), b, stride=s, padding=pad).permute(0, 2, 3, 4, 1)
+    _close(out, ref)
+    if st is not None:
+        o = out.float().cpu()
+        tot = st.slab.cpu().view(N, -1, K, 2).sum(1)
+        torch.testing.assert_close(tot[..., 0], o.sum((1, 2, 3)), rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("mode", ["s1", "s2", "up"])
+def test_conv3d_data_gradient_vs_torch(mode):
+    """3-D data gradients: stride 1 = forward gather with reversed taps (mode-3 weights); stride 2 = transposed
+    gather; nearest-x2 upsample = high-resolution data gradient + 2x2x2 sum pool (fmd_sum_pool2_3d)."""
+    O = ops()
+    N, D, H, W, C, K = 2, 4, 8, 8, 32, 48
+    s = 2 if mode == "s2" else 1
+    x = _to_ncdhw(_rand_ndhwc(N, D, H, W, C, 71)).requires_grad_()
+    g = torch.Generator().manual_seed(72)
+    w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if mode == "up" else x
+    y = F.conv3d(xin, _bfw(w), stride=s, padding=1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 4, 1).contiguous().to(torch.bfloat16).to(DEV)
+    if mode == "s2":
+        got, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 1), stride=2, transposed=True, out_hw_=(D, H, W))
+    else:
+        hi = (2 * D, 2 * H, 2 * W) if mode == "up" else (D, H, W)
+        g1, _ = O.conv(dyn, C, O.prep_weights(w.to(DEV), 3), out_hw_=hi)
+        if mode == "up":
+            got = torch.empty(N, D, H, W, C, device=DEV, dtype=torch.bfloat16)
+            O.sum_pool2_3d(g1, got)
+        else:
+            got = g1
+    _close(got, x.grad.permute(0, 2, 3, 4, 1), rel=2e-2)
+
+
+@pytest.mark.parametrize("mode", ["s1_pro", "s2", "up"])
+def test_wgrad3d_vs_torch(mode):
+    O = ops()
+    N, D, H, W, C, K = 2, 4, 8, 8, 32, 48
+    s, up = (2 if mode == "s2" else 1), mode == "up"
+    xb = _rand_ndhwc(N, D, H, W, C, 81)
+    x = _to_ncdhw(xb)
+    pro = None
+    if mode == "s1_pro":
+        a = torch.rand(N, C) + 0.5
+        bb = torch.randn(N, C) * 0.2
+        x = F.silu(x * a[:, :, None, None, None] + bb[:, :, None, None, None]).to(torch.bfloat16).float()
+        pro = (a.to(DEV), bb.to(DEV), True)
+    g = torch.Generator().manual_seed(82)
+    w = (torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)).requires_grad_()
+    bias = torch.zeros(K, requires_grad=True)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if up else x
+    y = F.conv3d(xin, w, bias, stride=s, padding=1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dw = torch.zeros(K, C, 3, 3, 3, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    O.wgrad(xb.to(DEV), dy.permute(0, 2, 3, 4, 1).contiguous().to(torch.bfloat16).to(DEV), dw, stride=s,
+            upsample=up, pro=pro, db=db)
+    torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
+    torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
