@@ -124,6 +124,9 @@ class WeightCache:
         jobs = [(key, e) for key, e in self._c.items() if e["kind"] in ("prep", "tiled")]
         if jobs:
             self._launch_batch(jobs)
+        for key, e in self._c.items():          # cubic (3-D) kernels: the batched prep takes <= 9 taps
+            if e["kind"] == "prep3":
+                ops.prep_weights(e["src"].detach(), *e["job"], out=e["buf"])
         for key, e in self._c.items():
             e["ver"] = self._ver(e["src"]) if e["kind"] != "fused" else tuple(self._ver(w) for w in e["src"])
         self._force.clear()
@@ -169,6 +172,10 @@ class WeightCache:
         if not self._fresh(key, self._ver(w)):
             e = self._c.get(key)
             buf = ops.prep_weights(w.detach(), mode, Kpad, Cpad, out=None if e is None else e["buf"])
+            if w.dim() == 5:
+                self._c[key] = dict(kind="prep3", src=w, buf=buf, ver=self._ver(w), job=(mode, Kpad, Cpad))
+                self._force.discard(key)
+                return buf
             K, C = w.shape[0], w.shape[1]
             ks = w.shape[2] if w.dim() == 4 else 1
             R, T, Cc = buf.shape
@@ -233,9 +240,10 @@ class Ctx:
 
 
 def _check_conv(c: Conv, ks, stride, pad):
-    if c.dims != 2:
-        raise NotImplementedError("fmdiff engine runs spatial_dims=2 (1-D/3-D kernels: next)")
-    if c.kernel_size != (ks, ks) or c.stride != (stride, stride) or c.padding != (pad, pad):
+    if c.dims not in (2, 3):
+        raise NotImplementedError("fmdiff engine runs spatial_dims=2 and 3 (1-D: next)")
+    n = c.dims
+    if c.kernel_size != (ks,) * n or c.stride != (stride,) * n or c.padding != (pad,) * n:
         raise NotImplementedError(f"unexpected conv geometry {c.kernel_size}/{c.stride}/{c.padding}")
 
 
@@ -284,17 +292,15 @@ class UNetEngine:
         """Plain 3x3 conv (input conv, DownsampleND, UpsampleND)."""
         _check_conv(conv, 3, stride, 1)
         Cin = x.C
-        N_, Hs_, Ws_, _ = x.t.shape
-        Ho_ = ops.out_hw(Hs_, 3, stride, 1, upsample)
-        halo = stride == 1 and ops.halo_eligible(N_, Hs_, Ho_, ops.out_hw(Ws_, 3, stride, 1, upsample),
-                                                 conv.out_channels, upsample=upsample, Cin=Cin)
+        N_, sp = x.t.shape[0], tuple(x.t.shape[1:-1])
+        Ho_ = ops.out_hw(sp[0], 3, stride, 1, upsample)
+        halo = len(sp) == 2 and stride == 1 and ops.halo_eligible(
+            N_, sp[0], Ho_, ops.out_hw(sp[1], 3, stride, 1, upsample), conv.out_channels, upsample=upsample, Cin=Cin)
         w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
                            bias=conv.bias, want_stats=True, wgt_tiled=wt)
         o = Act(out, st)
         if ctx.tape is not None:
-            N, H, W, _ = x.t.shape
-
             def bwd():
                 dy = o.grad
 
@@ -306,13 +312,18 @@ class UNetEngine:
                 self._wg(wg)
                 if not x.need_grad:
                     return
-                if upsample:
+                g, acc = _gdest(x)
+                if upsample and len(sp) == 2:
+                    # nearest-x2 folded into the weights: a 4x4 stride-2 transposed gather (mode 2)
                     wd = self.wc.get(conv.weight, 2)
-                    g, acc = _gdest(x)
-                    ops.conv(dy, Cin, wd, ks=4, stride=2, pad=1, out_hw_=(H, W), out=g, accumulate=bool(acc))
+                    ops.conv(dy, Cin, wd, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc))
+                elif upsample:
+                    # 3-D: data gradient at the upsampled resolution, then the 2x2x2 box sum the
+                    # nearest-x2 copy implies
+                    hi = self.dgrad3x3(conv.weight, dy, Cin, tuple(2 * v for v in sp))[0]
+                    ops.sum_pool2_3d(hi, g, acc=bool(acc))
                 else:
-                    g, acc = _gdest(x)
-                    self.dgrad3x3(conv.weight, dy, Cin, H, W, stride=stride, out=g, accumulate=bool(acc))
+                    self.dgrad3x3(conv.weight, dy, Cin, sp, stride=stride, out=g, accumulate=bool(acc))
             ctx.tape.append(bwd)
         return o
 
@@ -342,15 +353,17 @@ class UNetEngine:
             return None, self.wc.tiled(w, mode, Kpad, Cpad)
         return self.wc.get(w, mode, Kpad, Cpad), None
 
-    def dgrad3x3(self, w, dy, Cin, H, W, *, stride=1, Kpad=None, **kw):
-        """Data gradient of a 3x3 pad-1 conv.  Stride 1 = forward gather with flipped taps (so it runs on
-        the halo-tiled kernel); stride 2 = transposed gather."""
+    def dgrad3x3(self, w, dy, Cin, sp, *, stride=1, Kpad=None, **kw):
+        """Data gradient of a 3x3 (3x3x3) pad-1 conv onto the input grid ``sp`` ((H, W) or (D, H, W)).
+        Stride 1 = forward gather with flipped taps (so a 2-D one runs on the halo-tiled kernel);
+        stride 2 = transposed gather."""
+        sp = tuple(sp)
         if stride == 1:
-            halo = ops.halo_eligible(dy.shape[0], H, H, W, Cin, Cin=dy.shape[-1])
+            halo = len(sp) == 2 and ops.halo_eligible(dy.shape[0], sp[0], sp[0], sp[1], Cin, Cin=dy.shape[-1])
             base, tiled = self._wts(w, 3, halo, Kpad, None)
-            return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=(H, W), wgt_tiled=tiled, **kw)
+            return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=sp, wgt_tiled=tiled, **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,
-                        out_hw_=(H, W), **kw)
+                        out_hw_=sp, **kw)
 
     def _wgrad_target(self, conv: Conv, Cin: int):
         """fp32 buffer the wgrad kernel writes: param.grad itself unless channels were padded."""
@@ -368,9 +381,11 @@ class UNetEngine:
     def res_block(self, m: ResBlockND, xs: List[Act], ctx: Ctx):
         x0 = xs[0]
         x1 = xs[1] if len(xs) > 1 else None
-        N, H, W, C0 = x0.t.shape
+        N, C0, sp = x0.t.shape[0], x0.t.shape[-1], tuple(x0.t.shape[1:-1])
         C1 = x1.C if x1 is not None else 0
-        Cin, Cout, HW = C0 + C1, m.out_channels, H * W
+        Cin, Cout, HW = C0 + C1, m.out_channels, math.prod(sp)
+        d2 = len(sp) == 2            # halo kernels are 2-D only
+        H, W = sp[-2], sp[-1]
         if Cin != m.channels:
             raise ValueError(f"ResBlockND expects {m.channels} channels, got {Cin}")
         if m.dropout and m.training:
@@ -390,10 +405,10 @@ class UNetEngine:
             eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
             es = eo.shape[1]
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
-        halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
+        halo1 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
         mat1 = _materialise(halo1, x1, Cin, HW)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
-            halo1 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cin)
+            halo1 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cin)
         w1, w1t = self._wts(c1.weight, 0, halo1)
         t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
         src1 = x1.t if (x1 is not None and t1 is None) else None
@@ -414,10 +429,10 @@ class UNetEngine:
             kw["resid"] = x0.t
         else:
             _check_conv(sk.conv, 1, 1, 0)
-        halo2 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cout, pro=True)
+        halo2 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cout, pro=True)
         mat2 = _materialise(halo2, None, Cout, HW)
         if mat2 and not halo2:
-            halo2 = ops.halo_eligible(N, H, H, W, Cout, Cin=Cout)
+            halo2 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cout)
         if not isinstance(sk, Identity):
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
@@ -443,7 +458,7 @@ class UNetEngine:
             self._wg(wg2)
             # the skip data gradient (non-identity) is fused into the GroupNorm-1 backward below
             extra = dy if isinstance(sk, Identity) else None
-            dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, H, W, ep=(h, None, a2, b2), want_stats=True)
+            dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, sp, ep=(h, None, a2, b2), want_stats=True)
             if slot is not None:
                 demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
             else:
@@ -467,7 +482,7 @@ class UNetEngine:
             else:
                 self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
                                            db=c1.bias.grad))
-            dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, H, W, ep=(x0.t, x1.t if x1 else None, a1, b1),
+            dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, sp, ep=(x0.t, x1.t if x1 else None, a1, b1),
                                     want_stats=True)
             P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,
                                          g1.bias.grad)
@@ -486,8 +501,10 @@ class UNetEngine:
 
     def attention(self, m, x: Act, ctx: Ctx):
         """SpatialSelfAttention (raw reshape) or DiffusersAttentionND (self-attention only)."""
-        N, H, W, Cc = x.t.shape
-        T = H * W
+        N, Cc, sp = x.t.shape[0], x.t.shape[-1], tuple(x.t.shape[1:-1])
+        T = math.prod(sp)
+        H, W = T // sp[-1], sp[-1]        # 1x1 convs only: a 3-D volume runs as a (D*H, W) plane
+        x4 = x.t.view(N, H, W, Cc)
         if isinstance(m, SpatialSelfAttention):
             if m.use_linear:
                 raise NotImplementedError("LinearQKVAttention is not yet on the fmdiff engine")
@@ -507,44 +524,45 @@ class UNetEngine:
         else:
             raise NotImplementedError(type(m).__name__)
         a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
-        qkv, _ = ops.conv(x.t, 3 * inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
+        qkv, _ = ops.conv(x4, 3 * inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
         o, lse = ops.attention_fwd(qkv, T, heads, dh, raw)
         o4 = o.view(N, H, W, inner)
-        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x.t, want_stats=True)
-        y = Act(out, st)
+        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
+        y = Act(out.view(x.t.shape), st)
         if ctx.tape is None:
             return y
 
         def bwd():
-            dy = y.grad
+            dy = y.grad.view(N, H, W, Cc)
             self._wg(lambda: ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad))
             do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
             dqkv = ops.attention_bwd(qkv, o, do, lse, T, heads, dh, raw)
             def wgq():
                 if qparts is None:
-                    ops.wgrad(x.t, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
+                    ops.wgrad(x4, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
                 else:
                     for i, l in enumerate(qparts):
-                        ops.wgrad(x.t, dqkv, l.weight.grad, ks=1, pad=0, pro=(a, b, False), db=l.bias.grad,
+                        ops.wgrad(x4, dqkv, l.weight.grad, ks=1, pad=0, pro=(a, b, False), db=l.bias.grad,
                                   dy_offset=i * inner)
             self._wg(wgq)
             dz, s12 = ops.conv(dqkv, Cc, self.wc.get(wq, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W),
-                               ep=(x.t, None, None, None), want_stats=True)
+                               ep=(x4, None, None, None), want_stats=True)
             P, Q, R = ops.gn_bwd_prep(s12, N, T, Cc, norm.num_groups, mr, norm.weight, norm.bias, norm.weight.grad,
                                       norm.bias.grad)
             g, acc = _gdest(x)
-            ops.gn_bwd_apply(dz, x.t, None, P, Q, R, dy, g, acc)
+            ops.gn_bwd_apply(dz, x4, None, P, Q, R, dy, g, acc)
         ctx.tape.append(bwd)
         return y
 
     def head(self, norm, conv: Conv, h: Act, ctx: Ctx):
         """GroupNorm -> SiLU -> 3x3 conv to an fp32 NHWC output with CPAD channels."""
         _check_conv(conv, 3, 1, 1)
-        N, H, W, Cc = h.t.shape
+        N, Cc, sp = h.t.shape[0], h.t.shape[-1], tuple(h.t.shape[1:-1])
+        HW = math.prod(sp)
         K = conv.out_channels
         Kp = max(CPAD, -(-K // 8) * 8)
-        a, b, mr = ops.gn_prep(_stats(h), None, N, H * W, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
-        if Kp == CPAD and ops.head_eligible(H, W, Cc, K):
+        a, b, mr = ops.gn_prep(_stats(h), None, N, HW, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
+        if Kp == CPAD and len(sp) == 2 and ops.head_eligible(*sp, Cc, K):
             # VALU head kernels (csrc/head.hip): the GN/SiLU transform once per element, no MFMA padding
             out = ops.head_fwd(h.t, (a, b), conv.weight, conv.bias, K, Kp)
             if ctx.tape is not None:
@@ -552,7 +570,7 @@ class UNetEngine:
                     self._wg(lambda: ops.head_wgrad(dpred, K, h.t, (a, b), conv.weight.grad,
                                                     conv.bias.grad if conv.bias is not None else None))
                     dz, s12 = ops.head_dgrad(dpred, conv.weight, K, h.t, (a, b))
-                    P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
+                    P, Q, R = ops.gn_bwd_prep(s12, N, HW, Cc, norm.num_groups, mr, norm.weight, norm.bias,
                                               norm.weight.grad, norm.bias.grad)
                     g, acc = _gdest(h)
                     ops.gn_bwd_apply(dz, h.t, None, P, Q, R, None, g, acc)
@@ -564,15 +582,15 @@ class UNetEngine:
         if ctx.tape is not None:
             def bwd(dpred):
                 def wgh():
-                    tmpw = torch.zeros((Kp, Cc, 3, 3), device=out.device, dtype=F32)
+                    tmpw = torch.zeros((Kp, Cc, *conv.weight.shape[2:]), device=out.device, dtype=F32)
                     tmpb = torch.zeros((Kp,), device=out.device, dtype=F32)
                     ops.wgrad(h.t, dpred, tmpw, pro=(a, b, True), db=tmpb, accumulate=False)
                     conv.weight.grad.add_(tmpw[:K])
                     conv.bias.grad.add_(tmpb[:K])
                 self._wg(wgh)
-                dz, s12 = self.dgrad3x3(conv.weight, dpred, Cc, H, W, Kpad=Kp, ep=(h.t, None, a, b),
+                dz, s12 = self.dgrad3x3(conv.weight, dpred, Cc, sp, Kpad=Kp, ep=(h.t, None, a, b),
                                         want_stats=True)
-                P, Q, R = ops.gn_bwd_prep(s12, N, H * W, Cc, norm.num_groups, mr, norm.weight, norm.bias,
+                P, Q, R = ops.gn_bwd_prep(s12, N, HW, Cc, norm.num_groups, mr, norm.weight, norm.bias,
                                           norm.weight.grad, norm.bias.grad)
                 g, acc = _gdest(h)
                 ops.gn_bwd_apply(dz, h.t, None, P, Q, R, None, g, acc)
@@ -764,7 +782,7 @@ class UNetEngine:
 
     # ----------------------------------------------------------- utilities
     def stage_input(self, x: torch.Tensor, context: Optional[torch.Tensor]):
-        """NCHW fp32 (x, optional concat context) -> NHWC bf16 with CPAD-padded channels."""
+        """NC(D)HW fp32 (x, optional concat context) -> N(D)HWC bf16 with CPAD-padded channels."""
         Cin = x.shape[1] + (context.shape[1] if context is not None else 0)
         Cp = max(CPAD, -(-Cin // 8) * 8)
         return ops.noise_prepare(None, x.float().contiguous(), None, None,

@@ -109,18 +109,20 @@ def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, be
 
 def gn_apply_fwd(x0, x1, a, b, silu=True):
     """t = SiLU(a*x + b) over the channel concat of x0|x1 (NHWC bf16): the materialised GN prologue."""
-    N, H, W, C0 = x0.shape
+    N, C0 = x0.shape[0], x0.shape[-1]
+    HW = x0[0, ..., 0].numel()                    # any spatial rank (N, *sp, C)
     C1 = x1.shape[-1] if x1 is not None else 0
-    t = torch.empty((N, H, W, C0 + C1), device=x0.device, dtype=BF16)
-    _lib.call("fmd_gn_apply_fwd", _p(x0), _p(x1), C0, C1, N * H * W, H * W, _p(a), _p(b), int(silu), _p(t), stream())
+    t = torch.empty((*x0.shape[:-1], C0 + C1), device=x0.device, dtype=BF16)
+    _lib.call("fmd_gn_apply_fwd", _p(x0), _p(x1), C0, C1, N * HW, HW, _p(a), _p(b), int(silu), _p(t), stream())
     return t
 
 
 def gn_bwd_apply(dz, x0, x1, P, Q, R, extra, dx0, acc0, dx1=None, acc1=0):
-    N, H, W, Ct = dz.shape
+    N = dz.shape[0]
+    HW = dz[0, ..., 0].numel()                    # any spatial rank (N, *sp, C)
     C0 = x0.shape[-1]
     C1 = x1.shape[-1] if x1 is not None else 0
-    _lib.call("fmd_gn_bwd_apply", _p(dz), _p(x0), _p(x1), C0, C1, N * H * W, H * W, _p(P), _p(Q), _p(R),
+    _lib.call("fmd_gn_bwd_apply", _p(dz), _p(x0), _p(x1), C0, C1, N * HW, HW, _p(P), _p(Q), _p(R),
               _p(extra), _p(dx0), int(acc0), _p(dx1), int(acc1), stream())
 
 
@@ -129,7 +131,9 @@ def conv1x1_gn_apply(dy, wgt_t, dz, x0, x1, P, Q, R, dx0, acc0, dx1=None, acc1=0
     the ResBlock skip-conv data gradient fused into the block input's GroupNorm backward
     (fmd_conv_gn_apply; == conv(..., transposed=True) followed by gn_bwd_apply(extra=...))."""
     _need_cuda(dy, "conv1x1_gn_apply")
-    N, H, W, Kd = dy.shape
+    N, Kd = dy.shape[0], dy.shape[-1]
+    W = dy.shape[-2]
+    H = dy[0, ..., 0, 0].numel()                  # pointwise: a (D, H, W) volume runs as a (D*H, W) plane
     Ct = dz.shape[-1]
     d = ConvDesc()
     d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K = N, H, W, Kd, 0, H, W, Ct

@@ -24,7 +24,7 @@ def fm_timesteps(t: torch.Tensor, num_train_timesteps: int) -> torch.Tensor:
 def fm_loss(sd, spec, clean, ldct, noise, t, num_train_timesteps=1000, grad_accum=1):
     """Forward + loss of one FM chunk; returns (loss, scaled_loss) (flow_matching_lib.py:151-172)."""
     timesteps = fm_timesteps(t, num_train_timesteps)
-    tb = t[:, None, None, None]
+    tb = t.view(-1, *([1] * (clean.dim() - 1)))
     x_t = (1.0 - tb) * clean + tb * noise
     inp = torch.cat([x_t, ldct], dim=1) if ldct is not None else x_t
     pred = U.unet_forward(sd, spec, inp, timesteps)
