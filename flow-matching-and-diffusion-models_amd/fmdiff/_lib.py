@@ -101,6 +101,10 @@ SIGNATURES = {
     "fmd_grouped_linear_bwd": [p, i32, i32, p, p, i32, i32, p, i32, p, i32, p, p],
     "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
     "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_linear_attention_workspace": [i32, i32],
+    "fmd_linear_attention_state": [i32, i32],
+    "fmd_linear_attention_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, p, p],
+    "fmd_linear_attention_bwd": [p, p, p, p, i32, i32, i32, i32, i32, f32, p, p],
     "fmd_noise_prepare": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_mse": [p, i32, p, p, f32, i32, i32, i32, f32, p, i32, p, p, p],
     "fmd_adamw": [p, p, p, p, i64, f32, f32, f32, f32, f32, f32, f32, p],
@@ -114,7 +118,7 @@ SIGNATURES = {
     "fmd_head_wgrad_workspace": [i32, i32, i32, i32, i32],
     "fmd_head_wgrad": [p, i32, p, p, p, i32, i32, i32, i32, p, p, p, p],
 }
-_RESTYPE = {"fmd_wgrad_workspace": i64, "fmd_head_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_grouped_linear_bwd_workspace": i64}
+_RESTYPE = {"fmd_linear_attention_workspace": i64, "fmd_linear_attention_state": i64, "fmd_wgrad_workspace": i64, "fmd_head_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_grouped_linear_bwd_workspace": i64}
 
 _lib = None
 

@@ -506,9 +506,8 @@ class UNetEngine:
         H, W = T // sp[-1], sp[-1]        # 1x1 convs only: a 3-D volume runs as a (D*H, W) plane
         x4 = x.t.view(N, H, W, Cc)
         if isinstance(m, SpatialSelfAttention):
-            if m.use_linear:
-                raise NotImplementedError("LinearQKVAttention is not yet on the fmdiff engine")
             norm, heads, dh, inner, raw = m.norm, m.heads, m.dim_head, m.inner_dim, 1
+            lin = m.attention.eps if m.use_linear else None      # LinearQKVAttention (attention.py:53-70)
             wq = m.qkv.weight
             bq = m.qkv.bias
             wo, bo = m.proj_out.weight, m.proj_out.bias
@@ -521,11 +520,15 @@ class UNetEngine:
             wq = self.wc.fused([l.weight for l in qparts], "w")
             bq = self.wc.fused([l.bias for l in qparts], "b")
             wo, bo = m.to_out[0].weight, m.to_out[0].bias
+            lin = None
         else:
             raise NotImplementedError(type(m).__name__)
         a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
         qkv, _ = ops.conv(x4, 3 * inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
-        o, lse = ops.attention_fwd(qkv, T, heads, dh, raw)
+        if lin is not None:
+            o, lse = ops.linear_attention_fwd(qkv, T, heads, dh, raw, lin)
+        else:
+            o, lse = ops.attention_fwd(qkv, T, heads, dh, raw)
         o4 = o.view(N, H, W, inner)
         out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
         y = Act(out.view(x.t.shape), st)
@@ -536,7 +539,10 @@ class UNetEngine:
             dy = y.grad.view(N, H, W, Cc)
             self._wg(lambda: ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad))
             do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
-            dqkv = ops.attention_bwd(qkv, o, do, lse, T, heads, dh, raw)
+            if lin is not None:
+                dqkv = ops.linear_attention_bwd(qkv, do, lse, T, heads, dh, raw, lin)
+            else:
+                dqkv = ops.attention_bwd(qkv, o, do, lse, T, heads, dh, raw)
             def wgq():
                 if qparts is None:
                     ops.wgrad(x4, dqkv, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)

@@ -512,6 +512,28 @@ def attention_fwd(qkv, T, heads, dh, raw):
     return o, lse
 
 
+def _la_workspace(B, heads, dev):
+    return torch.empty((int(_lib.lib().fmd_linear_attention_workspace(B, heads)),), device=dev, dtype=F32)
+
+
+def linear_attention_fwd(qkv, T, heads, dh, raw, eps=1e-6):
+    """LinearQKVAttention over the fused qkv projection (csrc/attention.hip); returns (o, state)."""
+    B = qkv.shape[0]
+    o = torch.empty((B, T, heads * dh), device=qkv.device, dtype=BF16)
+    state = torch.empty((int(_lib.lib().fmd_linear_attention_state(B, heads)),), device=qkv.device, dtype=F32)
+    _lib.call("fmd_linear_attention_fwd", _p(qkv), B, T, heads, dh, int(raw), float(eps), _p(o), _p(state),
+              _p(_la_workspace(B, heads, qkv.device)), stream())
+    return o, state
+
+
+def linear_attention_bwd(qkv, dout, state, T, heads, dh, raw, eps=1e-6):
+    B = qkv.shape[0]
+    dqkv = torch.empty_like(qkv)
+    _lib.call("fmd_linear_attention_bwd", _p(qkv), _p(dout), _p(state), _p(_la_workspace(B, heads, qkv.device)), B, T,
+              heads, dh, int(raw), float(eps), _p(dqkv), stream())
+    return dqkv
+
+
 def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
     B = qkv.shape[0]
     dqkv = torch.empty_like(qkv)

@@ -247,6 +247,16 @@ int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int3
                       float* lse, fmd_stream_t s);
 int fmd_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, int32_t B,
                       int32_t T, int32_t heads, int32_t dh, int32_t raw, void* dqkv, fmd_stream_t s);
+/* LinearQKVAttention (src/nn/blocks/attention.py:53-70) inside SpatialSelfAttention(use_linear=True)
+ * (attention.py:104-117; same raw head split): out = softmax_d(q) (softmax_tokens(k)^T v / (sum ks + eps)).
+ * ``state`` (fmd_linear_attention_state floats) is written by the forward and read by the backward;
+ * ``ws`` holds fmd_linear_attention_workspace floats. dh <= 64. */
+size_t fmd_linear_attention_workspace(int32_t B, int32_t heads);
+size_t fmd_linear_attention_state(int32_t B, int32_t heads);
+int fmd_linear_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw,
+                             float eps, void* o, float* state, float* ws, fmd_stream_t s);
+int fmd_linear_attention_bwd(const void* qkv, const void* dout, const float* state, float* ws, int32_t B, int32_t T,
+                             int32_t heads, int32_t dh, int32_t raw, float eps, void* dqkv, fmd_stream_t s);
 
 /* ------------------------------------------ train step / sampler / optim
  * FM input x_t = (1-t)x0 + t*eps and DDPM add_noise (flow_matching_lib.py:151-158,

@@ -322,6 +322,30 @@ def test_attention(raw, T, heads, dh):
     _close(dq, f.grad, rel=2e-2)
 
 
+@pytest.mark.parametrize("raw,T,heads,dh", [(1, 256, 4, 64), (1, 4160, 2, 64), (0, 777, 2, 32), (1, 100, 3, 24)])
+def test_linear_attention(raw, T, heads, dh):
+    """LinearQKVAttention (oracle/unet.py _linear_attention, reference attention.py:53-70) vs fp32 autograd;
+    T > 1024 splits the token reductions over several chunks."""
+    from oracle.unet import _linear_attention
+    O = ops()
+    B = 2
+    inner = heads * dh
+    qkv = (torch.randn(B, T, 3 * inner) * 0.7).to(torch.bfloat16)
+    f = qkv.float().requires_grad_()
+    if raw:
+        q, k, v = f.transpose(1, 2).reshape(B, heads, T, 3 * dh).chunk(3, dim=-1)
+    else:
+        q, k, v = (f[..., i * inner:(i + 1) * inner].view(B, T, heads, dh).transpose(1, 2) for i in range(3))
+    o = _linear_attention(q, k, v)
+    o_tok = o.reshape(B, inner, T).transpose(1, 2) if raw else o.transpose(1, 2).reshape(B, T, inner)
+    do = torch.randn_like(o_tok).to(torch.bfloat16).float()
+    o_tok.backward(do)
+    og, state = O.linear_attention_fwd(qkv.to(DEV), T, heads, dh, raw)
+    _close(og, o_tok.detach())
+    dq = O.linear_attention_bwd(qkv.to(DEV), do.contiguous().to(torch.bfloat16).to(DEV), state, T, heads, dh, raw)
+    _close(dq, f.grad, rel=2e-2)
+
+
 def test_time_embedding_and_linear():
     O = ops()
     from oracle.unet import timestep_embedding

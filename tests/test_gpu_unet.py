@@ -154,7 +154,10 @@ def test_fused_train_step_split_capture_matches_full_graph(golden):
 
 UNET3D_CASES = {
     "efficient": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64],
-                      attention_resolutions=[2], use_linear_attn=False, sample_size=16),
+                      attention_resolutions=[2], sample_size=16),
+    # attention at every level (linear attention, use_linear_attn defaults to True) + softmax in the middle
+    "efficient_2d_attn": dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64],
+                              attention_resolutions=[1, 2], sample_size=64),
     "diffusers": dict(unet_impl="diffusers_nd", spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
                       block_out_channels=[32, 64], down_block_types=["DownBlock2D", "AttnDownBlock2D"],
                       up_block_types=["AttnUpBlock2D", "UpBlock2D"], sample_size=16, norm_num_groups=8),
@@ -163,7 +166,7 @@ UNET3D_CASES = {
 
 @pytest.mark.parametrize("impl", list(UNET3D_CASES))
 def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
-    """spatial_dims=3 (NDHWC volumes, 3x3x3 kernels, stride-2 down / nearest-x2 up, self-attention over the
+    """(plus one 2-D case with linear attention at every level)  spatial_dims=3 (NDHWC volumes, 3x3x3 kernels, stride-2 down / nearest-x2 up, self-attention over the
     flattened volume) through the engine's generic implicit-GEMM path vs the oracle's fp32 F.conv3d UNet
     (same tolerances as 2-D).  The reference ships no 3-D golden vectors: the oracle's 3-D path is the 2-D
     restatement (golden-pinned) with conv_nd/pool dispatching on dims."""
@@ -178,7 +181,8 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
     sd = U.seeded_state_dict(spec, 11)
     model.load_state_dict(sd)
     g = torch.Generator().manual_seed(5)
-    clean, ldct, noise = (torch.randn(2, 1, 16, 16, 16, generator=g) for _ in range(3))
+    shape = (2, 1, 64, 64) if cfg.get("spatial_dims", 2) == 2 else (2, 1, 16, 16, 16)
+    clean, ldct, noise = (torch.randn(*shape, generator=g) for _ in range(3))
     t = torch.rand(2, generator=g)
     Ntr = 1000
 
@@ -188,14 +192,14 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
         y = model(x_in.to(DEV), ts.to(DEV), context=None)
     y_ref = U.unet_forward(sd, spec, x_in, ts)
     err = _rel(y, y_ref)
-    print(f"{impl} 3-D forward rel L2 {err:.3e}")
+    print(f"{impl} forward rel L2 {err:.3e}")
     assert err < 2e-2
 
     sdg = {k: v.clone().requires_grad_() for k, v in sd.items()}
     loss_ref, scaled = OT.fm_loss(sdg, spec, clean, ldct, noise, t, Ntr)
     scaled.backward()
     cd, ld, nd, td = clean.to(DEV), ldct.to(DEV), noise.to(DEV), t.to(DEV)
-    tb = td.view(-1, 1, 1, 1, 1)
+    tb = td.view(-1, *([1] * (len(shape) - 1)))
     pred = model((1.0 - tb) * cd + tb * nd, (td * (Ntr - 1)).long(), context=ld)
     loss = F.mse_loss(pred, nd - cd)
     loss.backward()
@@ -212,6 +216,6 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
             if cos < worst[0]:
                 worst = (cos.item(), k)
     rel = math.sqrt(num / den)
-    print(f"{impl} 3-D grad rel L2 {rel:.3e}, worst cosine {worst}")
+    print(f"{impl} grad rel L2 {rel:.3e}, worst cosine {worst}")
     assert rel < 5e-2
     assert worst[0] > 0.99, worst
