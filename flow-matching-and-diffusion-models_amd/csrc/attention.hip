@@ -45,32 +45,91 @@ struct Map {
   }
 };
 
-__global__ __launch_bounds__(64) void attn_fwd_kernel(const bf16r* __restrict__ qkv, Map mp, bf16r* __restrict__ o,
-                                                      float* __restrict__ lse) {
+// q rows [Tq] and k/v rows [Tk] of one batch.  Self-attention reads all three from one qkv buffer
+// [T][3*inner] (cross = 0); SpatialCrossAttention (attention.py:120-189) reads q from the q_proj output
+// [Tq][inner] and k | v from the kv_proj output [Tk][2*inner] (cross = 1), with the same raw head split
+// (q.reshape(b, heads, Tq, dh), kv.reshape(b, heads, Tk, 2*dh).chunk(2)).  which: 0 q, 1 k, 2 v, 3 output.
+struct AGeo {
+  int Tq, Tk, heads, dh, inner, raw, cross;
+  FMD_HD int parts(int which) const { return which == 3 ? 1 : (cross ? (which ? 2 : 1) : 3); }
+  FMD_HD int slot(int which) const { return which == 3 ? 0 : (cross && which ? which - 1 : which); }
+  FMD_HD int rows(int which) const { return (which == 1 || which == 2) ? Tk : Tq; }
+  // element offset inside one batch's buffer (32-bit: the host checks every buffer < 2^32 elements)
+  FMD_DEV unsigned off(int which, int h, int r, int d) const {
+    const unsigned P = parts(which), T = rows(which);
+    if (raw) {
+      const unsigned f = ((unsigned)h * T + r) * P * dh + slot(which) * dh + d;
+      const unsigned c = f / T;
+      return (f - c * T) * P * inner + c;
+    }
+    return (unsigned)r * P * inner + slot(which) * inner + h * dh + d;
+  }
+  FMD_HD size_t qstride() const { return (size_t)Tq * parts(0) * inner; }
+  FMD_HD size_t kvstride() const { return (size_t)Tk * parts(1) * inner; }
+  FMD_HD size_t ostride() const { return (size_t)Tq * inner; }
+  bool fits() const {
+    return qstride() < (1ull << 32) && kvstride() < (1ull << 32) && (size_t)Tq * heads * dh < (1ull << 32);
+  }
+};
+
+// walks consecutive d of one (which, head, row): one division per row instead of one per element
+struct ARow {
+  unsigned t, c, T, ld, off;
+  int raw;
+  FMD_DEV unsigned cur() const { return raw ? t * ld + c : off; }
+  FMD_DEV void next() {
+    if (raw) {
+      if (++t == T) { t = 0; ++c; }
+    } else {
+      ++off;
+    }
+  }
+};
+FMD_DEV ARow arow(const AGeo& g, int which, int h, int r, int d0) {
+  ARow w;
+  w.raw = g.raw;
+  w.T = g.rows(which);
+  w.ld = g.parts(which) * g.inner;
+  if (g.raw) {
+    const unsigned f = ((unsigned)h * w.T + r) * g.parts(which) * g.dh + g.slot(which) * g.dh + d0;
+    w.c = f / w.T;
+    w.t = f - w.c * w.T;
+    w.off = 0;
+  } else {
+    w.t = w.c = 0;
+    w.off = g.off(which, h, r, d0);
+  }
+  return w;
+}
+
+// one wave per 64 query rows; online softmax over 64-key LDS blocks
+__global__ __launch_bounds__(64) void attn_fwd_kernel(const bf16r* __restrict__ qsrc, const bf16r* __restrict__ kvsrc,
+                                                      AGeo g, bf16r* __restrict__ o, float* __restrict__ lse) {
   const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int T = mp.T, dh = mp.dh;
-  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
+  const int Tk = g.Tk, dh = g.dh;
+  const bf16r* qb = qsrc + b * g.qstride();
+  const bf16r* kb = kvsrc + b * g.kvstride();
   const int r = qblk * 64 + threadIdx.x;
-  const bool live = r < T;
+  const bool live = r < g.Tq;
   const float scale = 1.0f / sqrtf((float)dh);
   float q[DMAX], acc[DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
-    q[d] = (live && d < dh) ? bf2f(base[mp.off(0, h, r, d)]) * scale : 0.f;
+    q[d] = (live && d < dh) ? bf2f(qb[g.off(0, h, r, d)]) * scale : 0.f;
     acc[d] = 0.f;
   }
   __shared__ float ks[64][DMAX + 1], vs[64][DMAX + 1];
   float m = -INFINITY, l = 0.f;
-  for (int k0 = 0; k0 < T; k0 += 64) {
+  for (int k0 = 0; k0 < Tk; k0 += 64) {
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * dh; i += 64) {
       const int kr = i / dh, d = i - (i / dh) * dh;
-      const bool ok = k0 + kr < T;
-      ks[kr][d] = ok ? bf2f(base[mp.off(1, h, k0 + kr, d)]) : 0.f;
-      vs[kr][d] = ok ? bf2f(base[mp.off(2, h, k0 + kr, d)]) : 0.f;
+      const bool ok = k0 + kr < Tk;
+      ks[kr][d] = ok ? bf2f(kb[g.off(1, h, k0 + kr, d)]) : 0.f;
+      vs[kr][d] = ok ? bf2f(kb[g.off(2, h, k0 + kr, d)]) : 0.f;
     }
     __syncthreads();
-    const int nk = min(64, T - k0);
+    const int nk = min(64, Tk - k0);
     for (int j = 0; j < nk; ++j) {
       float sc = 0.f;
 #pragma unroll
@@ -88,48 +147,49 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const bf16r* __restrict__ 
   }
   if (!live) return;
   const float inv = 1.f / l;
-  bf16r* ob = o + (size_t)b * T * mp.inner;
+  bf16r* ob = o + b * g.ostride();
 #pragma unroll
   for (int d = 0; d < DMAX; ++d)
-    if (d < dh) ob[mp.ooff(h, r, d)] = (bf16r)f2bf(acc[d] * inv);
-  lse[((size_t)b * mp.heads + h) * T + r] = m + logf(l);
+    if (d < dh) ob[g.off(3, h, r, d)] = (bf16r)f2bf(acc[d] * inv);
+  lse[((size_t)b * g.heads + h) * g.Tq + r] = m + logf(l);
 }
 
 // pass 1 (per query row): delta = sum_d dO*O, dQ = scale * sum_k dS K
-__global__ __launch_bounds__(64) void attn_bwd_q_kernel(const bf16r* __restrict__ qkv, const bf16r* __restrict__ o,
-                                                        const bf16r* __restrict__ dout, const float* __restrict__ lse,
-                                                        Map mp, float* __restrict__ delta,
-                                                        bf16r* __restrict__ dqkv) {
+__global__ __launch_bounds__(64) void attn_bwd_q_kernel(const bf16r* __restrict__ qsrc, const bf16r* __restrict__ kvsrc,
+                                                        const bf16r* __restrict__ o, const bf16r* __restrict__ dout,
+                                                        const float* __restrict__ lse, AGeo g,
+                                                        float* __restrict__ delta, bf16r* __restrict__ dq_out) {
   const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int T = mp.T, dh = mp.dh;
-  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
-  const bf16r* ob = o + (size_t)b * T * mp.inner;
-  const bf16r* dob = dout + (size_t)b * T * mp.inner;
+  const int Tk = g.Tk, dh = g.dh;
+  const bf16r* qb = qsrc + b * g.qstride();
+  const bf16r* kb = kvsrc + b * g.kvstride();
+  const bf16r* ob = o + b * g.ostride();
+  const bf16r* dob = dout + b * g.ostride();
   const int r = qblk * 64 + threadIdx.x;
-  const bool live = r < T;
+  const bool live = r < g.Tq;
   const float scale = 1.0f / sqrtf((float)dh);
   float q[DMAX], dq[DMAX], dov[DMAX];
   float dl = 0.f;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
     const bool ok = live && d < dh;
-    q[d] = ok ? bf2f(base[mp.off(0, h, r, d)]) * scale : 0.f;
-    dov[d] = ok ? bf2f(dob[mp.ooff(h, r, d)]) : 0.f;
-    dl += ok ? dov[d] * bf2f(ob[mp.ooff(h, r, d)]) : 0.f;
+    q[d] = ok ? bf2f(qb[g.off(0, h, r, d)]) * scale : 0.f;
+    dov[d] = ok ? bf2f(dob[g.off(3, h, r, d)]) : 0.f;
+    dl += ok ? dov[d] * bf2f(ob[g.off(3, h, r, d)]) : 0.f;
     dq[d] = 0.f;
   }
-  const float L = live ? lse[((size_t)b * mp.heads + h) * T + r] : 0.f;
+  const float L = live ? lse[((size_t)b * g.heads + h) * g.Tq + r] : 0.f;
   __shared__ float ks[64][DMAX + 1], vs[64][DMAX + 1];
-  for (int k0 = 0; k0 < T; k0 += 64) {
+  for (int k0 = 0; k0 < Tk; k0 += 64) {
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * dh; i += 64) {
       const int kr = i / dh, d = i - (i / dh) * dh;
-      const bool ok = k0 + kr < T;
-      ks[kr][d] = ok ? bf2f(base[mp.off(1, h, k0 + kr, d)]) : 0.f;
-      vs[kr][d] = ok ? bf2f(base[mp.off(2, h, k0 + kr, d)]) : 0.f;
+      const bool ok = k0 + kr < Tk;
+      ks[kr][d] = ok ? bf2f(kb[g.off(1, h, k0 + kr, d)]) : 0.f;
+      vs[kr][d] = ok ? bf2f(kb[g.off(2, h, k0 + kr, d)]) : 0.f;
     }
     __syncthreads();
-    const int nk = min(64, T - k0);
+    const int nk = min(64, Tk - k0);
     for (int j = 0; j < nk; ++j) {
       float sc = 0.f, dp = 0.f;
 #pragma unroll
@@ -143,49 +203,50 @@ __global__ __launch_bounds__(64) void attn_bwd_q_kernel(const bf16r* __restrict_
     }
   }
   if (!live) return;
-  delta[((size_t)b * mp.heads + h) * T + r] = dl;
-  bf16r* db = dqkv + (size_t)b * T * 3 * mp.inner;
+  delta[((size_t)b * g.heads + h) * g.Tq + r] = dl;
+  bf16r* db = dq_out + b * g.qstride();
 #pragma unroll
   for (int d = 0; d < DMAX; ++d)
-    if (d < dh) db[mp.off(0, h, r, d)] = (bf16r)f2bf(dq[d] * scale);
+    if (d < dh) db[g.off(0, h, r, d)] = (bf16r)f2bf(dq[d] * scale);
 }
 
 // pass 2 (per key row): dV = sum_q P dO,  dK = scale * sum_q dS Q
-__global__ __launch_bounds__(64) void attn_bwd_kv_kernel(const bf16r* __restrict__ qkv, const bf16r* __restrict__ dout,
-                                                         const float* __restrict__ lse,
-                                                         const float* __restrict__ delta, Map mp,
-                                                         bf16r* __restrict__ dqkv) {
+__global__ __launch_bounds__(64) void attn_bwd_kv_kernel(const bf16r* __restrict__ qsrc, const bf16r* __restrict__ kvsrc,
+                                                         const bf16r* __restrict__ dout, const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, AGeo g,
+                                                         bf16r* __restrict__ dkv_out) {
   const int kblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int T = mp.T, dh = mp.dh;
-  const bf16r* base = qkv + (size_t)b * T * 3 * mp.inner;
-  const bf16r* dob = dout + (size_t)b * T * mp.inner;
+  const int Tq = g.Tq, dh = g.dh;
+  const bf16r* qb = qsrc + b * g.qstride();
+  const bf16r* kb = kvsrc + b * g.kvstride();
+  const bf16r* dob = dout + b * g.ostride();
   const int r = kblk * 64 + threadIdx.x;
-  const bool live = r < T;
+  const bool live = r < g.Tk;
   const float scale = 1.0f / sqrtf((float)dh);
   float kv[DMAX], vv[DMAX], dk[DMAX], dv[DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
     const bool ok = live && d < dh;
-    kv[d] = ok ? bf2f(base[mp.off(1, h, r, d)]) : 0.f;
-    vv[d] = ok ? bf2f(base[mp.off(2, h, r, d)]) : 0.f;
+    kv[d] = ok ? bf2f(kb[g.off(1, h, r, d)]) : 0.f;
+    vv[d] = ok ? bf2f(kb[g.off(2, h, r, d)]) : 0.f;
     dk[d] = 0.f;
     dv[d] = 0.f;
   }
   __shared__ float qs[64][DMAX + 1], dos[64][DMAX + 1], ls[64], dls[64];
-  for (int q0 = 0; q0 < T; q0 += 64) {
+  for (int q0 = 0; q0 < Tq; q0 += 64) {
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * dh; i += 64) {
       const int qr = i / dh, d = i - (i / dh) * dh;
-      const bool ok = q0 + qr < T;
-      qs[qr][d] = ok ? bf2f(base[mp.off(0, h, q0 + qr, d)]) * scale : 0.f;
-      dos[qr][d] = ok ? bf2f(dob[mp.ooff(h, q0 + qr, d)]) : 0.f;
+      const bool ok = q0 + qr < Tq;
+      qs[qr][d] = ok ? bf2f(qb[g.off(0, h, q0 + qr, d)]) * scale : 0.f;
+      dos[qr][d] = ok ? bf2f(dob[g.off(3, h, q0 + qr, d)]) : 0.f;
     }
-    if (q0 + (int)threadIdx.x < T) {
-      ls[threadIdx.x] = lse[((size_t)b * mp.heads + h) * T + q0 + threadIdx.x];
-      dls[threadIdx.x] = delta[((size_t)b * mp.heads + h) * T + q0 + threadIdx.x];
+    if (q0 + (int)threadIdx.x < Tq) {
+      ls[threadIdx.x] = lse[((size_t)b * g.heads + h) * Tq + q0 + threadIdx.x];
+      dls[threadIdx.x] = delta[((size_t)b * g.heads + h) * Tq + q0 + threadIdx.x];
     }
     __syncthreads();
-    const int nq = min(64, T - q0);
+    const int nq = min(64, Tq - q0);
     for (int j = 0; j < nq; ++j) {
       float sc = 0.f, dp = 0.f;
 #pragma unroll
@@ -199,12 +260,12 @@ __global__ __launch_bounds__(64) void attn_bwd_kv_kernel(const bf16r* __restrict
     }
   }
   if (!live) return;
-  bf16r* db = dqkv + (size_t)b * T * 3 * mp.inner;
+  bf16r* db = dkv_out + b * g.kvstride();
 #pragma unroll
   for (int d = 0; d < DMAX; ++d)
     if (d < dh) {
-      db[mp.off(1, h, r, d)] = (bf16r)f2bf(dk[d]);   // qs already carries the scale
-      db[mp.off(2, h, r, d)] = (bf16r)f2bf(dv[d]);
+      db[g.off(1, h, r, d)] = (bf16r)f2bf(dk[d]);   // qs already carries the scale
+      db[g.off(2, h, r, d)] = (bf16r)f2bf(dv[d]);
     }
 }
 
@@ -473,9 +534,11 @@ extern "C" int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t 
       return (int)hipGetLastError();
     });
   }
-  Map mp{T, heads, dh, heads * dh, raw};
+  const AGeo g{T, T, heads, dh, heads * dh, raw, 0};
+  if (!g.fits()) return -1;
   dim3 grid((T + 63) / 64, heads, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, mp, (bf16r*)o, lse);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)qkv, g,
+                     (bf16r*)o, lse);
   return (int)hipGetLastError();
 }
 
@@ -498,26 +561,28 @@ extern "C" int fmd_attention_bwd(const void* qkv, const void* o, const void* dou
       return (int)hipGetLastError();
     });
   }
-  Map mp{T, heads, dh, heads * dh, raw};
+  const AGeo g{T, T, heads, dh, heads * dh, raw, 0};
+  if (!g.fits()) return -1;
   dim3 grid((T + 63) / 64, heads, B);
-  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)o,
-                     (const bf16r*)dout, lse, mp, delta, (bf16r*)dqkv);
+  hipLaunchKernelGGL(attn_bwd_q_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)qkv,
+                     (const bf16r*)o, (const bf16r*)dout, lse, g, delta, (bf16r*)dqkv);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)dout, lse,
-                     delta, mp, (bf16r*)dqkv);
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)qkv,
+                     (const bf16r*)dout, lse, delta, g, (bf16r*)dqkv);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // Linear attention: LinearQKVAttention (src/nn/blocks/attention.py:53-70) inside
-// SpatialSelfAttention(use_linear=True) (attention.py:104-117, same raw head split as above):
+// SpatialSelfAttention(use_linear=True) (attention.py:104-117) and SpatialCrossAttention(use_linear=True)
+// (attention.py:157-189), same head splits as above (AGeo):
 //   ks = softmax_tokens(k), qs = softmax_d(q), A = ks^T v [dh][dh], s = sum_tokens ks [dh],
 //   ctx = A / (s + eps), out = qs ctx.
-// Token reductions (column softmax statistics, A, s and the backward's dctx) are split over up to
-// LA_MAXCH token chunks per (batch, head) into fp32 partial slabs, reduced by a per-(batch, head)
-// kernel -- no atomics, deterministic.  The backward never needs a second token pass for the
-// column-softmax Jacobian: sum_n ks*dks = sum_e ctx*dctx + ds*s in closed form.
+// Token reductions (column softmax statistics, A, s over the Tk key rows; the backward's dctx over the
+// Tq query rows) are split over up to LA_MAXCH token chunks per (batch, head) into fp32 partial slabs,
+// reduced by a per-(batch, head) kernel -- no atomics, deterministic.  The backward never needs a second
+// token pass for the column-softmax Jacobian: sum_n ks*dks = sum_e ctx*dctx + ds*s in closed form.
 // state per (batch, head): [ctx D*D | M D | Z D | s D] (fp32, kept from forward for backward).
 namespace {
 
@@ -528,85 +593,37 @@ constexpr int LA_STATE = LA_D * LA_D + 3 * LA_D;
 constexpr int LA_PART = LA_D * LA_D + LA_D;
 
 struct LaArgs {
-  Map mp;
-  int nch, per;     // token chunks per (batch, head), tokens per chunk
+  AGeo g;
+  int nchq, perq;   // query-row chunks per (batch, head), rows per chunk
+  int nchk, perk;   // key-row chunks
   float eps;
 };
 
-// 32-bit versions of Map::off / Map::ooff (the host checks T * 3 * inner < 2^32)
-FMD_DEV unsigned la_off(const Map& mp, int which, int h, int r, int d) {
-  if (mp.raw) {
-    const unsigned f = (unsigned)h * mp.T * 3 * mp.dh + (unsigned)r * 3 * mp.dh + which * mp.dh + d;
-    const unsigned c = f / (unsigned)mp.T;
-    return (f - c * mp.T) * 3 * mp.inner + c;
-  }
-  return (unsigned)r * 3 * mp.inner + which * mp.inner + h * mp.dh + d;
-}
-FMD_DEV unsigned la_ooff(const Map& mp, int h, int r, int d) {
-  if (mp.raw) {
-    const unsigned g = (unsigned)h * mp.T * mp.dh + (unsigned)r * mp.dh + d;
-    const unsigned c = g / (unsigned)mp.T;
-    return (g - c * mp.T) * mp.inner + c;
-  }
-  return (unsigned)r * mp.inner + h * mp.dh + d;
+FMD_DEV void la_range(int T, int per, int c, int& n0, int& n1) {
+  n0 = c * per;
+  n1 = min(T, n0 + per);
 }
 
-// walks consecutive d of one (which, head, row): one division per row instead of one per element
-struct LaRow {
-  unsigned t, c, T, ld, off;
-  int raw;
-  FMD_DEV unsigned cur() const { return raw ? t * ld + c : off; }
-  FMD_DEV void next() {
-    if (raw) {
-      if (++t == T) { t = 0; ++c; }
-    } else {
-      ++off;
-    }
-  }
-};
-FMD_DEV LaRow la_row(const Map& mp, int which, int h, int r, int d0, bool out) {
-  LaRow w;
-  w.raw = mp.raw;
-  w.T = mp.T;
-  w.ld = out ? mp.inner : 3 * mp.inner;
-  if (mp.raw) {
-    const unsigned f = out ? (unsigned)h * mp.T * mp.dh + (unsigned)r * mp.dh + d0
-                           : (unsigned)h * mp.T * 3 * mp.dh + (unsigned)r * 3 * mp.dh + which * mp.dh + d0;
-    w.c = f / (unsigned)mp.T;
-    w.t = f - w.c * mp.T;
-    w.off = 0;
-  } else {
-    w.t = w.c = 0;
-    w.off = out ? la_ooff(mp, h, r, d0) : la_off(mp, which, h, r, d0);
-  }
-  return w;
-}
-
-FMD_DEV void la_range(const LaArgs& a, int c, int& n0, int& n1) {
-  n0 = c * a.per;
-  n1 = min(a.mp.T, n0 + a.per);
-}
-
-// partial column max / sum-exp of k over one token chunk: ws[(bh*nch + c)][2][D]
-__global__ __launch_bounds__(256) void la_kstats(const bf16r* __restrict__ qkv, LaArgs a, float* __restrict__ ws) {
+// partial column max / sum-exp of k over one key chunk: ws[(bh*nchk + c)][2][D]
+__global__ __launch_bounds__(256) void la_kstats(const bf16r* __restrict__ kvsrc, LaArgs a, float* __restrict__ ws) {
   const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
-  const Map& mp = a.mp;
-  const bf16r* base = qkv + (size_t)b * mp.T * 3 * mp.inner;
-  const int d = t & 63, g = t >> 6;
+  const AGeo& g = a.g;
+  const bf16r* kb = kvsrc + b * g.kvstride();
+  const int d = t & 63, gi = t >> 6;
   int n0, n1;
-  la_range(a, c, n0, n1);
+  la_range(g.Tk, a.perk, c, n0, n1);
   float m = -INFINITY, z = 0.f;
-  if (d < mp.dh) {
-    for (int n = n0 + g; n < n1; n += 4) {
-      const float x = bf2f(base[la_off(mp, 1, h, n, d)]);
+  if (d < g.dh) {
+    for (int n = n0 + gi; n < n1; n += 4) {
+      const float x = bf2f(kb[g.off(1, h, n, d)]);
       const float mn = fmaxf(m, x);
       z = z * __expf(m - mn) + __expf(x - mn);
       m = mn;
     }
   }
   __shared__ float sm[4][64], sz[4][64];
-  sm[g][d] = m;
-  sz[g][d] = z;
+  sm[gi][d] = m;
+  sz[gi][d] = z;
   __syncthreads();
   if (t < 64) {
     float M = sm[0][t];
@@ -614,52 +631,52 @@ __global__ __launch_bounds__(256) void la_kstats(const bf16r* __restrict__ qkv, 
     float Z = 0.f;
     if (M > -INFINITY)
       for (int i = 0; i < 4; ++i) Z += sz[i][t] * __expf(sm[i][t] - M);
-    float* o = ws + ((size_t)(b * mp.heads + h) * a.nch + c) * 2 * LA_D;
+    float* o = ws + ((size_t)(b * g.heads + h) * a.nchk + c) * 2 * LA_D;
     o[t] = M;
     o[LA_D + t] = Z;
   }
 }
 
 // combine the chunk statistics of one (batch, head) into M, Z (thread t < 64 = column t)
-FMD_DEV void la_combine_stats(const LaArgs& a, const float* st, float& M, float& Z) {
+FMD_DEV void la_combine_stats(int nch, const float* st, float& M, float& Z) {
   const int t = threadIdx.x;
   M = -INFINITY;
-  for (int c = 0; c < a.nch; ++c) M = fmaxf(M, st[(size_t)c * 2 * LA_D + t]);
+  for (int c = 0; c < nch; ++c) M = fmaxf(M, st[(size_t)c * 2 * LA_D + t]);
   Z = 0.f;
-  for (int c = 0; c < a.nch; ++c) {
+  for (int c = 0; c < nch; ++c) {
     const float mc = st[(size_t)c * 2 * LA_D + t];
     if (mc > -INFINITY) Z += st[(size_t)c * 2 * LA_D + LA_D + t] * __expf(mc - M);
   }
 }
 
-// stage ks = exp(k - M)/Z and v rows [LA_SB][D] of tokens [n, n + LA_SB) into LDS (zero padded)
-FMD_DEV void la_stage_kv(const bf16r* base, const Map& mp, int h, int n, int n1, const float* M, const float* Zi,
+// stage ks = exp(k - M)/Z and v rows [LA_SB][D] of key rows [n, n + LA_SB) into LDS (zero padded)
+FMD_DEV void la_stage_kv(const bf16r* kb, const AGeo& g, int h, int n, int n1, const float* M, const float* Zi,
                          float* ks, float* vs) {
   for (int e = threadIdx.x; e < LA_SB * LA_D; e += blockDim.x) {
     const int j = e >> 6, d = e & 63, r = n + j;
     float kv = 0.f, vv = 0.f;
-    if (r < n1 && d < mp.dh) {
-      kv = __expf(bf2f(base[la_off(mp, 1, h, r, d)]) - M[d]) * Zi[d];
-      vv = bf2f(base[la_off(mp, 2, h, r, d)]);
+    if (r < n1 && d < g.dh) {
+      kv = __expf(bf2f(kb[g.off(1, h, r, d)]) - M[d]) * Zi[d];
+      vv = bf2f(kb[g.off(2, h, r, d)]);
     }
     ks[e] = kv;
-    if (vs) vs[e] = vv;
+    vs[e] = vv;
   }
 }
 
-// partial A = ks^T v and s = sum ks over one token chunk: ws_part[(bh*nch + c)][D*D + D]
-__global__ __launch_bounds__(256) void la_ctx_part(const bf16r* __restrict__ qkv, LaArgs a,
+// partial A = ks^T v and s = sum ks over one key chunk: ws_part[(bh*nchk + c)][D*D + D]
+__global__ __launch_bounds__(256) void la_ctx_part(const bf16r* __restrict__ kvsrc, LaArgs a,
                                                     const float* __restrict__ wstat, float* __restrict__ state,
                                                     float* __restrict__ part) {
   const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
-  const Map& mp = a.mp;
-  const int bh = b * mp.heads + h;
-  const bf16r* base = qkv + (size_t)b * mp.T * 3 * mp.inner;
+  const AGeo& g = a.g;
+  const int bh = b * g.heads + h;
+  const bf16r* kb = kvsrc + b * g.kvstride();
   __shared__ float M[LA_D], Zi[LA_D];
   __shared__ __attribute__((aligned(16))) float ks[LA_SB * LA_D], vs[LA_SB * LA_D];
   if (t < 64) {
     float m, z;
-    la_combine_stats(a, wstat + (size_t)bh * a.nch * 2 * LA_D, m, z);
+    la_combine_stats(a.nchk, wstat + (size_t)bh * a.nchk * 2 * LA_D, m, z);
     M[t] = m;
     Zi[t] = z > 0.f ? 1.f / z : 0.f;
     if (c == 0) {
@@ -669,12 +686,12 @@ __global__ __launch_bounds__(256) void la_ctx_part(const bf16r* __restrict__ qkv
   }
   __syncthreads();
   int n0, n1;
-  la_range(a, c, n0, n1);
+  la_range(g.Tk, a.perk, c, n0, n1);
   const int di = t >> 4, ei = t & 15;
   float acc[4][4] = {};
   float ssum = 0.f;
   for (int n = n0; n < n1; n += LA_SB) {
-    la_stage_kv(base, mp, h, n, n1, M, Zi, ks, vs);
+    la_stage_kv(kb, g, h, n, n1, M, Zi, ks, vs);
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < LA_SB; ++j) {
@@ -690,7 +707,7 @@ __global__ __launch_bounds__(256) void la_ctx_part(const bf16r* __restrict__ qkv
       for (int j = 0; j < LA_SB; ++j) ssum += ks[j * LA_D + t];
     __syncthreads();
   }
-  float* o = part + ((size_t)bh * a.nch + c) * LA_PART;
+  float* o = part + ((size_t)bh * a.nchk + c) * LA_PART;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     *(float4*)&o[(4 * di + i) * LA_D + 4 * ei] = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
@@ -701,28 +718,29 @@ __global__ __launch_bounds__(256) void la_ctx_part(const bf16r* __restrict__ qkv
 __global__ __launch_bounds__(256) void la_ctx_reduce(LaArgs a, const float* __restrict__ part,
                                                       float* __restrict__ state) {
   const int h = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  const int bh = b * a.mp.heads + h;
-  const float* p = part + (size_t)bh * a.nch * LA_PART;
+  const int bh = b * a.g.heads + h;
+  const float* p = part + (size_t)bh * a.nchk * LA_PART;
   float* st = state + (size_t)bh * LA_STATE;
   const int d = t >> 2, e0 = (t & 3) * 16;
   float s = 0.f;
-  for (int c = 0; c < a.nch; ++c) s += p[(size_t)c * LA_PART + LA_D * LA_D + d];
+  for (int c = 0; c < a.nchk; ++c) s += p[(size_t)c * LA_PART + LA_D * LA_D + d];
   const float inv = 1.f / (s + a.eps);
   for (int e = e0; e < e0 + 16; ++e) {
     float A = 0.f;
-    for (int c = 0; c < a.nch; ++c) A += p[(size_t)c * LA_PART + d * LA_D + e];
+    for (int c = 0; c < a.nchk; ++c) A += p[(size_t)c * LA_PART + d * LA_D + e];
     st[d * LA_D + e] = A * inv;
   }
   if ((t & 3) == 0) st[LA_D * LA_D + 2 * LA_D + d] = s;
 }
 
-// 4 lanes per token, 16 dims each: softmax_d(q) of the token -> LDS (fp32, zero padded)
-FMD_DEV void la_q_softmax(const bf16r* base, const Map& mp, int h, int r, bool live, int d0, float* qv, float* qs_row) {
+// 4 lanes per query row, 16 dims each: softmax_d(q) of the row -> LDS (fp32, zero padded)
+FMD_DEV void la_q_softmax(const bf16r* qb, const AGeo& g, int h, int r, bool live, int d0, float* qv,
+                          float* qs_row) {
   float m = -INFINITY;
-  LaRow w = la_row(mp, 0, h, live ? r : 0, d0, false);
+  ARow w = arow(g, 0, h, live ? r : 0, d0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    qv[i] = (live && d0 + i < mp.dh) ? bf2f(base[w.cur()]) : -INFINITY;
+    qv[i] = (live && d0 + i < g.dh) ? bf2f(qb[w.cur()]) : -INFINITY;
     w.next();
     m = fmaxf(m, qv[i]);
   }
@@ -731,7 +749,7 @@ FMD_DEV void la_q_softmax(const bf16r* base, const Map& mp, int h, int r, bool l
   float z = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    qv[i] = (live && d0 + i < mp.dh) ? __expf(qv[i] - m) : 0.f;
+    qv[i] = (live && d0 + i < g.dh) ? __expf(qv[i] - m) : 0.f;
     z += qv[i];
   }
   z += __shfl_xor(z, 1);
@@ -744,20 +762,19 @@ FMD_DEV void la_q_softmax(const bf16r* base, const Map& mp, int h, int r, bool l
   }
 }
 
-// out[n][e] = sum_d softmax_d(q[n])[d] * ctx[d][e]; 64 tokens per workgroup, 4 lanes per token
-__global__ __launch_bounds__(256) void la_out(const bf16r* __restrict__ qkv, LaArgs a, const float* __restrict__ state,
-                                              bf16r* __restrict__ o) {
+// out[n][e] = sum_d softmax_d(q[n])[d] * ctx[d][e]; 64 query rows per workgroup, 4 lanes per row
+__global__ __launch_bounds__(256) void la_out(const bf16r* __restrict__ qsrc, LaArgs a,
+                                              const float* __restrict__ state, bf16r* __restrict__ o) {
   const int h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
-  const Map& mp = a.mp;
-  const int bh = b * mp.heads + h, dh = mp.dh;
+  const AGeo& g = a.g;
+  const int bh = b * g.heads + h, dh = g.dh;
   __shared__ __attribute__((aligned(16))) float ctx[LA_D * LA_D], qs[LA_SB * LA_D];
   for (int e = t; e < LA_D * LA_D; e += 256) ctx[e] = state[(size_t)bh * LA_STATE + e];
   const int j = t >> 2, q0 = (t & 3) * 16;
   const int r = blockIdx.x * LA_SB + j;
-  const bool live = r < mp.T;
-  const bf16r* base = qkv + (size_t)b * mp.T * 3 * mp.inner;
+  const bool live = r < g.Tq;
   float qv[16];
-  la_q_softmax(base, mp, h, r, live, q0, qv, &qs[j * LA_D]);
+  la_q_softmax(qsrc + b * g.qstride(), g, h, r, live, q0, qv, &qs[j * LA_D]);
   __syncthreads();
   if (!live) return;
   float acc[16] = {};
@@ -772,8 +789,8 @@ __global__ __launch_bounds__(256) void la_out(const bf16r* __restrict__ qkv, LaA
       acc[i + 3] += qd * cv.w;
     }
   }
-  bf16r* ob = o + (size_t)b * mp.T * mp.inner;
-  LaRow w = la_row(mp, 0, h, r, q0, true);
+  bf16r* ob = o + b * g.ostride();
+  ARow w = arow(g, 3, h, r, q0);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (q0 + i < dh) ob[w.cur()] = (bf16r)f2bf(acc[i]);
@@ -781,33 +798,33 @@ __global__ __launch_bounds__(256) void la_out(const bf16r* __restrict__ qkv, LaA
   }
 }
 
-// backward, query side, per token chunk: dq (softmax_d Jacobian) and the partial dctx = qs^T dout
-__global__ __launch_bounds__(256) void la_bwd_q(const bf16r* __restrict__ qkv, const bf16r* __restrict__ dout, LaArgs a,
-                                                const float* __restrict__ state, float* __restrict__ part,
-                                                bf16r* __restrict__ dqkv) {
+// backward, query side, per query chunk: dq (softmax_d Jacobian) and the partial dctx = qs^T dout
+__global__ __launch_bounds__(256) void la_bwd_q(const bf16r* __restrict__ qsrc, const bf16r* __restrict__ dout,
+                                                LaArgs a, const float* __restrict__ state, float* __restrict__ part,
+                                                bf16r* __restrict__ dq_out) {
   const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
-  const Map& mp = a.mp;
-  const int bh = b * mp.heads + h, dh = mp.dh;
-  const bf16r* base = qkv + (size_t)b * mp.T * 3 * mp.inner;
-  const bf16r* dob = dout + (size_t)b * mp.T * mp.inner;
-  bf16r* dbase = dqkv + (size_t)b * mp.T * 3 * mp.inner;
+  const AGeo& g = a.g;
+  const int bh = b * g.heads + h, dh = g.dh;
+  const bf16r* qb = qsrc + b * g.qstride();
+  const bf16r* dob = dout + b * g.ostride();
+  bf16r* dqb = dq_out + b * g.qstride();
   __shared__ __attribute__((aligned(16))) float ctx[LA_D * LA_D], qs[LA_SB * LA_D], dos[LA_SB * LA_D];
   for (int e = t; e < LA_D * LA_D; e += 256) ctx[e] = state[(size_t)bh * LA_STATE + e];
   int n0, n1;
-  la_range(a, c, n0, n1);
-  const int j = t >> 2, d0 = (t & 3) * 16;   // phase 1: 4 lanes per token, 16 dims each
+  la_range(g.Tq, a.perq, c, n0, n1);
+  const int j = t >> 2, d0 = (t & 3) * 16;   // phase 1: 4 lanes per row, 16 dims each
   const int di = t >> 4, ei = t & 15;       // phase 2: 4x4 tile of dctx
   float acc[4][4] = {};
   for (int n = n0; n < n1; n += LA_SB) {
     __syncthreads();
     for (int e = t; e < LA_SB * LA_D; e += 256) {
       const int jj = e >> 6, dd = e & 63, r = n + jj;
-      dos[e] = (r < n1 && dd < dh) ? bf2f(dob[la_ooff(mp, h, r, dd)]) : 0.f;
+      dos[e] = (r < n1 && dd < dh) ? bf2f(dob[g.off(3, h, r, dd)]) : 0.f;
     }
     const int r = n + j;
     const bool live = r < n1;
     float qv[16];
-    la_q_softmax(base, mp, h, r, live, d0, qv, &qs[j * LA_D]);
+    la_q_softmax(qb, g, h, r, live, d0, qv, &qs[j * LA_D]);
     __syncthreads();
     // dqs[d] = sum_e dout[e] ctx[d][e]; dq = qs * (dqs - sum_d qs*dqs)
     float dq[16];
@@ -826,10 +843,10 @@ __global__ __launch_bounds__(256) void la_bwd_q(const bf16r* __restrict__ qkv, c
     dot += __shfl_xor(dot, 1);
     dot += __shfl_xor(dot, 2);
     if (live) {
-      LaRow w = la_row(mp, 0, h, r, d0, false);
+      ARow w = arow(g, 0, h, r, d0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        if (d0 + i < dh) dbase[w.cur()] = (bf16r)f2bf(qv[i] * (dq[i] - dot));
+        if (d0 + i < dh) dqb[w.cur()] = (bf16r)f2bf(qv[i] * (dq[i] - dot));
         w.next();
       }
     }
@@ -844,7 +861,7 @@ __global__ __launch_bounds__(256) void la_bwd_q(const bf16r* __restrict__ qkv, c
         for (int k2 = 0; k2 < 4; ++k2) acc[i][k2] += q4[i] * d4[k2];
     }
   }
-  float* o = part + ((size_t)bh * a.nch + c) * LA_PART;
+  float* o = part + ((size_t)bh * a.nchq + c) * LA_PART;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     *(float4*)&o[(4 * di + i) * LA_D + 4 * ei] = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
@@ -855,8 +872,8 @@ __global__ __launch_bounds__(256) void la_bwd_q(const bf16r* __restrict__ qkv, c
 __global__ __launch_bounds__(256) void la_bwd_reduce(LaArgs a, const float* __restrict__ part,
                                                       const float* __restrict__ state, float* __restrict__ tail) {
   const int h = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  const int bh = b * a.mp.heads + h;
-  const float* p = part + (size_t)bh * a.nch * LA_PART;
+  const int bh = b * a.g.heads + h;
+  const float* p = part + (size_t)bh * a.nchq * LA_PART;
   const float* st = state + (size_t)bh * LA_STATE;
   float* o = tail + (size_t)bh * (LA_D * LA_D + 2 * LA_D);
   const int d = t >> 2, e0 = (t & 3) * 16;
@@ -864,10 +881,10 @@ __global__ __launch_bounds__(256) void la_bwd_reduce(LaArgs a, const float* __re
   const float inv = 1.f / (s + a.eps);
   float P = 0.f;
   for (int e = e0; e < e0 + 16; ++e) {
-    float g = 0.f;
-    for (int c = 0; c < a.nch; ++c) g += p[(size_t)c * LA_PART + d * LA_D + e];
-    o[d * LA_D + e] = g * inv;
-    P += g * st[d * LA_D + e];
+    float gsum = 0.f;
+    for (int c = 0; c < a.nchq; ++c) gsum += p[(size_t)c * LA_PART + d * LA_D + e];
+    o[d * LA_D + e] = gsum * inv;
+    P += gsum * st[d * LA_D + e];
   }
   P += __shfl_xor(P, 1);
   P += __shfl_xor(P, 2);
@@ -878,15 +895,15 @@ __global__ __launch_bounds__(256) void la_bwd_reduce(LaArgs a, const float* __re
   }
 }
 
-// backward, key/value side, per token chunk: dv = ks dA, dk = ks * (v dA^T + ds - cc)
-__global__ __launch_bounds__(256) void la_bwd_kv(const bf16r* __restrict__ qkv, LaArgs a,
+// backward, key/value side, per key chunk: dv = ks dA, dk = ks * (v dA^T + ds - cc)
+__global__ __launch_bounds__(256) void la_bwd_kv(const bf16r* __restrict__ kvsrc, LaArgs a,
                                                  const float* __restrict__ state, const float* __restrict__ tail,
-                                                 bf16r* __restrict__ dqkv) {
+                                                 bf16r* __restrict__ dkv_out) {
   const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
-  const Map& mp = a.mp;
-  const int bh = b * mp.heads + h, dh = mp.dh;
-  const bf16r* base = qkv + (size_t)b * mp.T * 3 * mp.inner;
-  bf16r* dbase = dqkv + (size_t)b * mp.T * 3 * mp.inner;
+  const AGeo& g = a.g;
+  const int bh = b * g.heads + h, dh = g.dh;
+  const bf16r* kb = kvsrc + b * g.kvstride();
+  bf16r* dkb = dkv_out + b * g.kvstride();
   __shared__ __attribute__((aligned(16))) float dA[LA_D * LA_D], ks[LA_SB * LA_D], vs[LA_SB * LA_D];
   __shared__ float M[LA_D], Zi[LA_D], dsv[LA_D], cc[LA_D];
   const float* tb = tail + (size_t)bh * (LA_D * LA_D + 2 * LA_D);
@@ -900,10 +917,10 @@ __global__ __launch_bounds__(256) void la_bwd_kv(const bf16r* __restrict__ qkv, 
   }
   __syncthreads();
   int n0, n1;
-  la_range(a, c, n0, n1);
+  la_range(g.Tk, a.perk, c, n0, n1);
   const int j = t >> 2, q0 = (t & 3) * 16;
   for (int n = n0; n < n1; n += LA_SB) {
-    la_stage_kv(base, mp, h, n, n1, M, Zi, ks, vs);
+    la_stage_kv(kb, g, h, n, n1, M, Zi, ks, vs);
     __syncthreads();
     const int r = n + j;
     if (r < n1) {
@@ -912,29 +929,29 @@ __global__ __launch_bounds__(256) void la_bwd_kv(const bf16r* __restrict__ qkv, 
         const float kd = ks[j * LA_D + d];
 #pragma unroll
         for (int i = 0; i < 16; i += 4) {
-          const float4 g = *(const float4*)&dA[d * LA_D + q0 + i];
-          dv[i] += kd * g.x;
-          dv[i + 1] += kd * g.y;
-          dv[i + 2] += kd * g.z;
-          dv[i + 3] += kd * g.w;
+          const float4 gg = *(const float4*)&dA[d * LA_D + q0 + i];
+          dv[i] += kd * gg.x;
+          dv[i + 1] += kd * gg.y;
+          dv[i + 2] += kd * gg.z;
+          dv[i + 3] += kd * gg.w;
         }
       }
 #pragma unroll 2
       for (int i = 0; i < 16; ++i) {          // dks[d] = sum_e v[e] dA[d][e]
         float sacc = 0.f;
         for (int e = 0; e < LA_D; e += 4) {
-          const float4 g = *(const float4*)&dA[(q0 + i) * LA_D + e];
+          const float4 gg = *(const float4*)&dA[(q0 + i) * LA_D + e];
           const float4 vv = *(const float4*)&vs[j * LA_D + e];
-          sacc += g.x * vv.x + g.y * vv.y + g.z * vv.z + g.w * vv.w;
+          sacc += gg.x * vv.x + gg.y * vv.y + gg.z * vv.z + gg.w * vv.w;
         }
         dk[i] = ks[j * LA_D + q0 + i] * (sacc + dsv[q0 + i] - cc[q0 + i]);
       }
-      LaRow wk = la_row(mp, 1, h, r, q0, false), wv = la_row(mp, 2, h, r, q0, false);
+      ARow wk = arow(g, 1, h, r, q0), wv = arow(g, 2, h, r, q0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         if (q0 + i < dh) {
-          dbase[wk.cur()] = (bf16r)f2bf(dk[i]);
-          dbase[wv.cur()] = (bf16r)f2bf(dv[i]);
+          dkb[wk.cur()] = (bf16r)f2bf(dk[i]);
+          dkb[wv.cur()] = (bf16r)f2bf(dv[i]);
         }
         wk.next();
         wv.next();
@@ -944,13 +961,44 @@ __global__ __launch_bounds__(256) void la_bwd_kv(const bf16r* __restrict__ qkv, 
   }
 }
 
-LaArgs la_args(int32_t T, int32_t heads, int32_t dh, int32_t raw, float eps) {
+LaArgs la_args(const AGeo& g, float eps) {
   LaArgs a;
-  a.mp = Map{T, heads, dh, heads * dh, raw};
-  a.nch = std::min(LA_MAXCH, std::max(1, (T + 1023) / 1024));
-  a.per = (T + a.nch - 1) / a.nch;
+  a.g = g;
+  a.nchq = std::min(LA_MAXCH, std::max(1, (g.Tq + 1023) / 1024));
+  a.perq = (g.Tq + a.nchq - 1) / a.nchq;
+  a.nchk = std::min(LA_MAXCH, std::max(1, (g.Tk + 1023) / 1024));
+  a.perk = (g.Tk + a.nchk - 1) / a.nchk;
   a.eps = eps;
   return a;
+}
+
+bool geo_ok(const AGeo& g) {
+  return g.dh >= 1 && g.dh <= LA_D && g.Tq >= 1 && g.Tk >= 1 && g.heads >= 1 && g.fits();
+}
+
+int la_fwd(const bf16r* q, const bf16r* kv, const AGeo& g, int B, float eps, bf16r* o, float* state, float* ws,
+           hipStream_t s) {
+  const LaArgs a = la_args(g, eps);
+  float* part = ws;
+  float* wstat = ws + (size_t)B * g.heads * LA_MAXCH * LA_PART;
+  const dim3 gk(a.nchk, g.heads, B);
+  hipLaunchKernelGGL(la_kstats, gk, dim3(256), 0, s, kv, a, wstat);
+  hipLaunchKernelGGL(la_ctx_part, gk, dim3(256), 0, s, kv, a, (const float*)wstat, state, part);
+  hipLaunchKernelGGL(la_ctx_reduce, dim3(g.heads, B), dim3(256), 0, s, a, (const float*)part, state);
+  hipLaunchKernelGGL(la_out, dim3((g.Tq + LA_SB - 1) / LA_SB, g.heads, B), dim3(256), 0, s, q, a,
+                     (const float*)state, o);
+  return (int)hipGetLastError();
+}
+
+int la_bwd(const bf16r* q, const bf16r* kv, const bf16r* dout, const AGeo& g, int B, float eps, const float* state,
+           float* ws, bf16r* dq, bf16r* dkv, hipStream_t s) {
+  const LaArgs a = la_args(g, eps);
+  float* part = ws;
+  float* tail = ws + (size_t)B * g.heads * ((size_t)LA_MAXCH * (LA_PART + 2 * LA_D));
+  hipLaunchKernelGGL(la_bwd_q, dim3(a.nchq, g.heads, B), dim3(256), 0, s, q, dout, a, state, part, dq);
+  hipLaunchKernelGGL(la_bwd_reduce, dim3(g.heads, B), dim3(256), 0, s, a, (const float*)part, state, tail);
+  hipLaunchKernelGGL(la_bwd_kv, dim3(a.nchk, g.heads, B), dim3(256), 0, s, kv, a, state, (const float*)tail, dkv);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -965,32 +1013,49 @@ extern "C" size_t fmd_linear_attention_state(int32_t B, int32_t heads) { return 
 
 extern "C" int fmd_linear_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw,
                                         float eps, void* o, float* state, float* ws, fmd_stream_t s) {
-  if (dh > LA_D || dh < 1 || T < 1 || B < 1 || heads < 1 || (size_t)T * 3 * heads * dh >= (1ull << 32)) return -1;
-  const LaArgs a = la_args(T, heads, dh, raw, eps);
-  float* part = ws;
-  float* wstat = ws + (size_t)B * heads * LA_MAXCH * LA_PART;
-  const dim3 gc(a.nch, heads, B);
-  hipLaunchKernelGGL(la_kstats, gc, dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, a, wstat);
-  hipLaunchKernelGGL(la_ctx_part, gc, dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, a, (const float*)wstat, state,
-                     part);
-  hipLaunchKernelGGL(la_ctx_reduce, dim3(heads, B), dim3(256), 0, (hipStream_t)s, a, (const float*)part, state);
-  hipLaunchKernelGGL(la_out, dim3((T + LA_SB - 1) / LA_SB, heads, B), dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, a,
-                     (const float*)state, (bf16r*)o);
-  return (int)hipGetLastError();
+  const AGeo g{T, T, heads, dh, heads * dh, raw, 0};
+  if (B < 1 || !geo_ok(g)) return -1;
+  return la_fwd((const bf16r*)qkv, (const bf16r*)qkv, g, B, eps, (bf16r*)o, state, ws, (hipStream_t)s);
 }
 
 extern "C" int fmd_linear_attention_bwd(const void* qkv, const void* dout, const float* state, float* ws, int32_t B,
                                         int32_t T, int32_t heads, int32_t dh, int32_t raw, float eps, void* dqkv,
                                         fmd_stream_t s) {
-  if (dh > LA_D || dh < 1 || T < 1 || B < 1 || heads < 1 || (size_t)T * 3 * heads * dh >= (1ull << 32)) return -1;
-  const LaArgs a = la_args(T, heads, dh, raw, eps);
-  float* part = ws;
-  float* tail = ws + (size_t)B * heads * ((size_t)LA_MAXCH * (LA_PART + 2 * LA_D));
-  const dim3 gc(a.nch, heads, B);
-  hipLaunchKernelGGL(la_bwd_q, gc, dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)dout, a, state, part,
-                     (bf16r*)dqkv);
-  hipLaunchKernelGGL(la_bwd_reduce, dim3(heads, B), dim3(256), 0, (hipStream_t)s, a, (const float*)part, state, tail);
-  hipLaunchKernelGGL(la_bwd_kv, gc, dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, a, state, (const float*)tail,
-                     (bf16r*)dqkv);
+  const AGeo g{T, T, heads, dh, heads * dh, raw, 0};
+  if (B < 1 || !geo_ok(g)) return -1;
+  return la_bwd((const bf16r*)qkv, (const bf16r*)qkv, (const bf16r*)dout, g, B, eps, state, ws, (bf16r*)dqkv,
+                (bf16r*)dqkv, (hipStream_t)s);
+}
+
+// cross-attention (SpatialCrossAttention): q [B][Tq][inner], kv [B][Tk][2*inner]; linear = LinearQKVAttention
+// (state / ws as above), else softmax (lse [B][heads][Tq]; the backward's delta has the same shape)
+extern "C" int fmd_cross_attention_fwd(const void* q, const void* kv, int32_t B, int32_t Tq, int32_t Tk,
+                                       int32_t heads, int32_t dh, int32_t raw, int32_t linear, float eps, void* o,
+                                       float* lse_or_state, float* ws, fmd_stream_t s) {
+  const AGeo g{Tq, Tk, heads, dh, heads * dh, raw, 1};
+  if (B < 1 || !geo_ok(g)) return -1;
+  if (linear)
+    return la_fwd((const bf16r*)q, (const bf16r*)kv, g, B, eps, (bf16r*)o, lse_or_state, ws, (hipStream_t)s);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Tq + 63) / 64, heads, B), dim3(64), 0, (hipStream_t)s, (const bf16r*)q,
+                     (const bf16r*)kv, g, (bf16r*)o, lse_or_state);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_cross_attention_bwd(const void* q, const void* kv, const void* o, const void* dout,
+                                       const float* lse_or_state, float* ws_or_delta, int32_t B, int32_t Tq,
+                                       int32_t Tk, int32_t heads, int32_t dh, int32_t raw, int32_t linear, float eps,
+                                       void* dq, void* dkv, fmd_stream_t s) {
+  const AGeo g{Tq, Tk, heads, dh, heads * dh, raw, 1};
+  if (B < 1 || !geo_ok(g)) return -1;
+  if (linear)
+    return la_bwd((const bf16r*)q, (const bf16r*)kv, (const bf16r*)dout, g, B, eps, lse_or_state, ws_or_delta,
+                  (bf16r*)dq, (bf16r*)dkv, (hipStream_t)s);
+  const dim3 gq((Tq + 63) / 64, heads, B), gk((Tk + 63) / 64, heads, B);
+  hipLaunchKernelGGL(attn_bwd_q_kernel, gq, dim3(64), 0, (hipStream_t)s, (const bf16r*)q, (const bf16r*)kv,
+                     (const bf16r*)o, (const bf16r*)dout, lse_or_state, g, ws_or_delta, (bf16r*)dq);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, gk, dim3(64), 0, (hipStream_t)s, (const bf16r*)q, (const bf16r*)kv,
+                     (const bf16r*)dout, lse_or_state, (const float*)ws_or_delta, g, (bf16r*)dkv);
   return (int)hipGetLastError();
 }

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #define FMD_DEV __device__ __forceinline__
+#define FMD_HD __host__ __device__ __forceinline__
 
 typedef uint16_t bf16r;                                           // raw bf16 bits in memory
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;        // MFMA A/B fragment (4 VGPR)

@@ -419,3 +419,97 @@ extern "C" int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int3
                      (const bf16r*)x1, C0, C1, (long long)M, HW, a, b, silu, (bf16r*)t);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// SpatialCrossAttention's context_norm (src/nn/blocks/attention.py:150-151, :177): GroupNorm over the
+// flattened context (few channels: the 4-channel VAE latent of configs/LDCT/PixelAttention) straight from
+// its fp32 (N, C, Tc) channel-major or (N, Tc, C) token-major layout into the token-major bf16
+// [N][Tc][Cpad] operand of the kv 1x1 projection (channels >= C zero); mean / rstd per (sample, group)
+// are kept for the gamma / beta gradient.  The context is conditioning data: no gradient flows into it.
+namespace {
+
+FMD_DEV float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+FMD_DEV float ctx_at(const float* x, size_t base, int C, int T, int tok_major, int c, int r) {
+  return tok_major ? x[base + (size_t)r * C + c] : x[base + (size_t)c * T + r];
+}
+
+__global__ __launch_bounds__(256) void ctx_norm_fwd_kernel(const float* __restrict__ x, int C, int T, int tok_major,
+                                                           int G, float eps, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int Cpad,
+                                                           bf16r* __restrict__ out, float* __restrict__ mr) {
+  const int g = blockIdx.x, n = blockIdx.y, t = threadIdx.x;
+  __shared__ float red[4];
+  const int Cg = C / G, cnt = Cg * T;
+  const size_t base = (size_t)n * C * T;
+  float s = 0.f;
+  for (int i = t; i < cnt; i += 256) s += ctx_at(x, base, C, T, tok_major, g * Cg + i / T, i % T);
+  const float mean = block_sum256(s, red) / cnt;
+  float v = 0.f;
+  for (int i = t; i < cnt; i += 256) {
+    const float d = ctx_at(x, base, C, T, tok_major, g * Cg + i / T, i % T) - mean;
+    v += d * d;
+  }
+  const float rstd = rsqrtf(block_sum256(v, red) / cnt + eps);
+  for (int i = t; i < cnt; i += 256) {
+    const int c = g * Cg + i / T, r = i % T;
+    const float y = (ctx_at(x, base, C, T, tok_major, c, r) - mean) * rstd * gamma[c] + beta[c];
+    out[((size_t)n * T + r) * Cpad + c] = (bf16r)f2bf(y);
+  }
+  if (g == 0)
+    for (int i = t; i < (Cpad - C) * T; i += 256) out[((size_t)n * T + i / (Cpad - C)) * Cpad + C + i % (Cpad - C)] = 0;
+  if (t == 0) {
+    mr[(n * G + g) * 2] = mean;
+    mr[(n * G + g) * 2 + 1] = rstd;
+  }
+}
+
+// dgamma[c] += sum dY * xhat, dbeta[c] += sum dY over all samples and tokens (one workgroup per channel)
+__global__ __launch_bounds__(256) void ctx_norm_bwd_kernel(const float* __restrict__ x, int N, int C, int T,
+                                                           int tok_major, int G, const float* __restrict__ mr,
+                                                           const bf16r* __restrict__ dy, int Cpad,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  __shared__ float red[4];
+  const int g = c / (C / G);
+  float sg = 0.f, sb = 0.f;
+  for (long long i = t; i < (long long)N * T; i += 256) {
+    const int n = (int)(i / T), r = (int)(i % T);
+    const float d = bf2f(dy[((size_t)n * T + r) * Cpad + c]);
+    const float xh = (ctx_at(x, (size_t)n * C * T, C, T, tok_major, c, r) - mr[(n * G + g) * 2]) * mr[(n * G + g) * 2 + 1];
+    sg += d * xh;
+    sb += d;
+  }
+  sg = block_sum256(sg, red);
+  sb = block_sum256(sb, red);
+  if (t == 0) {
+    dgamma[c] += sg;
+    dbeta[c] += sb;
+  }
+}
+
+}  // namespace
+
+extern "C" int fmd_context_norm_fwd(const float* ctx, int32_t N, int32_t C, int32_t T, int32_t tok_major,
+                                    int32_t groups, float eps, const float* gamma, const float* beta, int32_t Cpad,
+                                    void* out, float* mr, fmd_stream_t s) {
+  if (N < 1 || C < 1 || T < 1 || groups < 1 || C % groups || Cpad < C) return -1;
+  hipLaunchKernelGGL(ctx_norm_fwd_kernel, dim3(groups, N), dim3(256), 0, (hipStream_t)s, ctx, C, T, tok_major, groups,
+                     eps, gamma, beta, Cpad, (bf16r*)out, mr);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_context_norm_bwd(const float* ctx, int32_t N, int32_t C, int32_t T, int32_t tok_major,
+                                    int32_t groups, const float* mr, const void* dout, int32_t Cpad, float* dgamma,
+                                    float* dbeta, fmd_stream_t s) {
+  if (N < 1 || C < 1 || T < 1 || groups < 1 || C % groups || Cpad < C) return -1;
+  hipLaunchKernelGGL(ctx_norm_bwd_kernel, dim3(C), dim3(256), 0, (hipStream_t)s, ctx, N, C, T, tok_major, groups, mr,
+                     (const bf16r*)dout, Cpad, dgamma, dbeta);
+  return (int)hipGetLastError();
+}

@@ -101,6 +101,10 @@ SIGNATURES = {
     "fmd_grouped_linear_bwd": [p, i32, i32, p, p, i32, i32, p, i32, p, i32, p, p],
     "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
     "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_cross_attention_fwd": [p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p, p],
+    "fmd_cross_attention_bwd": [p, p, p, p, p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p],
+    "fmd_context_norm_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, i32, p, p, p],
+    "fmd_context_norm_bwd": [p, i32, i32, i32, i32, i32, p, p, i32, p, p, p],
     "fmd_linear_attention_workspace": [i32, i32],
     "fmd_linear_attention_state": [i32, i32],
     "fmd_linear_attention_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, p, p],

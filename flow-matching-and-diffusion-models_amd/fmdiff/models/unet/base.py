@@ -29,13 +29,11 @@ class BaseUNetND(nn.Module):
         from ...runtime.engine import unet_apply
         if context_ca is not None:
             self._prepare_input(x, None, context_ca)   # reference validation (unet.py:301)
-            raise NotImplementedError("cross-attention conditioning (configs/LDCT/PixelAttention) is not yet on "
-                                      "the fmdiff HIP engine")
         if getattr(self, "center_input_sample", False):
             raise NotImplementedError("center_input_sample is not yet on the fmdiff HIP engine")
         t = self._normalize_timesteps(t, x)
         # the channel concat of `context` is fused into the NHWC staging kernel
-        return unet_apply(self, x, t, context)
+        return unet_apply(self, x, t, context, context_ca)
 
     def engine(self):
         """The cached fused engine bound to this module (built on first GPU use)."""

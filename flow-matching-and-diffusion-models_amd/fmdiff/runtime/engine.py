@@ -227,7 +227,7 @@ class WeightCache:
 
 
 class Ctx:
-    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark")
+    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark", "cca")
 
     def __init__(self, emb, save, N):
         self.emb = emb
@@ -237,6 +237,7 @@ class Ctx:
         self.eo_all = None      # [N][sum O] grouped emb projections of all ResBlocks
         self.demb_all = None
         self.mark = 0           # tape length when the decoder started (backward part 1 = tape[mark:])
+        self.cca = None         # cross-attention context (context_ca), fp32 as passed to the model
 
 
 def _check_conv(c: Conv, ks, stride, pad):
@@ -560,6 +561,71 @@ class UNetEngine:
         ctx.tape.append(bwd)
         return y
 
+    @staticmethod
+    def _context_flat(context: torch.Tensor, cdim: int):
+        """(fp32 contiguous context, token_major) with SpatialCrossAttention's shape rules
+        (attention.py:163-177): (b, c_ctx, tokens) / (b, tokens, c_ctx) / (b, c_ctx, *spatial)."""
+        if context.dim() == 3:
+            if context.shape[1] == cdim:
+                return context.float().contiguous(), False
+            if context.shape[-1] == cdim:
+                return context.float().contiguous(), True
+            raise ValueError(f"Context channels mismatch: expected {cdim}, got {context.shape}.")
+        if context.shape[1] != cdim:
+            raise ValueError(f"Context channels mismatch: expected {cdim}, got {context.shape}.")
+        return context.float().reshape(context.shape[0], cdim, -1).contiguous(), False
+
+    def cross_attention(self, m: SpatialCrossAttention, x: Act, ctx: Ctx):
+        """SpatialCrossAttention (attention.py:157-189): GN(x) folded into the q 1x1 gather; context_norm of the
+        context into the kv 1x1 operand (fmd_context_norm_fwd); raw head split; softmax or linear attention
+        over the context tokens; proj_out + residual in one epilogue.  No gradient flows into the context."""
+        if ctx.cca is None:
+            raise ValueError("SpatialCrossAttention requires a non-empty context tensor.")
+        cf, tok = self._context_flat(ctx.cca, m.context_dim)
+        Tk = cf.shape[1] if tok else cf.shape[2]
+        N, Cc, sp = x.t.shape[0], x.t.shape[-1], tuple(x.t.shape[1:-1])
+        T = math.prod(sp)
+        H, W = T // sp[-1], sp[-1]
+        x4 = x.t.view(N, H, W, Cc)
+        norm, cnm, heads, dh, inner = m.norm, m.context_norm, m.heads, m.dim_head, m.inner_dim
+        lin = m.attention.eps if m.use_linear else None
+        Cp = max(8, -(-m.context_dim // 8) * 8)
+        wq, bq, wkv, bkv = m.q_proj.weight, m.q_proj.bias, m.kv_proj.weight, m.kv_proj.bias
+        wo, bo = m.proj_out.weight, m.proj_out.bias
+        a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
+        q, _ = ops.conv(x4, inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
+        cn, cmr = ops.context_norm_fwd(cf, tok, cnm.num_groups, cnm.eps, cnm.weight, cnm.bias, Cp)
+        kv, _ = ops.conv(cn, 2 * inner, self.wc.get(wkv, 0, None, Cp), ks=1, pad=0, bias=bkv)
+        o, saved = ops.cross_attention_fwd(q, kv, T, Tk, heads, dh, lin)
+        o4 = o.view(N, H, W, inner)
+        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
+        y = Act(out.view(x.t.shape), st)
+        if ctx.tape is None:
+            return y
+
+        def bwd():
+            dy = y.grad.view(N, H, W, Cc)
+            self._wg(lambda: ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad))
+            do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
+            dq, dkv = ops.cross_attention_bwd(q, kv, o, do, saved, T, Tk, heads, dh, lin)
+
+            def wg():
+                ops.wgrad(x4, dq, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
+                tgt = self._wgrad_target(m.kv_proj, Cp)
+                ops.wgrad(cn, dkv, tgt, ks=1, pad=0, db=bkv.grad)
+                self._wgrad_finish(m.kv_proj, Cp, tgt)
+            self._wg(wg)
+            dcn, _ = ops.conv(dkv, Cp, self.wc.get(wkv, 1, None, Cp), ks=1, pad=0, transposed=True, out_hw_=(Tk, 1))
+            ops.context_norm_bwd(cf, tok, cnm.num_groups, cmr, dcn, cnm.weight.grad, cnm.bias.grad)
+            dz, s12 = ops.conv(dq, Cc, self.wc.get(wq, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W),
+                               ep=(x4, None, None, None), want_stats=True)
+            P, Q, R = ops.gn_bwd_prep(s12, N, T, Cc, norm.num_groups, mr, norm.weight, norm.bias, norm.weight.grad,
+                                      norm.bias.grad)
+            g, acc = _gdest(x)
+            ops.gn_bwd_apply(dz, x4, None, P, Q, R, dy, g, acc)
+        ctx.tape.append(bwd)
+        return y
+
     def head(self, norm, conv: Conv, h: Act, ctx: Ctx):
         """GroupNorm -> SiLU -> 3x3 conv to an fp32 NHWC output with CPAD channels."""
         _check_conv(conv, 3, 1, 1)
@@ -661,7 +727,8 @@ class UNetEngine:
         return ctx
 
     # ---------------------------------------------------------------- model
-    def forward(self, xin: torch.Tensor, t: torch.Tensor, save: bool, t_scale: float = 1.0, t_trunc: bool = False):
+    def forward(self, xin: torch.Tensor, t: torch.Tensor, save: bool, t_scale: float = 1.0, t_trunc: bool = False,
+                context_ca: Optional[torch.Tensor] = None):
         """xin: NHWC bf16 [N,H,W,CPAD] (channels past the model's in_channels are 0), t: [N] timesteps
         (``t*t_scale``, truncated to integers if ``t_trunc``).
 
@@ -669,6 +736,7 @@ class UNetEngine:
         m = self.m
         N = xin.shape[0]
         ctx = self.time_mlp(t, save, N, t_scale, t_trunc)
+        ctx.cca = context_ca
         x = Act(xin, need_grad=False)
         if self.kind == "efficient":
             hs = []
@@ -733,7 +801,7 @@ class UNetEngine:
         if isinstance(layer, (SpatialSelfAttention, DiffusersAttentionND)):
             return self.attention(layer, h, ctx)
         if isinstance(layer, SpatialCrossAttention):
-            raise NotImplementedError("SpatialCrossAttention is not yet on the fmdiff engine")
+            return self.cross_attention(layer, h, ctx)
         raise NotImplementedError(type(layer).__name__)
 
     def backward(self, ctx: Ctx, dpred: torch.Tensor, part: int = 0):
@@ -813,9 +881,9 @@ def get_engine(model) -> UNetEngine:
 
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, x, t, context, engine, *params):
+    def forward(fctx, x, t, context, context_ca, engine, *params):
         xin = engine.stage_input(x, context)
-        out, ctx = engine.forward(xin, t, save=True)
+        out, ctx = engine.forward(xin, t, save=True, context_ca=context_ca)
         fctx.engine = engine
         fctx.ctx = ctx
         fctx.kpad = out.shape[-1]
@@ -828,17 +896,18 @@ class _UNetFunction(torch.autograd.Function):
         dpred = ops.nchw_to_nhwc(gout.contiguous(), fctx.kpad)
         eng.backward(fctx.ctx, dpred)
         fctx.ctx = None
-        return (None, None, None, None) + tuple(None for _ in eng.params())
+        return (None, None, None, None, None) + tuple(None for _ in eng.params())
 
 
-def unet_apply(model, x: torch.Tensor, t: torch.Tensor, context: Optional[torch.Tensor]):
+def unet_apply(model, x: torch.Tensor, t: torch.Tensor, context: Optional[torch.Tensor],
+               context_ca: Optional[torch.Tensor] = None):
     """Module-level entry: NCHW fp32 in -> NCHW fp32 out, differentiable w.r.t. the parameters."""
     ops._need_cuda(x, type(model).__name__)
     eng = get_engine(model)
     eng.m_out_channels = model.conv_out.out_channels if eng.kind == "diffusers" else int(model.out_channels)
     params = eng.params()
     if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-        return _UNetFunction.apply(x, t, context, eng, *params)
+        return _UNetFunction.apply(x, t, context, context_ca, eng, *params)
     xin = eng.stage_input(x, context)
-    out, _ = eng.forward(xin, t, save=False)
+    out, _ = eng.forward(xin, t, save=False, context_ca=context_ca)
     return ops.nhwc_to_nchw(out, eng.m_out_channels)

@@ -534,6 +534,53 @@ def linear_attention_bwd(qkv, dout, state, T, heads, dh, raw, eps=1e-6):
     return dqkv
 
 
+def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None):
+    """SpatialCrossAttention core (csrc/attention.hip): q [B][Tq][inner], kv [B][Tk][2*inner] -> (o, saved),
+    softmax (saved = lse) or LinearQKVAttention when ``linear_eps`` is given (saved = state)."""
+    B = q.shape[0]
+    o = torch.empty((B, Tq, heads * dh), device=q.device, dtype=BF16)
+    lin = linear_eps is not None
+    if lin:
+        saved = torch.empty((int(_lib.lib().fmd_linear_attention_state(B, heads)),), device=q.device, dtype=F32)
+        ws = _la_workspace(B, heads, q.device)
+    else:
+        saved = torch.empty((B, heads, Tq), device=q.device, dtype=F32)
+        ws = None
+    _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, 1, int(lin),
+              float(linear_eps or 0.0), _p(o), _p(saved), _p(ws), stream())
+    return o, saved
+
+
+def cross_attention_bwd(q, kv, o, dout, saved, Tq, Tk, heads, dh, linear_eps=None):
+    B = q.shape[0]
+    lin = linear_eps is not None
+    ws = _la_workspace(B, heads, q.device) if lin else torch.empty((B, heads, Tq), device=q.device, dtype=F32)
+    dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+    _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(ws), B, Tq, Tk, heads, dh, 1,
+              int(lin), float(linear_eps or 0.0), _p(dq), _p(dkv), stream())
+    return dq, dkv
+
+
+def context_norm_fwd(ctx, tok_major, groups, eps, gamma, beta, Cpad):
+    """GroupNorm of a cross-attention context (fp32 [N][C][T] or token-major [N][T][C]) -> bf16 [N][T][1][Cpad]
+    (a 1-wide NHWC plane for the kv 1x1 conv) and the (mean, rstd) table."""
+    _need_cuda(ctx, "context_norm_fwd")
+    N = ctx.shape[0]
+    C, T = (ctx.shape[2], ctx.shape[1]) if tok_major else (ctx.shape[1], ctx.shape[2])
+    out = torch.empty((N, T, 1, Cpad), device=ctx.device, dtype=BF16)
+    mr = torch.empty((N, groups, 2), device=ctx.device, dtype=F32)
+    _lib.call("fmd_context_norm_fwd", _p(ctx), N, C, T, int(tok_major), groups, float(eps), _p(gamma), _p(beta), Cpad,
+              _p(out), _p(mr), stream())
+    return out, mr
+
+
+def context_norm_bwd(ctx, tok_major, groups, mr, dout, dgamma, dbeta):
+    N = ctx.shape[0]
+    C, T = (ctx.shape[2], ctx.shape[1]) if tok_major else (ctx.shape[1], ctx.shape[2])
+    _lib.call("fmd_context_norm_bwd", _p(ctx), N, C, T, int(tok_major), groups, _p(mr), _p(dout), dout.shape[-1],
+              _p(dgamma), _p(dbeta), stream())
+
+
 def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
     B = qkv.shape[0]
     dqkv = torch.empty_like(qkv)

@@ -251,6 +251,25 @@ int fmd_attention_bwd(const void* qkv, const void* o, const void* dout, const fl
  * (attention.py:104-117; same raw head split): out = softmax_d(q) (softmax_tokens(k)^T v / (sum ks + eps)).
  * ``state`` (fmd_linear_attention_state floats) is written by the forward and read by the backward;
  * ``ws`` holds fmd_linear_attention_workspace floats. dh <= 64. */
+/* SpatialCrossAttention (attention.py:120-189): q [B][Tq][inner] (q_proj output), kv [B][Tk][2*inner]
+ * (kv_proj output), raw head split q.reshape(b, heads, Tq, dh), kv.reshape(b, heads, Tk, 2dh).chunk(2).
+ * linear = 1: LinearQKVAttention (lse_or_state = fmd_linear_attention_state floats, ws = workspace);
+ * linear = 0: softmax (lse_or_state = lse [B][heads][Tq]; backward: ws_or_delta = delta [B][heads][Tq]). */
+int fmd_cross_attention_fwd(const void* q, const void* kv, int32_t B, int32_t Tq, int32_t Tk, int32_t heads,
+                            int32_t dh, int32_t raw, int32_t linear, float eps, void* o, float* lse_or_state,
+                            float* ws, fmd_stream_t s);
+int fmd_cross_attention_bwd(const void* q, const void* kv, const void* o, const void* dout, const float* lse_or_state,
+                            float* ws_or_delta, int32_t B, int32_t Tq, int32_t Tk, int32_t heads, int32_t dh,
+                            int32_t raw, int32_t linear, float eps, void* dq, void* dkv, fmd_stream_t s);
+/* context_norm of SpatialCrossAttention: GroupNorm over the fp32 context ((N, C, T) or token-major (N, T, C))
+ * -> bf16 [N][T][Cpad] (zero pad channels); mr [N][groups][2] = mean, rstd.  The backward accumulates
+ * dgamma / dbeta only (the context is conditioning data). */
+int fmd_context_norm_fwd(const float* ctx, int32_t N, int32_t C, int32_t T, int32_t tok_major, int32_t groups,
+                         float eps, const float* gamma, const float* beta, int32_t Cpad, void* out, float* mr,
+                         fmd_stream_t s);
+int fmd_context_norm_bwd(const float* ctx, int32_t N, int32_t C, int32_t T, int32_t tok_major, int32_t groups,
+                         const float* mr, const void* dout, int32_t Cpad, float* dgamma, float* dbeta,
+                         fmd_stream_t s);
 size_t fmd_linear_attention_workspace(int32_t B, int32_t heads);
 size_t fmd_linear_attention_state(int32_t B, int32_t heads);
 int fmd_linear_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw,

@@ -346,6 +346,33 @@ def test_linear_attention(raw, T, heads, dh):
     _close(dq, f.grad, rel=2e-2)
 
 
+@pytest.mark.parametrize("linear,Tq,Tk,heads,dh", [(0, 256, 1024, 4, 64), (0, 70, 33, 2, 32), (1, 256, 1024, 4, 64),
+                                                  (1, 1500, 2100, 2, 24)])
+def test_cross_attention(linear, Tq, Tk, heads, dh):
+    """SpatialCrossAttention core (reference attention.py:179-184: raw q / kv reshapes, chunk(2)) vs fp32 autograd,
+    softmax and LinearQKVAttention."""
+    from oracle.unet import _linear_attention
+    O = ops()
+    B = 2
+    inner = heads * dh
+    qb = (torch.randn(B, Tq, inner) * 0.7).to(torch.bfloat16)
+    kvb = (torch.randn(B, Tk, 2 * inner) * 0.7).to(torch.bfloat16)
+    qf, kvf = qb.float().requires_grad_(), kvb.float().requires_grad_()
+    q = qf.transpose(1, 2).reshape(B, heads, Tq, dh)
+    k, v = kvf.transpose(1, 2).reshape(B, heads, Tk, 2 * dh).chunk(2, dim=-1)
+    o = _linear_attention(q, k, v) if linear else F.scaled_dot_product_attention(q, k, v)
+    o_tok = o.reshape(B, inner, Tq).transpose(1, 2)
+    do = torch.randn_like(o_tok).to(torch.bfloat16).float()
+    o_tok.backward(do)
+    eps = 1e-6 if linear else None
+    og, saved = O.cross_attention_fwd(qb.to(DEV), kvb.to(DEV), Tq, Tk, heads, dh, eps)
+    _close(og, o_tok.detach())
+    dq, dkv = O.cross_attention_bwd(qb.to(DEV), kvb.to(DEV), og, do.contiguous().to(torch.bfloat16).to(DEV), saved,
+                                    Tq, Tk, heads, dh, eps)
+    _close(dq, qf.grad, rel=2e-2)
+    _close(dkv, kvf.grad, rel=2e-2)
+
+
 def test_time_embedding_and_linear():
     O = ops()
     from oracle.unet import timestep_embedding

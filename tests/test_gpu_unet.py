@@ -219,3 +219,58 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
     print(f"{impl} grad rel L2 {rel:.3e}, worst cosine {worst}")
     assert rel < 5e-2
     assert worst[0] > 0.99, worst
+
+
+@pytest.mark.parametrize("ctx_layout", ["nchw", "tokens_last"])
+def test_cross_attention_unet_vs_oracle(ctx_layout):
+    """conditioning "attention" (configs/LDCT/PixelAttention/*): EfficientUNetND with linear self- and
+    cross-attention at ds 2 and softmax cross-attention in the middle, context_ca = a 4-channel latent;
+    forward and FM train-step parameter gradients vs the oracle (context_norm gamma/beta included)."""
+    import torch.nn.functional as F
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from oracle import spec as S
+    from oracle import unet as U
+    cfg = dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64], sample_size=32,
+               cross_attention_dim=4, attention_resolutions=[2], cross_attention_resolutions=[2],
+               cross_attention_in_middle=True)
+    model = DiffusionUNetFactory().build(cfg, "attention", 1).to(DEV)
+    spec = S.derive_spec(cfg, "attention", 1)
+    sd = U.seeded_state_dict(spec, 21)
+    model.load_state_dict(sd)
+    g = torch.Generator().manual_seed(9)
+    clean, noise = (torch.randn(2, 1, 32, 32, generator=g) for _ in range(2))
+    lat = torch.randn(2, 4, 8, 8, generator=g)
+    ctx = lat if ctx_layout == "nchw" else lat.reshape(2, 4, 64).transpose(1, 2).contiguous()
+    t = torch.rand(2, generator=g)
+    ts = (t * 999).long()
+    tb = t.view(-1, 1, 1, 1)
+    x_t = (1.0 - tb) * clean + tb * noise
+    with torch.no_grad():
+        y = model(x_t.to(DEV), ts.to(DEV), context_ca=ctx.to(DEV))
+    y_ref = U.unet_forward(sd, spec, x_t, ts, context_ca=ctx)
+    err = _rel(y, y_ref)
+    print(f"cross-attention UNet forward rel L2 {err:.3e}")
+    assert err < 2e-2
+
+    sdg = {k: v.clone().requires_grad_() for k, v in sd.items()}
+    loss_ref = F.mse_loss(U.unet_forward(sdg, spec, x_t, ts, context_ca=ctx), noise - clean)
+    loss_ref.backward()
+    pred = model(x_t.to(DEV), ts.to(DEV), context_ca=ctx.to(DEV))
+    loss = F.mse_loss(pred, (noise - clean).to(DEV))
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) / loss_ref.item() < 1e-2
+    num = den = 0.0
+    worst = (1.0, "")
+    for k, p in model.named_parameters():
+        gk = p.grad.double().cpu()
+        r = sdg[k].grad.double()
+        num += (gk - r).pow(2).sum().item()
+        den += r.pow(2).sum().item()
+        if r.norm() > 1e-3 * math.sqrt(den + 1e-30):
+            cos = (gk * r).sum() / (gk.norm() * r.norm() + 1e-30)
+            if cos < worst[0]:
+                worst = (cos.item(), k)
+    rel = math.sqrt(num / den)
+    print(f"cross-attention UNet grad rel L2 {rel:.3e}, worst cosine {worst}")
+    assert rel < 5e-2
+    assert worst[0] > 0.99, worst
