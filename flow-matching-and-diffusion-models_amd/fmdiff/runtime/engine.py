@@ -397,14 +397,16 @@ class UNetEngine:
         g1, g2 = m.norm1, m.norm2
         el = m.emb_layers
         ss = m.use_scale_shift_norm
-        add = (not ss) and m.add_embedding_to_hidden
+        add = (not ss) and m.add_embedding_to_hidden and el is not None
         slot = self.gl_slot.get(id(m)) if ctx.eo_all is not None else None
         if slot is not None:   # view into the grouped projection (row stride = gl.total)
             eo = ctx.eo_all[:, slot[0]:slot[0] + slot[1]]
             es = self.gl.total
-        else:
+        elif ss or add:
             eo = ops.linear(ctx.emb, el.weight, el.bias, in_silu=m.emb_activation_before_proj)
             es = eo.shape[1]
+        else:   # the embedding projection feeds nothing (or the block has none: VAE ResBlocks)
+            eo, es = None, 0
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         halo1 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
         mat1 = _materialise(halo1, x1, Cin, HW)
@@ -462,9 +464,11 @@ class UNetEngine:
             dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, sp, ep=(h, None, a2, b2), want_stats=True)
             if slot is not None:
                 demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
-            else:
+            elif eo is not None:
                 demb = torch.empty_like(eo)
                 ds_ = demb.shape[1]
+            else:
+                demb, ds_ = None, 0
             if ss:
                 P2, Q2, R2 = ops.gn_bwd_prep(s2, N, HW, Cout, g2.num_groups, mr2, g2.weight, g2.bias, g2.weight.grad,
                                              g2.bias.grad, emb=eo, emb_stride=es, emb_mode=1, demb=demb,

@@ -274,3 +274,33 @@ def test_cross_attention_unet_vs_oracle(ctx_layout):
     print(f"cross-attention UNet grad rel L2 {rel:.3e}, worst cosine {worst}")
     assert rel < 5e-2
     assert worst[0] > 0.99, worst
+
+
+def test_autoencoder_kl_vs_reference_fixture():
+    """AutoencoderKL (config D) encode moments / posterior.mode() and decode through the HIP engine vs the
+    reference module's own outputs (tests/golden/make_vae_golden.py) and the oracle restatement."""
+    import json
+    import os
+    import warnings
+    from fmdiff.models.vae import AutoencoderKL
+    G = torch.load(os.path.join(os.path.dirname(__file__), "golden", "vae_golden.pt"), weights_only=True)
+    cfg = json.loads(bytes(G["cfg_json"].tolist()).decode())
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**cfg)
+    vae.load_state_dict(G["state"])
+    vae = vae.to(DEV).eval()
+    x = G["x"].to(DEV)
+    post = vae.encode(vae.image_to_model_range(x))
+    err_m = _rel(post.mode(), G["mode"])
+    err_lv = _rel(post.logvar, G["moments"][:, 4:])
+    rec = vae.decode(G["z"].to(DEV))
+    err_r = _rel(rec, G["rec"])
+    print(f"VAE mode rel L2 {err_m:.3e}, logvar {err_lv:.3e}, decode {err_r:.3e}")
+    assert err_m < 2e-2 and err_lv < 2e-2 and err_r < 2e-2
+    # module-level encoder / decoder forwards
+    enc_out = vae.encoder(vae.image_to_model_range(x))
+    from oracle import vae as V
+    sd = G["state"]
+    ref_enc = V.encoder(sd, cfg, G["x"] * 2.0 - 1.0)
+    assert _rel(enc_out, ref_enc) < 2e-2

@@ -146,3 +146,40 @@ def test_cosine_schedule_matches_transformers():
         assert math.isclose(opt.param_groups[0]["lr"], OS.cosine_with_warmup(step, 5, 40), rel_tol=1e-12)
         opt.step()
         sch.step()
+
+
+def _vae_golden():
+    import json
+    import os
+    G = torch.load(os.path.join(os.path.dirname(__file__), "golden", "vae_golden.pt"), weights_only=True)
+    return G, json.loads(bytes(G["cfg_json"].tolist()).decode())
+
+
+def test_vae_oracle_matches_reference_fixture():
+    """oracle/vae.py (encode moments, decode) vs the reference AutoencoderKL's own outputs
+    (tests/golden/make_vae_golden.py)."""
+    from oracle import vae as V
+    G, cfg = _vae_golden()
+    sd = G["state"]
+    with torch.no_grad():
+        m = V.encode_moments(sd, cfg, G["x"] * 2.0 - 1.0)
+        r = V.decode(sd, cfg, G["z"])
+    mu, logvar = m.chunk(2, 1)
+    torch.testing.assert_close(mu, G["mode"], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(logvar.clamp(-30.0, 20.0), G["moments"][:, 4:], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(r, G["rec"], rtol=1e-5, atol=1e-5)
+
+
+def test_vae_module_state_dict_drop_in():
+    """fmdiff AutoencoderKL: same constructor and state_dict keys/shapes as the reference."""
+    import warnings
+    from fmdiff.models.vae import AutoencoderKL
+    G, cfg = _vae_golden()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**cfg)
+    ref = G["state"]
+    own = vae.state_dict()
+    assert list(own.keys()) == list(ref.keys())
+    assert all(own[k].shape == ref[k].shape for k in own)
+    vae.load_state_dict(ref)
