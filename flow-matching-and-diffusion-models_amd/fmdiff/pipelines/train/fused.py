@@ -89,19 +89,20 @@ class FusedTrainStep:
         self._split = False
 
     # ---------------------------------------------------------------- body
-    def _chunk(self, clean, ldct, noise, t_or_ts):
+    def _chunk(self, clean, ldct, noise, t_or_ts, cca=None):
         N, Cx = clean.shape[:2]
         Cc = ldct.shape[1] if ldct is not None else 0
         Cp = max(8, -(-(Cx + Cc) // 8) * 8)
         if self.objective == "flow_matching":
             inp = ops.noise_prepare(clean, noise, t_or_ts, None, ldct, Cp)        # (1-t) x0 + t eps
-            out, ctx = self.eng.forward(inp, t_or_ts, save=True, t_scale=float(self.N_train - 1), t_trunc=True)
+            out, ctx = self.eng.forward(inp, t_or_ts, save=True, t_scale=float(self.N_train - 1), t_trunc=True,
+                                        context_ca=cca)
             ta, tb, sign = noise, clean, -1.0                                      # target eps - x0
         else:
             sel = self.acp[t_or_ts]
             ca, cb = sel.sqrt(), (1 - sel).sqrt()
             inp = ops.noise_prepare(clean, noise, ca, cb, ldct, Cp)               # add_noise
-            out, ctx = self.eng.forward(inp, t_or_ts, save=True)
+            out, ctx = self.eng.forward(inp, t_or_ts, save=True, context_ca=cca)
             ta, tb, sign = noise, None, 0.0                                        # target eps
         dpred = torch.empty(out.shape, device=out.device, dtype=torch.bfloat16)
         ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
@@ -119,9 +120,10 @@ class FusedTrainStep:
     def _allreduce(self):
         bucketed_allreduce(self.flat.grad, self.buckets, self.pg)
 
-    def step(self, clean, ldct, noise=None, t=None):
-        """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss."""
-        loss = self._fwd_bwd(clean, ldct, noise, t)
+    def step(self, clean, ldct, noise=None, t=None, context_ca=None):
+        """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss.
+        ``context_ca``: cross-attention conditioning (conditioning "attention", e.g. VAE latents)."""
+        loss = self._fwd_bwd(clean, ldct, noise, t, context_ca)
         if self.overlap:
             self._overlapped_tail(self._bwd_rest)
         else:
@@ -144,7 +146,7 @@ class FusedTrainStep:
                         self.hp["total"], b1, b2, self.hp["eps"], self.hp["wd"], 1.0 / self.world)
         ops.counter_add(self.step_ctr)
 
-    def _fwd_bwd(self, clean, ldct, noise=None, t=None):
+    def _fwd_bwd(self, clean, ldct, noise=None, t=None, context_ca=None):
         """Weight refresh, gradient zeroing and forward + backward of every grad-accumulation chunk."""
         self.eng.invalidate_weights()            # bf16 kernel weights re-derived from the updated masters
         self.flat.grad.zero_()
@@ -160,17 +162,20 @@ class FusedTrainStep:
             else:
                 tt = t[c0:c0 + chunk] if t is not None else torch.randint(0, self.N_train, (cl.shape[0],),
                                                                            device=cl.device)
-            loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt)
+            cc = context_ca[c0:c0 + chunk].contiguous() if context_ca is not None else None
+            loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt, cc)
         return loss
 
     # ---------------------------------------------------------- hipGraph
-    def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None):
+    def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None,
+                context_ca=None):
         """Capture one step into a hipGraph.  Single process: the whole step (RNG, forward, loss, backward,
         AdamW).  With several ranks (``split_collectives``, default: world > 1) the graph holds RNG +
         forward + backward, and each replay is followed by the bucketed RCCL all-reduce and the AdamW
         launch issued eagerly: no collective is ever recorded into a graph."""
         self._split = self.world > 1 if split_collectives is None else bool(split_collectives)
-        self._static = (clean.clone(), ldct.clone() if ldct is not None else None)
+        self._static = (clean.clone(), ldct.clone() if ldct is not None else None, None, None,
+                        context_ca.clone() if context_ca is not None else None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -194,11 +199,13 @@ class FusedTrainStep:
                 self._bwd_rest()
             self._graph2 = g2
 
-    def replay(self, clean=None, ldct=None):
+    def replay(self, clean=None, ldct=None, context_ca=None):
         if clean is not None:
             self._static[0].copy_(clean)
         if ldct is not None:
             self._static[1].copy_(ldct)
+        if context_ca is not None:
+            self._static[4].copy_(context_ca)
         self._graph.replay()
         if self._split:
             if self._graph2 is not None:
@@ -219,6 +226,7 @@ class FusedFlowSampler:
         self.sched.set_timesteps(num_inference_steps)
         self.S = num_inference_steps
         self._graph = None
+        self.cca = None
 
     def _prepare(self, init, cond):
         dev = init.device
@@ -238,13 +246,16 @@ class FusedFlowSampler:
     def _one(self):
         if self.eng._tt is None:   # no precomputed embedding table: the MLP runs on t = ts[idx]
             ops.fill_from_table(self.ts, self.idx, self.tbuf)
-        out, _ = self.eng.forward(self.inp, self.tbuf, save=False)
+        out, _ = self.eng.forward(self.inp, self.tbuf, save=False, context_ca=self.cca)
         ops.flow_euler(self.x, out, self.sig, self.idx, self.cond, self.inp)
         ops.counter_add(self.idx)
 
     @torch.no_grad()
-    def sample(self, init: torch.Tensor, cond: Optional[torch.Tensor] = None, use_graph: bool = True):
+    def sample(self, init: torch.Tensor, cond: Optional[torch.Tensor] = None, use_graph: bool = True,
+               context_ca: Optional[torch.Tensor] = None):
+        """``cond``: concatenated conditioning; ``context_ca``: cross-attention conditioning."""
         self._prepare(init, cond)
+        self.cca = context_ca.float().contiguous() if context_ca is not None else None
         if not use_graph:
             for _ in range(self.S):
                 self._one()
