@@ -697,6 +697,27 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   return rc;
 }
 
+// The split-K combine alone: out = sum of d->splits fp32 slabs in d->ws ([splits][M][K]) + the conv
+// epilogue (bias, bias2, per-sample bias, residual, data-gradient SiLU' / GN-backward sums, statistics).
+// Used by convolutions assembled from several partial launches (3-D convs as three depth-tap planes).
+extern "C" int fmd_conv_combine(const fmd_conv_desc* d, fmd_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!d->ws || d->splits < 1 || d->N < 1 || d->K < 1 || !d->out) return -1;
+  const int M = d->N * (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  const int HWo = (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  const bool rows_ok = d->K % 4 == 0 && M % FMD_SPLIT_STATS_ROWS == 0 && HWo % FMD_SPLIT_STATS_ROWS == 0;
+  if (d->stats && (!rows_ok || d->out_f32 || d->accumulate)) return -5;
+  if (rows_ok) {
+    hipLaunchKernelGGL(splitk_reduce_rows, dim3(M / FMD_SPLIT_STATS_ROWS, (d->K + 63) / 64), dim3(256), 0, s, *d, M);
+  } else {
+    const size_t total = (size_t)M * d->K;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, s, *d, M);
+  }
+  return (int)hipGetLastError();
+}
+
 // 1x1 (or any generic-path) conv whose epilogue is the GroupNorm-backward apply of fmd_gn_bwd_apply:
 // dx = conv(...) + P*dz + Q*x + R (+ dx), split over the concat sources at g->C0.  d: no split-K, no
 // stats/bias/residual/out (the result only exists as dx).

@@ -51,6 +51,9 @@ struct HArgs {
   int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
   const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
+  int depth, ncb;         // 3-D (depth > 0): images are the N*depth slices; main chunk = (depth tap kz,
+                          // 32-channel block cb) = kz*ncb + cb, reading slice z + kz - 1 (zeros outside);
+                          // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
 };
@@ -133,6 +136,8 @@ void conv3x3_halo(const HArgs A) {
   const int tile = b / A.ntc;
   const int n = tile / per_img;
   const int tin = tile - n * per_img;
+  const int smp = A.depth ? n / A.depth : n;          // sample of this image (3-D: slice n of sample smp)
+  const int zz = A.depth ? n - smp * A.depth : 0;
   const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
   const int co0 = tco * BCO;
   const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;   // halo origin (stored-input coordinates)
@@ -146,7 +151,7 @@ void conv3x3_halo(const HArgs A) {
   // the GN affine of image n for every input channel, and the epilogue's per-cout vectors
   if (PRO != 0) {
     for (int i = tid; i < 2 * A.C; i += NT)
-      coef[i] = i < A.C ? d.pro_a[(size_t)n * A.C + i] : d.pro_b[(size_t)n * A.C + (i - A.C)];
+      coef[i] = i < A.C ? d.pro_a[(size_t)smp * A.C + i] : d.pro_b[(size_t)smp * A.C + (i - A.C)];
   }
   if (tid < BCO) {
     const int co = co0 + tid;
@@ -154,10 +159,10 @@ void conv3x3_halo(const HArgs A) {
     float bsum = 0.f;
     if (ok && d.bias) bsum += d.bias[co];
     if (ok && d.bias2) bsum += d.bias2[co];
-    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)n * d.K + co];
+    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)smp * d.K + co];
     epi[tid] = bsum;
-    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)n * d.K + co] : 0.f;
-    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)n * d.K + co] : 0.f;
+    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)smp * d.K + co] : 0.f;
+    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)smp * d.K + co] : 0.f;
   }
 
   // ---- weights: one contiguous 8 KiB tile per tap, copied global -> LDS by the DMA path
@@ -184,11 +189,20 @@ void conv3x3_halo(const HArgs A) {
   int cs = 0;                // its pixel stride
   int cch = 0;               // its first channel (GN affine table index)
   bool cok = false;
+  int zsh = 0;               // 3-D: source slice offset (kz - 1) of the chunk being staged
 
   auto setup = [&](int chunk) {
     if (chunk < A.nchunk1) {
-      const int c = chunk * BK + kc * 8;
-      cok = c < A.C;
+      int cb = chunk;
+      bool zok = true;
+      if (A.depth) {
+        const int kz = chunk / A.ncb;
+        cb = chunk - kz * A.ncb;
+        zsh = kz - 1;
+        zok = zz + zsh >= 0 && zz + zsh < A.depth;
+      }
+      const int c = cb * BK + kc * 8;
+      cok = c < A.C && zok;
       cbase = !cok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
       cs = (c < d.C0) ? d.C0 : d.C1;
       cch = cok ? c : 0;
@@ -211,7 +225,7 @@ void conv3x3_halo(const HArgs A) {
       const int py = pos / HROW, px = pos - (pos / HROW) * HROW;   // constant divisor: mul-shift
       const int y = hy0 + py, x = hx0 + px;
       valid = on && cok && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
-      pix = (n * d.Hs + y) * d.Ws + x;
+      pix = ((n + zsh) * d.Hs + y) * d.Ws + x;
       lpos = pos;
       act = on;
     } else {
@@ -548,7 +562,7 @@ void conv3x3_halo(const HArgs A) {
         if (co + r < K) {
           if (d.bias) bias[r] += d.bias[co + r];
           if (d.bias2) bias[r] += d.bias2[co + r];
-          if (d.bias_nc) bias[r] += d.bias_nc[(size_t)n * K + co + r];
+          if (d.bias_nc) bias[r] += d.bias_nc[(size_t)smp * K + co + r];
         }
       }
       float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
@@ -578,7 +592,7 @@ void conv3x3_halo(const HArgs A) {
             const bf16r* xp = (c < C0e) ? (const bf16r*)d.ep_x0 + p * C0e + c
                                         : (const bf16r*)d.ep_x1 + p * (K - C0e) + (c - C0e);
             xv[r] = bf2f(*xp);
-            if (dep) v[r] *= silu_grad(d.ep_a[(size_t)n * K + c] * xv[r] + d.ep_b[(size_t)n * K + c]);
+            if (dep) v[r] *= silu_grad(d.ep_a[(size_t)smp * K + c] * xv[r] + d.ep_b[(size_t)smp * K + c]);
           }
         }
         if (d.out_f32) {
@@ -646,14 +660,17 @@ __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, i
 // Called by fmd_conv when the problem qualifies (3x3, stride 1, pad 1, forward gather,
 // output tile 16x16 inside one image, >= 128 tiles).  Returns 1 if not applicable.
 extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed || d->Do > 0 || d->Ds > 0) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed) return 1;
+  const bool d3 = d->Do > 0 || d->Ds > 0;
+  if (d3 && (d->Ds != d->Do || d->upsample)) return 1;   // 3-D: stride-1 same-depth 3x3x3 only
+  const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
   if (d->splits > 1 && (!d->ws || d->stats)) return 1;
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
   if (d->pro_a && d->C0 + d->C1 > CMAX) return 1;   // the GN affine table holds CMAX channels
-  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
-      (long long)d->N * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
+  if ((long long)Nn * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      (long long)Nn * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
   HArgs A;
   A.d = *d;
   A.C = d->C0 + d->C1;
@@ -661,7 +678,10 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.tiles_x = d->Wo / TW;
   A.tiles_y = d->Ho / TH;
   A.ntc = (d->K + BCO - 1) / BCO;
-  A.nchunk1 = (A.C + BK - 1) / BK;
+  A.depth = d3 ? d->Do : 0;
+  A.ncb = (A.C + BK - 1) / BK;
+  A.nchunk1 = d3 ? 3 * A.ncb : A.ncb;   // 3-D: weights pre-tiled as a 3*ncb*32-channel 2-D conv (kz-major)
+  A.d.N = Nn;
   A.nchunk2 = d->src2 ? (A.C23 + BK - 1) / BK : 0;
   A.nsteps_slots = A.nchunk1 * 9 + A.nchunk2;
   A.splits = d->splits > 1 ? d->splits : 1;
@@ -670,7 +690,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
   A.dbg = g_dbg;
-  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < 128) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;

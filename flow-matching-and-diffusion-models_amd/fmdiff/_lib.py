@@ -101,6 +101,7 @@ SIGNATURES = {
     "fmd_grouped_linear_bwd": [p, i32, i32, p, p, i32, i32, p, i32, p, i32, p, p],
     "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
     "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_conv_combine": [C.POINTER(ConvDesc), p],
     "fmd_cross_attention_fwd": [p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p, p],
     "fmd_cross_attention_bwd": [p, p, p, p, p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p],
     "fmd_context_norm_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, i32, p, p, p],

@@ -48,6 +48,8 @@ HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdif
 # least MAT_MIN_HW pixels, where the streaming pass costs less than the in-kernel transform it removes
 MAT_PRO = os.environ.get("FMD_MAT_PRO", "0") == "1"   # measured net-negative at batch 8
 MAT_CMAX = 128
+# 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
+DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
 MAT_MIN_HW = 128 * 128
 
 
@@ -116,6 +118,8 @@ class WeightCache:
         for key, e in self._c.items():          # fp32 derived buffers first: they feed the bf16 layouts
             if e["kind"] == "pad":
                 e["buf"][: e["src"].numel()].copy_(e["src"].detach().reshape(-1))
+            elif e["kind"] == "dpack":
+                self._dpack(e["src"], e["mode"], e["buf"])
             elif e["kind"] == "fused":
                 o = 0
                 for w in e["src"]:
@@ -198,6 +202,32 @@ class WeightCache:
                                 job=(K, C, ks, mode, R, Cc, 1, T, buf.numel()))
             self._force.discard(key)
         return self._c[key]["buf"]
+
+    @staticmethod
+    def _dpack(w, mode, buf):
+        """fp32 [R][3 * Cr][3][3] 2-D view of a 3x3x3 weight for the depth-tap halo conv: channel block
+        kz*Cr + c holds tap kz of input channel c (Cr = C rounded up to 32, zero padded).  mode 0: the
+        forward weight; mode 3: the data-gradient weight W'[c][k][kz][ky][kx] = W[k][c][2-kz][2-ky][2-kx]."""
+        src = w.detach() if mode == 0 else w.detach().flip(2, 3, 4).transpose(0, 1)
+        R, Cs = src.shape[:2]
+        Cr = buf.shape[1] // 3
+        v = buf.view(R, 3, Cr, 3, 3)
+        if Cr != Cs:
+            v[:, :, Cs:].zero_()
+        v[:, :, :Cs].copy_(src.permute(0, 2, 1, 3, 4))
+
+    def dtiled(self, w: torch.Tensor, mode: int):
+        """Halo-tiled depth-tap layout of a 3x3x3 weight (mode 0 forward, 3 data gradient)."""
+        key = (id(w), "dpack", mode)
+        if not self._fresh(key, self._ver(w)):
+            e = self._c.get(key)
+            R, Cs = (w.shape[0], w.shape[1]) if mode == 0 else (w.shape[1], w.shape[0])
+            buf = e["buf"] if e is not None else torch.empty((R, 3 * (-(-Cs // HALO_BK) * HALO_BK), 3, 3),
+                                                             device=w.device, dtype=F32)
+            self._dpack(w, mode, buf)
+            self._c[key] = dict(kind="dpack", src=w, mode=mode, buf=buf, ver=self._ver(w))
+            self._force.discard(key)
+        return self.tiled(self._c[key]["buf"], 0)
 
     def padded(self, v: torch.Tensor, n: int):
         key = (id(v), "pad", n)
@@ -295,8 +325,11 @@ class UNetEngine:
         Cin = x.C
         N_, sp = x.t.shape[0], tuple(x.t.shape[1:-1])
         Ho_ = ops.out_hw(sp[0], 3, stride, 1, upsample)
-        halo = len(sp) == 2 and stride == 1 and ops.halo_eligible(
-            N_, sp[0], Ho_, ops.out_hw(sp[1], 3, stride, 1, upsample), conv.out_channels, upsample=upsample, Cin=Cin)
+        if len(sp) == 2:
+            halo = stride == 1 and ops.halo_eligible(N_, sp[0], Ho_, ops.out_hw(sp[1], 3, stride, 1, upsample),
+                                                     conv.out_channels, upsample=upsample, Cin=Cin)
+        else:
+            halo = stride == 1 and not upsample and self._halo_ok(N_, sp, conv.out_channels, Cin)
         w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
                            bias=conv.bias, want_stats=True, wgt_tiled=wt)
@@ -351,6 +384,8 @@ class UNetEngine:
         """(base, tiled) kernel layouts of ``w``: only the one the chosen conv path reads is derived
         (and refreshed by every optimizer step), the other is None."""
         if halo:
+            if w.dim() == 5 and w.shape[2] == 3:
+                return None, self.wc.dtiled(w, mode)
             return None, self.wc.tiled(w, mode, Kpad, Cpad)
         return self.wc.get(w, mode, Kpad, Cpad), None
 
@@ -360,11 +395,19 @@ class UNetEngine:
         stride 2 = transposed gather."""
         sp = tuple(sp)
         if stride == 1:
-            halo = len(sp) == 2 and ops.halo_eligible(dy.shape[0], sp[0], sp[0], sp[1], Cin, Cin=dy.shape[-1])
+            halo = self._halo_ok(dy.shape[0], sp, Cin, dy.shape[-1])
             base, tiled = self._wts(w, 3, halo, Kpad, None)
             return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=sp, wgt_tiled=tiled, **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,
                         out_hw_=sp, **kw)
+
+    @staticmethod
+    def _halo_ok(N, sp, K, Cin, pro=False) -> bool:
+        """3x3 (3x3x3) stride-1 conv onto the grid ``sp`` on the halo kernel (3-D: depth-tap chunks)."""
+        if len(sp) == 2:
+            return ops.halo_eligible(N, sp[0], sp[0], sp[1], K, Cin=Cin, pro=pro)
+        D, H, W = sp
+        return DEPTH_HALO and ops.halo_eligible(N * D, H, H, W, K, Cin=Cin, pro=pro, ztaps=3)
 
     def _wgrad_target(self, conv: Conv, Cin: int):
         """fp32 buffer the wgrad kernel writes: param.grad itself unless channels were padded."""
@@ -385,7 +428,6 @@ class UNetEngine:
         N, C0, sp = x0.t.shape[0], x0.t.shape[-1], tuple(x0.t.shape[1:-1])
         C1 = x1.C if x1 is not None else 0
         Cin, Cout, HW = C0 + C1, m.out_channels, math.prod(sp)
-        d2 = len(sp) == 2            # halo kernels are 2-D only
         H, W = sp[-2], sp[-1]
         if Cin != m.channels:
             raise ValueError(f"ResBlockND expects {m.channels} channels, got {Cin}")
@@ -408,10 +450,10 @@ class UNetEngine:
         else:   # the embedding projection feeds nothing (or the block has none: VAE ResBlocks)
             eo, es = None, 0
         a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
-        halo1 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cin, pro=True)
+        halo1 = self._halo_ok(N, sp, Cout, Cin, pro=True)
         mat1 = _materialise(halo1, x1, Cin, HW)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
-            halo1 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cin)
+            halo1 = self._halo_ok(N, sp, Cout, Cin)
         w1, w1t = self._wts(c1.weight, 0, halo1)
         t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
         src1 = x1.t if (x1 is not None and t1 is None) else None
@@ -432,10 +474,10 @@ class UNetEngine:
             kw["resid"] = x0.t
         else:
             _check_conv(sk.conv, 1, 1, 0)
-        halo2 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cout, pro=True)
+        halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
         mat2 = _materialise(halo2, None, Cout, HW)
         if mat2 and not halo2:
-            halo2 = d2 and ops.halo_eligible(N, H, H, W, Cout, Cin=Cout)
+            halo2 = self._halo_ok(N, sp, Cout, Cout)
         if not isinstance(sk, Identity):
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)

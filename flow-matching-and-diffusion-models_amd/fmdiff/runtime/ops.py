@@ -163,13 +163,13 @@ HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
 SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
 
 
-def halo_splits(N, Ho, Wo, K, Cin) -> int:
+def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
     """Split-K factor the halo kernel uses: 1 when the 16x16 tiles x cout tiles already give >= 128
     workgroups, else enough chunk-range splits (>= 2 chunks each) to reach ~256; 0 = not eligible."""
     nwg = N * (Ho // 16) * (Wo // 16) * -(-K // 128)
     if nwg >= 128:
         return 1
-    nch = -(-max(Cin, 1) // HALO_BK)
+    nch = -(-max(Cin, 1) // HALO_BK) * ztaps
     sp = min(-(-256 // max(nwg, 1)), nch // 2, 16)
     if sp < 2 or nwg * sp < 128:
         return 0
@@ -180,13 +180,13 @@ def halo_splits(N, Ho, Wo, K, Cin) -> int:
 
 
 def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False, Cin=0,
-                  pro=False) -> bool:
+                  pro=False, ztaps=1) -> bool:
     """Mirror of fmd_conv_halo's applicability test (csrc/conv_halo.hip): 3x3 s1 p1 forward gather,
     16x16 output tiles, K > 16, at least 128 workgroups (with split-K over channel chunks when the
     level is small), GN-prologue inputs of at most HALO_CMAX channels."""
     return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed and not (pro and Cin > HALO_CMAX)
             and Ho % 16 == 0 and Wo % 16 == 0 and (Ho == 2 * Hs if upsample else Ho == Hs)
-            and halo_splits(N, Ho, Wo, K, Cin) > 0)
+            and halo_splits(N, Ho, Wo, K, Cin, ztaps) > 0)
 
 
 def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, transposed=False, out_hw_=None,
@@ -232,14 +232,29 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         if x1 is None and x0.shape[-1] != K:
             raise ValueError("epilogue tensor channels must match the conv output channels")
     T = ks * ks * (ks if d3 else 1)
+    # host-side operand checks: the kernels index weights as [>=K rows][T][exactly C0+C1] (main) and
+    # [>=K][1][C2+C3] (1x1 segment); halo tiles as [K/128][C/32][9][32][128] blocks
+    if wgt is not None and (wgt.dim() != 3 or wgt.shape[0] < K or wgt.shape[1] != T or wgt.shape[2] != C0 + C1):
+        raise ValueError(f"conv weights {tuple(wgt.shape)} do not match K={K}, taps={T}, C={C0 + C1}")
+    if src2 is not None and wgt2 is not None and (wgt2.shape[0] < K or wgt2.shape[-1] != d.C2 + d.C3):
+        raise ValueError(f"1x1 segment weights {tuple(wgt2.shape)} do not match K={K}, C={d.C2 + d.C3}")
+    for tw, cc, taps in ((wgt_tiled, C0 + C1, 27 if d3 else 9), (wgt2_tiled if src2 is not None else None,
+                                                               d.C2 + d.C3, 1)):
+        if tw is not None and tw.numel() < -(-K // 128) * 128 * -(-cc // HALO_BK) * HALO_BK * taps:
+            raise ValueError(f"halo-tiled weights ({tw.numel()} elements) too small for K={K}, C={cc}")
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
     bpx = 256 if K <= 16 else 128
-    halo = not d3 and not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
-                                                            C0 + C1, pro is not None)
+    if d3:   # depth-tap chunks on the halo kernel: pre-tiled (kz, channel block) weights are required
+        halo = (not force_generic and wgt_tiled is not None and Ds == Do and
+                halo_eligible(N * Ds, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
+                              pro is not None, ztaps=3))
+    else:
+        halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
+                                                   C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
     if halo:
-        splits = halo_splits(N, Ho, Wo, K, C0 + C1)
+        splits = halo_splits(N * max(Ds, 1), Ho, Wo, K, C0 + C1, 3 if d3 else 1)
         bpx = 256
         if wgt_tiled is None:
             wgt_tiled = tile_weights(wgt)
@@ -269,6 +284,37 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
             st = channel_stats(out, y=(ep[0], ep[1], ep[0].shape[-1]))
         else:
             st = channel_stats(out)
+    return out, st
+
+
+def conv_combine(ws, K, out_shape, *, bias=None, bias2=None, bias_nc=None, resid=None, ep=None, out=None,
+                 accumulate=False, want_stats=False):
+    """out (bf16, N-D ``out_shape`` = (N, *sp)) = sum of the fp32 slabs ws [S][M][K] + conv epilogue
+    (fmd_conv_combine); returns (out, Stats)."""
+    N, sp = out_shape[0], tuple(out_shape[1:])
+    Do, Ho, Wo = (0, *sp) if len(sp) == 2 else sp
+    if out is None:
+        out = torch.empty((N, *sp, K), device=ws.device, dtype=BF16)
+    d = ConvDesc()
+    d.N, d.Ho, d.Wo, d.Do, d.Hs, d.Ws, d.Ds, d.K = N, Ho, Wo, Do, Ho, Wo, Do, K
+    d.ks, d.stride, d.pad = 3, 1, 1
+    d.ws, d.splits = _p(ws), ws.shape[0]
+    d.bias, d.bias2, d.bias_nc, d.resid, d.out = _p(bias), _p(bias2), _p(bias_nc), _p(resid), _p(out)
+    d.accumulate = int(accumulate)
+    if ep is not None:
+        x0, x1, ea, eb = ep
+        d.ep_x0, d.ep_x1, d.ep_C0, d.ep_a, d.ep_b = _p(x0), _p(x1), x0.shape[-1], _p(ea), _p(eb)
+    HWo = max(Do, 1) * Ho * Wo
+    M = N * HWo
+    st = None
+    fused = want_stats and not accumulate and K % 4 == 0 and HWo % SPLIT_STATS_ROWS == 0
+    if fused:
+        slab = torch.empty((M // SPLIT_STATS_ROWS, K, 2), device=ws.device, dtype=F32)
+        d.stats = _p(slab)
+        st = Stats(slab, SPLIT_STATS_ROWS)
+    _lib.call("fmd_conv_combine", C.byref(d), stream())
+    if want_stats and not fused:
+        st = channel_stats(out, y=(ep[0], ep[1], ep[0].shape[-1])) if ep is not None else channel_stats(out)
     return out, st
 
 

@@ -81,6 +81,11 @@ typedef struct fmd_conv_desc {
 int fmd_conv(const fmd_conv_desc* d, fmd_stream_t s);
 /* Halo-tiled 3x3 stride-1 conv; returns 1 (nothing launched) when the problem does not qualify. */
 int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t s);
+/* Split-K combine alone: d->out = sum of the d->splits fp32 slabs [splits][M][K] in d->ws + the conv epilogue
+ * (bias, bias2, bias_nc, resid, ep_*, stats with FMD_SPLIT_STATS_ROWS-pixel rows).  Replaces nothing on its
+ * own: it closes convolutions issued as several partial launches (3-D 3x3x3 convs as three depth-tap planes
+ * of the 2-D halo kernel, ConvND 3-D path, src/nn/ops/convolution.py:36). */
+int fmd_conv_combine(const fmd_conv_desc* d, fmd_stream_t s);
 /* GroupNorm-backward apply fused as a conv epilogue (fmd_conv_gn_apply):
  * dx = conv(d) + P*dz + Q*x + R (+ dx if acc), x/dx split over two concat sources at C0. */
 typedef struct fmd_gn_apply_desc {

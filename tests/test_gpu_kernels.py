@@ -796,3 +796,83 @@ def test_wgrad3d_vs_torch(mode):
             upsample=up, pro=pro, db=db)
     torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
     torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("case", ["fwd_concat_stats", "fwd_skip", "fwd_resid", "fwd_pro", "dgrad_ep_stats",
+                                  "dgrad_acc", "fwd_split"])
+def test_conv3d_depth_halo_matches_generic(case):
+    """3x3x3 s1 conv on the halo kernel with (depth tap, channel block) chunks vs the generic 3-D implicit GEMM
+    (itself checked against F.conv3d above); N = 2 so the depth-boundary zeros between samples are exercised."""
+    O = ops()
+    from fmdiff.runtime.engine import WeightCache
+    wc = WeightCache()
+    N, D, H, W = 2, 66, 16, 16                       # 132 slices x 1 tile: halo-eligible without split
+    if case == "fwd_split":
+        D = 24                                       # 48 slices: split-K over (kz, channel block) chunks
+    C0, C1, K = 64, (32 if case in ("fwd_concat_stats", "fwd_pro") else 0), 128
+    dgrad = case.startswith("dgrad")
+    x0 = _rand_ndhwc(N, D, H, W, C0, 71).to(DEV)
+    x1 = _rand_ndhwc(N, D, H, W, C1, 72).to(DEV) if C1 else None
+    g = torch.Generator().manual_seed(73)
+    Cin = C0 + C1
+    w = (torch.randn(K, Cin if not dgrad else C0, 3, 3, 3, generator=g) / math.sqrt(Cin * 27)).to(DEV)
+    if dgrad:   # data gradient of a C0 -> K conv: dy has K channels, the result C0
+        src, Kout, mode = _rand_ndhwc(N, D, H, W, K, 74).to(DEV), C0, 3
+    else:
+        src, Kout, mode = x0, K, 0
+    b = (torch.randn(Kout, generator=g) * 0.1).to(DEV)
+    kw, extra = {}, {}
+    if case in ("fwd_concat_stats", "fwd_split"):
+        kw = dict(bias=b, bias_nc=(torch.randn(N, Kout, generator=g) * 0.1).to(DEV), want_stats=True)
+    elif case == "fwd_pro":
+        a_ = (torch.rand(N, Cin, generator=g) + 0.5).to(DEV)
+        b_ = (torch.randn(N, Cin, generator=g) * 0.2).to(DEV)
+        kw = dict(bias=b, pro=(a_, b_, True), want_stats=True)
+    elif case == "fwd_skip":
+        ws_ = (torch.randn(K, C0, 1, 1, 1, generator=g) / 8).to(DEV)
+        x2 = _rand_ndhwc(N, D, H, W, C0, 75).to(DEV)
+        kw = dict(bias=b, bias2=(torch.randn(K, generator=g) * 0.1).to(DEV), want_stats=True, src2=x2)
+        extra = dict(wgt2=wc.get(ws_, 0), wgt2_tiled=wc.tiled(ws_, 0))
+    elif case == "fwd_resid":
+        kw = dict(bias=b, resid=_rand_ndhwc(N, D, H, W, K, 76).to(DEV), want_stats=True)
+    elif case == "dgrad_ep_stats":
+        xe = _rand_ndhwc(N, D, H, W, C0, 77).to(DEV)
+        kw = dict(ep=(xe, None, (torch.rand(N, C0, generator=g) + 0.5).to(DEV),
+                      (torch.randn(N, C0, generator=g) * 0.2).to(DEV)), want_stats=True)
+    else:
+        base = _rand_ndhwc(N, D, H, W, C0, 78).to(DEV)
+    src1 = x1 if not dgrad else None
+    halo_ok = O.halo_eligible(N * D, H, H, W, Kout, Cin=src.shape[-1] + (C1 if not dgrad else 0),
+                              pro="pro" in kw, ztaps=3)
+    assert halo_ok
+    if case == "dgrad_acc":
+        kw_g, kw_r = dict(out=base.clone(), accumulate=True), dict(out=base.clone(), accumulate=True)
+    else:
+        kw_g = kw_r = kw
+    got, st = O.conv(src, Kout, None, ks=3, stride=1, pad=1, src1=src1, wgt_tiled=wc.dtiled(w, mode),
+                     **{k: v for k, v in extra.items() if k == "wgt2_tiled"}, **kw_g)
+    ref, rst = O.conv(src, Kout, wc.get(w, mode), ks=3, stride=1, pad=1, src1=src1, force_generic=True,
+                      **{k: v for k, v in extra.items() if k == "wgt2"}, **kw_r)
+    _close(got, ref, rel=1e-2)
+    if kw.get("want_stats"):
+        t1 = st.slab.double().view(N, -1, Kout, 2).sum(1)
+        t2 = rst.slab.double().view(N, -1, Kout, 2).sum(1)
+        _close(t1, t2, rel=1e-2)
+
+
+def test_conv_combine_matches_torch():
+    """fmd_conv_combine: sum of fp32 split slabs + bias + residual -> bf16, with fused statistics."""
+    O = ops()
+    g = torch.Generator().manual_seed(81)
+    N, D, H, W, K = 2, 4, 8, 8, 64
+    M = N * D * H * W
+    ws = torch.randn(3, M, K, generator=g).to(DEV)
+    b = (torch.randn(K, generator=g) * 0.1).to(DEV)
+    r = _rand_ndhwc(N, D, H, W, K, 82).to(DEV)
+    out, st = O.conv_combine(ws, K, (N, D, H, W), bias=b, resid=r, want_stats=True)
+    ref = (ws.sum(0).view(N, D, H, W, K) + b + r.float()).to(torch.bfloat16)
+    _close(out, ref, rel=1e-2)
+    s = st.slab.double().view(N, -1, K, 2).sum(1)
+    rf = ref.double().view(N, -1, K)
+    _close(s[..., 0], rf.sum(1), rel=1e-3)
+    _close(s[..., 1], (rf * rf).sum(1), rel=1e-3)
