@@ -41,6 +41,8 @@ struct HWArgs {
   int C, ldy;
   int tiles_x, tiles_y, ntiles;    // pixel tiles over N x Ho x Wo
   int ntc, nci, splits, per_split;
+  int depth, ncc;                  // 3-D (depth > 0): tiles over the N*depth slices; input chunk tci =
+                                   // (depth tap kz, 64-channel block) = kz*ncc + cb reading slice z + kz - 1
 };
 
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU
@@ -60,7 +62,10 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   const int tci = b % A.nci; b /= A.nci;
   const int tco = b % A.ntc; b /= A.ntc;
   const int split = b;
-  const int co0 = tco * WCO, ci0 = tci * WCI;
+  const int kz = A.depth ? tci / A.ncc : 0;            // 3-D: depth tap of this workgroup's input chunk
+  const int zsh = A.depth ? kz - 1 : 0;
+  const int co0 = tco * WCO, ci0 = (A.depth ? tci - kz * A.ncc : tci) * WCI;
+  const int T = A.depth ? 27 : 9;
   const int t0 = split * A.per_split, t1 = min(A.ntiles, t0 + A.per_split);
   const bool do_bias = d.db != nullptr && tci == 0;
 
@@ -91,14 +96,17 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   auto load_tile = [&](int t) {
     int n, ty0, tx0;
     tile_org(t, n, ty0, tx0);
-    if (PRO != 0 && n != cur_n) {     // GN affine of this thread's 8 channels for image n
-      const f32x4* a4 = (const f32x4*)(d.pro_a + (size_t)n * A.C + c);
-      const f32x4* b4 = (const f32x4*)(d.pro_b + (size_t)n * A.C + c);
+    const int smp = A.depth ? n / A.depth : n;   // sample of image n (3-D: slices share the affine)
+    if (PRO != 0 && smp != cur_n) {   // GN affine of this thread's 8 channels for sample smp
+      const f32x4* a4 = (const f32x4*)(d.pro_a + (size_t)smp * A.C + c);
+      const f32x4* b4 = (const f32x4*)(d.pro_b + (size_t)smp * A.C + c);
       const f32x4 a0 = a4[0], a1 = a4[1], b0 = b4[0], b1 = b4[1];
 #pragma unroll
       for (int e = 0; e < 4; ++e) { pa[e] = a0[e]; pa[4 + e] = a1[e]; pb[e] = b0[e]; pb[4 + e] = b1[e]; }
-      cur_n = n;
+      cur_n = smp;
     }
+    const int zs = A.depth ? n - smp * A.depth + zsh : 0;
+    const bool zok = !A.depth || (zs >= 0 && zs < A.depth);
 #pragma unroll
     for (int k = 0; k < XLD; ++k) {
       const int q = tid + NT * k;
@@ -108,9 +116,9 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       // logical (possibly nearest-x2-upsampled) input coordinates; the upsample is a gather of the
       // stored low-resolution pixel, so the LDS image is the same as without it
       const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-      const bool valid = act && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
+      const bool valid = act && zok && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
       const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
-      const int pix = valid ? (n * d.Hs + sy) * d.Ws + sx : 0;
+      const int pix = valid ? ((n + zsh) * d.Hs + sy) * d.Ws + sx : 0;
       rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
     }
@@ -212,8 +220,8 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
     }
   }
 
-  // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout)
-  const size_t per = (size_t)d.K * 9 * A.C;
+  // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout; 3-D tap = kz*9 + ky*3 + kx)
+  const size_t per = (size_t)d.K * T * A.C;
   float* ws = d.ws + (size_t)split * per;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
         const int ci = ci0 + wci * 16 + l16;
-        ws[((size_t)co * 9 + tap) * A.C + ci] = acc[i][tap][r];
+        ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[i][tap][r];
       }
   if (do_bias) {
     // lanes of the 4 pixel groups, then the 4 cin-waves (each summed one k-step) of a cout half
@@ -251,23 +259,28 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 // 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
 // Returns 1 (nothing launched) when the problem does not qualify.  d->splits = pixel-tile splits.
 extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->Do > 0 || d->Ds > 0) return 1;
+  if (d->ks != 3 || d->stride != 1 || d->pad != 1) return 1;
+  const bool d3 = d->Do > 0 || d->Ds > 0;
+  if (d3 && (d->Ds != d->Do || d->upsample)) return 1;   // 3-D: stride-1 same-depth 3x3x3 only
+  const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (d->Ho % WTH || d->Wo % WTW) return 1;
   const int C = d->C0 + d->C1;
   if (d->K % WCO || C % WCI || (d->C0 % 8) || !d->ws) return 1;
   const int ldy = d->ldy > 0 ? d->ldy : d->K;
   if (ldy % 8) return 1;
-  if ((long long)d->N * d->Hs * d->Ws >= (1LL << 31) / 8) return 1;
+  if ((long long)Nn * d->Hs * d->Ws >= (1LL << 31) / 8) return 1;
   HWArgs A;
   A.d = *d;
   A.C = C;
   A.ldy = ldy;
   A.tiles_x = d->Wo / WTW;
   A.tiles_y = d->Ho / WTH;
-  A.ntiles = d->N * A.tiles_x * A.tiles_y;
+  A.ntiles = Nn * A.tiles_x * A.tiles_y;
   A.ntc = d->K / WCO;
-  A.nci = C / WCI;
+  A.depth = d3 ? d->Do : 0;
+  A.ncc = C / WCI;
+  A.nci = d3 ? 3 * A.ncc : A.ncc;
   A.splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.ntiles + A.splits - 1) / A.splits;
   const int nwg = A.ntc * A.nci * A.splits;

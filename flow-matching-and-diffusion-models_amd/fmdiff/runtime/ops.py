@@ -385,13 +385,14 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
     d.force_generic = int(force_generic)
     if splits is None:
-        if not d3 and not force_generic and wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample,
-                                                                 ldy):
-            # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk, pixel-tile split);
-            # partial slabs capped at ~96 MB (their write + reduce read)
-            tiles = N * (Ho // 8) * (Wo // 16)
-            base = (K // 128) * (Ct // 64)
-            splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36)))
+        if (not force_generic and (not d3 or (Ds == Do and not upsample)) and
+                wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample, ldy)):
+            # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk [x depth tap], pixel-tile
+            # split); partial slabs capped at ~96 MB (their write + reduce read)
+            zt = 3 if d3 else 1
+            tiles = N * max(Do, 1) * (Ho // 8) * (Wo // 16)
+            base = (K // 128) * (Ct // 64) * zt
+            splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36 * zt)))
         else:
             # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
             T = ks * ks * (ks if d3 else 1)

@@ -876,3 +876,28 @@ def test_conv_combine_matches_torch():
     rf = ref.double().view(N, -1, K)
     _close(s[..., 0], rf.sum(1), rel=1e-3)
     _close(s[..., 1], (rf * rf).sum(1), rel=1e-3)
+
+
+@pytest.mark.parametrize("pro,concat", [(True, False), (False, True)])
+def test_wgrad3d_depth_halo_matches_generic(pro, concat):
+    """3x3x3 weight gradient on the halo kernel with (depth tap, 64-channel block) input chunks vs the generic
+    3-D weight-gradient GEMM (checked against autograd of F.conv3d above); N = 2 exercises the sample
+    boundaries of the depth taps."""
+    O = ops()
+    N, D, H, W, C0, K = 2, 5, 8, 16, 64, 128
+    C1 = 64 if concat else 0
+    assert O.wgrad_halo_eligible(H, W, H, W, K, C0 + C1, C0)
+    x0 = _rand_ndhwc(N, D, H, W, C0, 91).to(DEV)
+    x1 = _rand_ndhwc(N, D, H, W, C1, 92).to(DEV) if C1 else None
+    dy = _rand_ndhwc(N, D, H, W, K, 93).to(DEV)
+    g = torch.Generator().manual_seed(94)
+    pk = (((torch.rand(N, C0 + C1, generator=g) + 0.5).to(DEV), (torch.randn(N, C0 + C1, generator=g) * 0.2).to(DEV),
+           True) if pro else None)
+    outs = []
+    for generic in (False, True):
+        dw = torch.zeros(K, C0 + C1, 3, 3, 3, device=DEV)
+        db = torch.zeros(K, device=DEV)
+        O.wgrad(x0, dy, dw, src1=x1, pro=pk, db=db, force_generic=generic)
+        outs.append((dw, db))
+    _close(outs[0][0], outs[1][0], rel=1e-2)
+    _close(outs[0][1], outs[1][1], rel=1e-3)
