@@ -158,6 +158,9 @@ UNET3D_CASES = {
     # attention at every level (linear attention, use_linear_attn defaults to True) + softmax in the middle
     "efficient_2d_attn": dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64],
                               attention_resolutions=[1, 2], sample_size=64),
+    # 32^3 x batch 2: the 3x3x3 convs / data / weight gradients of the top level take the depth-tap halo kernels
+    "efficient_32": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
+                         block_out_channels=[32, 64], attention_resolutions=[], sample_size=32),
     "diffusers": dict(unet_impl="diffusers_nd", spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
                       block_out_channels=[32, 64], down_block_types=["DownBlock2D", "AttnDownBlock2D"],
                       up_block_types=["AttnUpBlock2D", "UpBlock2D"], sample_size=16, norm_num_groups=8),
@@ -181,7 +184,8 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
     sd = U.seeded_state_dict(spec, 11)
     model.load_state_dict(sd)
     g = torch.Generator().manual_seed(5)
-    shape = (2, 1, 64, 64) if cfg.get("spatial_dims", 2) == 2 else (2, 1, 16, 16, 16)
+    S3 = cfg.get("sample_size", 16)
+    shape = (2, 1, 64, 64) if cfg.get("spatial_dims", 2) == 2 else (2, 1, S3, S3, S3)
     clean, ldct, noise = (torch.randn(*shape, generator=g) for _ in range(3))
     t = torch.rand(2, generator=g)
     Ntr = 1000
