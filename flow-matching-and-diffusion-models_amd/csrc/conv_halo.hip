@@ -51,8 +51,9 @@ struct HArgs {
   int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
   const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
   const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
-  int depth, ncb;         // 3-D (depth > 0): images are the N*depth slices; main chunk = (depth tap kz,
-                          // 32-channel block cb) = kz*ncb + cb, reading slice z + kz - 1 (zeros outside);
+  int depth, ncb, dsrc;   // 3-D (depth > 0): images are the N*depth output slices; main chunk = (depth tap
+                          // kz, 32-channel block cb) = kz*ncb + cb, reading logical input slice z + kz - 1
+                          // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
@@ -189,7 +190,7 @@ void conv3x3_halo(const HArgs A) {
   int cs = 0;                // its pixel stride
   int cch = 0;               // its first channel (GN affine table index)
   bool cok = false;
-  int zsh = 0;               // 3-D: source slice offset (kz - 1) of the chunk being staged
+  int srcsl = n;             // stored source image of the chunk being staged (3-D: depth-tap slice)
 
   auto setup = [&](int chunk) {
     if (chunk < A.nchunk1) {
@@ -198,8 +199,9 @@ void conv3x3_halo(const HArgs A) {
       if (A.depth) {
         const int kz = chunk / A.ncb;
         cb = chunk - kz * A.ncb;
-        zsh = kz - 1;
-        zok = zz + zsh >= 0 && zz + zsh < A.depth;
+        const int zl = zz + kz - 1;                 // logical input depth == output depth (stride 1)
+        zok = zl >= 0 && zl < A.depth;
+        srcsl = smp * A.dsrc + (UP ? zl >> 1 : zl);
       }
       const int c = cb * BK + kc * 8;
       cok = c < A.C && zok;
@@ -225,7 +227,7 @@ void conv3x3_halo(const HArgs A) {
       const int py = pos / HROW, px = pos - (pos / HROW) * HROW;   // constant divisor: mul-shift
       const int y = hy0 + py, x = hx0 + px;
       valid = on && cok && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
-      pix = ((n + zsh) * d.Hs + y) * d.Ws + x;
+      pix = (srcsl * d.Hs + y) * d.Ws + x;
       lpos = pos;
       act = on;
     } else {
@@ -662,7 +664,7 @@ __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, i
 extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;
-  if (d3 && (d->Ds != d->Do || d->upsample)) return 1;   // 3-D: stride-1 same-depth 3x3x3 only
+  if (d3 && d->Do != (d->upsample ? 2 * d->Ds : d->Ds)) return 1;   // 3-D: stride-1 3x3x3 (nearest-x2)
   const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
   if (d->splits > 1 && (!d->ws || d->stats)) return 1;
   if (d->Ho % TH || d->Wo % TW) return 1;
@@ -679,6 +681,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.tiles_y = d->Ho / TH;
   A.ntc = (d->K + BCO - 1) / BCO;
   A.depth = d3 ? d->Do : 0;
+  A.dsrc = d3 ? d->Ds : 0;
   A.ncb = (A.C + BK - 1) / BK;
   A.nchunk1 = d3 ? 3 * A.ncb : A.ncb;   // 3-D: weights pre-tiled as a 3*ncb*32-channel 2-D conv (kz-major)
   A.d.N = Nn;

@@ -41,8 +41,9 @@ struct HWArgs {
   int C, ldy;
   int tiles_x, tiles_y, ntiles;    // pixel tiles over N x Ho x Wo
   int ntc, nci, splits, per_split;
-  int depth, ncc;                  // 3-D (depth > 0): tiles over the N*depth slices; input chunk tci =
-                                   // (depth tap kz, 64-channel block) = kz*ncc + cb reading slice z + kz - 1
+  int depth, ncc, dsrc;            // 3-D (depth > 0): tiles over the N*depth output slices; input chunk
+                                   // tci = (depth tap kz, 64-channel block) = kz*ncc + cb reading logical
+                                   // slice z + kz - 1 (stored slice >> 1 under nearest-x2; dsrc = stored depth)
 };
 
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU
@@ -105,8 +106,9 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       for (int e = 0; e < 4; ++e) { pa[e] = a0[e]; pa[4 + e] = a1[e]; pb[e] = b0[e]; pb[4 + e] = b1[e]; }
       cur_n = smp;
     }
-    const int zs = A.depth ? n - smp * A.depth + zsh : 0;
-    const bool zok = !A.depth || (zs >= 0 && zs < A.depth);
+    const int zl = A.depth ? n - smp * A.depth + zsh : 0;   // logical input slice (== output depth range)
+    const bool zok = !A.depth || (zl >= 0 && zl < A.depth);
+    const int srcsl = A.depth ? smp * A.dsrc + (d.upsample ? zl >> 1 : zl) : n;
 #pragma unroll
     for (int k = 0; k < XLD; ++k) {
       const int q = tid + NT * k;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
       const bool valid = act && zok && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
       const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
-      const int pix = valid ? ((n + zsh) * d.Hs + sy) * d.Ws + sx : 0;
+      const int pix = valid ? (srcsl * d.Hs + sy) * d.Ws + sx : 0;
       rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
     }
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   if (d->ks != 3 || d->stride != 1 || d->pad != 1) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;
-  if (d3 && (d->Ds != d->Do || d->upsample)) return 1;   // 3-D: stride-1 same-depth 3x3x3 only
+  if (d3 && d->Do != (d->upsample ? 2 * d->Ds : d->Ds)) return 1;   // 3-D: stride-1 3x3x3 (nearest-x2)
   const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (d->Ho % WTH || d->Wo % WTW) return 1;
@@ -279,6 +281,7 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   A.ntiles = Nn * A.tiles_x * A.tiles_y;
   A.ntc = d->K / WCO;
   A.depth = d3 ? d->Do : 0;
+  A.dsrc = d3 ? d->Ds : 0;
   A.ncc = C / WCI;
   A.nci = d3 ? 3 * A.ncc : A.ncc;
   A.splits = d->splits > 1 ? d->splits : 1;

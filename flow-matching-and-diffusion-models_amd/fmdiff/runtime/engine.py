@@ -328,8 +328,11 @@ class UNetEngine:
         if len(sp) == 2:
             halo = stride == 1 and ops.halo_eligible(N_, sp[0], Ho_, ops.out_hw(sp[1], 3, stride, 1, upsample),
                                                      conv.out_channels, upsample=upsample, Cin=Cin)
-        else:
-            halo = stride == 1 and not upsample and self._halo_ok(N_, sp, conv.out_channels, Cin)
+        else:   # depth-tap halo, nearest-x2 included (output depth 2D)
+            Do_ = 2 * sp[0] if upsample else sp[0]
+            halo = DEPTH_HALO and stride == 1 and ops.halo_eligible(
+                N_ * Do_, sp[1], ops.out_hw(sp[1], 3, 1, 1, upsample), ops.out_hw(sp[2], 3, 1, 1, upsample),
+                conv.out_channels, upsample=upsample, Cin=Cin, ztaps=3)
         w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
                            bias=conv.bias, want_stats=True, wgt_tiled=wt)

@@ -246,15 +246,15 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
     bpx = 256 if K <= 16 else 128
     if d3:   # depth-tap chunks on the halo kernel: pre-tiled (kz, channel block) weights are required
-        halo = (not force_generic and wgt_tiled is not None and Ds == Do and
-                halo_eligible(N * Ds, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
+        halo = (not force_generic and wgt_tiled is not None and Do == (2 * Ds if upsample else Ds) and
+                halo_eligible(N * Do, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
                               pro is not None, ztaps=3))
     else:
         halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
                                                    C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
     if halo:
-        splits = halo_splits(N * max(Ds, 1), Ho, Wo, K, C0 + C1, 3 if d3 else 1)
+        splits = halo_splits(N * max(Do, 1), Ho, Wo, K, C0 + C1, 3 if d3 else 1)
         bpx = 256
         if wgt_tiled is None:
             wgt_tiled = tile_weights(wgt)
@@ -385,7 +385,7 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
     d.force_generic = int(force_generic)
     if splits is None:
-        if (not force_generic and (not d3 or (Ds == Do and not upsample)) and
+        if (not force_generic and (not d3 or Do == (2 * Ds if upsample else Ds)) and
                 wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample, ldy)):
             # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk [x depth tap], pixel-tile
             # split); partial slabs capped at ~96 MB (their write + reduce read)

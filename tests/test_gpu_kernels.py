@@ -799,7 +799,7 @@ def test_wgrad3d_vs_torch(mode):
 
 
 @pytest.mark.parametrize("case", ["fwd_concat_stats", "fwd_skip", "fwd_resid", "fwd_pro", "dgrad_ep_stats",
-                                  "dgrad_acc", "fwd_split"])
+                                  "dgrad_acc", "fwd_split", "fwd_up"])
 def test_conv3d_depth_halo_matches_generic(case):
     """3x3x3 s1 conv on the halo kernel with (depth tap, channel block) chunks vs the generic 3-D implicit GEMM
     (itself checked against F.conv3d above); N = 2 so the depth-boundary zeros between samples are exercised."""
@@ -811,7 +811,8 @@ def test_conv3d_depth_halo_matches_generic(case):
         D = 24                                       # 48 slices: split-K over (kz, channel block) chunks
     C0, C1, K = 64, (32 if case in ("fwd_concat_stats", "fwd_pro") else 0), 128
     dgrad = case.startswith("dgrad")
-    x0 = _rand_ndhwc(N, D, H, W, C0, 71).to(DEV)
+    up = case == "fwd_up"                            # nearest-x2 source: (D/2, H/2, W/2)
+    x0 = _rand_ndhwc(N, D // 2, H // 2, W // 2, C0, 71).to(DEV) if up else _rand_ndhwc(N, D, H, W, C0, 71).to(DEV)
     x1 = _rand_ndhwc(N, D, H, W, C1, 72).to(DEV) if C1 else None
     g = torch.Generator().manual_seed(73)
     Cin = C0 + C1
@@ -833,6 +834,8 @@ def test_conv3d_depth_halo_matches_generic(case):
         x2 = _rand_ndhwc(N, D, H, W, C0, 75).to(DEV)
         kw = dict(bias=b, bias2=(torch.randn(K, generator=g) * 0.1).to(DEV), want_stats=True, src2=x2)
         extra = dict(wgt2=wc.get(ws_, 0), wgt2_tiled=wc.tiled(ws_, 0))
+    elif case == "fwd_up":
+        kw = dict(bias=b, want_stats=True, upsample=True)
     elif case == "fwd_resid":
         kw = dict(bias=b, resid=_rand_ndhwc(N, D, H, W, K, 76).to(DEV), want_stats=True)
     elif case == "dgrad_ep_stats":
@@ -842,8 +845,8 @@ def test_conv3d_depth_halo_matches_generic(case):
     else:
         base = _rand_ndhwc(N, D, H, W, C0, 78).to(DEV)
     src1 = x1 if not dgrad else None
-    halo_ok = O.halo_eligible(N * D, H, H, W, Kout, Cin=src.shape[-1] + (C1 if not dgrad else 0),
-                              pro="pro" in kw, ztaps=3)
+    halo_ok = O.halo_eligible(N * D, H // 2 if up else H, H, W, Kout, upsample=up,
+                              Cin=src.shape[-1] + (C1 if not dgrad else 0), pro="pro" in kw, ztaps=3)
     assert halo_ok
     if case == "dgrad_acc":
         kw_g, kw_r = dict(out=base.clone(), accumulate=True), dict(out=base.clone(), accumulate=True)
@@ -878,17 +881,20 @@ def test_conv_combine_matches_torch():
     _close(s[..., 1], (rf * rf).sum(1), rel=1e-3)
 
 
-@pytest.mark.parametrize("pro,concat", [(True, False), (False, True)])
-def test_wgrad3d_depth_halo_matches_generic(pro, concat):
+@pytest.mark.parametrize("pro,concat,up", [(True, False, False), (False, True, False), (True, False, True)])
+def test_wgrad3d_depth_halo_matches_generic(pro, concat, up):
     """3x3x3 weight gradient on the halo kernel with (depth tap, 64-channel block) input chunks vs the generic
     3-D weight-gradient GEMM (checked against autograd of F.conv3d above); N = 2 exercises the sample
     boundaries of the depth taps."""
     O = ops()
     N, D, H, W, C0, K = 2, 5, 8, 16, 64, 128
     C1 = 64 if concat else 0
-    assert O.wgrad_halo_eligible(H, W, H, W, K, C0 + C1, C0)
-    x0 = _rand_ndhwc(N, D, H, W, C0, 91).to(DEV)
-    x1 = _rand_ndhwc(N, D, H, W, C1, 92).to(DEV) if C1 else None
+    sd, sh, sw = (D // 2 + 1, H // 2, W // 2) if up else (D, H, W)
+    if up:
+        D = 2 * sd
+    assert O.wgrad_halo_eligible(sh, sw, H, W, K, C0 + C1, C0, upsample=up)
+    x0 = _rand_ndhwc(N, sd, sh, sw, C0, 91).to(DEV)
+    x1 = _rand_ndhwc(N, sd, sh, sw, C1, 92).to(DEV) if C1 else None
     dy = _rand_ndhwc(N, D, H, W, K, 93).to(DEV)
     g = torch.Generator().manual_seed(94)
     pk = (((torch.rand(N, C0 + C1, generator=g) + 0.5).to(DEV), (torch.randn(N, C0 + C1, generator=g) * 0.2).to(DEV),
@@ -897,7 +903,7 @@ def test_wgrad3d_depth_halo_matches_generic(pro, concat):
     for generic in (False, True):
         dw = torch.zeros(K, C0 + C1, 3, 3, 3, device=DEV)
         db = torch.zeros(K, device=DEV)
-        O.wgrad(x0, dy, dw, src1=x1, pro=pk, db=db, force_generic=generic)
+        O.wgrad(x0, dy, dw, src1=x1, pro=pk, db=db, force_generic=generic, upsample=up)
         outs.append((dw, db))
     _close(outs[0][0], outs[1][0], rel=1e-2)
     _close(outs[0][1], outs[1][1], rel=1e-3)
