@@ -102,56 +102,85 @@ FMD_DEV ARow arow(const AGeo& g, int which, int h, int r, int d0) {
   return w;
 }
 
-// one wave per 64 query rows; online softmax over 64-key LDS blocks
-__global__ __launch_bounds__(64) void attn_fwd_kernel(const bf16r* __restrict__ qsrc, const bf16r* __restrict__ kvsrc,
-                                                      AGeo g, bf16r* __restrict__ o, float* __restrict__ lse) {
-  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int Tk = g.Tk, dh = g.dh;
+// Blocked forward for long sequences (T * dh beyond the slab kernels, e.g. the VAE mid-block at 32x32):
+// 64 query rows per 256-thread workgroup, 4 lanes per row splitting the head dim (16 each), keys / values
+// staged 64 rows at a time into LDS as fp32 with one index division per 16-element run (ARow).
+__global__ __launch_bounds__(256) void attn_fwd_blocked(const bf16r* __restrict__ qsrc,
+                                                        const bf16r* __restrict__ kvsrc, AGeo g,
+                                                        bf16r* __restrict__ o, float* __restrict__ lse) {
+  constexpr int KB = 64, LD = DMAX + 4;
+  const int h = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int dh = g.dh, Tk = g.Tk;
   const bf16r* qb = qsrc + b * g.qstride();
   const bf16r* kb = kvsrc + b * g.kvstride();
-  const int r = qblk * 64 + threadIdx.x;
+  const int j = t >> 2, d0 = (t & 3) * 16;
+  const int r = blockIdx.x * KB + j;
   const bool live = r < g.Tq;
   const float scale = 1.0f / sqrtf((float)dh);
-  float q[DMAX], acc[DMAX];
+  __shared__ __attribute__((aligned(16))) float ks[KB * LD], vs[KB * LD];
+  float q[16], acc[16];
+  {
+    ARow w = arow(g, 0, h, live ? r : 0, d0);
 #pragma unroll
-  for (int d = 0; d < DMAX; ++d) {
-    q[d] = (live && d < dh) ? bf2f(qb[g.off(0, h, r, d)]) * scale : 0.f;
-    acc[d] = 0.f;
+    for (int i = 0; i < 16; ++i) {
+      q[i] = (live && d0 + i < dh) ? bf2f(qb[w.cur()]) * scale : 0.f;
+      acc[i] = 0.f;
+      w.next();
+    }
   }
-  __shared__ float ks[64][DMAX + 1], vs[64][DMAX + 1];
   float m = -INFINITY, l = 0.f;
-  for (int k0 = 0; k0 < Tk; k0 += 64) {
+  for (int k0 = 0; k0 < Tk; k0 += KB) {
     __syncthreads();
-    for (int i = threadIdx.x; i < 64 * dh; i += 64) {
-      const int kr = i / dh, d = i - (i / dh) * dh;
-      const bool ok = k0 + kr < Tk;
-      ks[kr][d] = ok ? bf2f(kb[g.off(1, h, k0 + kr, d)]) : 0.f;
-      vs[kr][d] = ok ? bf2f(kb[g.off(2, h, k0 + kr, d)]) : 0.f;
+    {
+      const int kr = t >> 2, kd = (t & 3) * 16, rr = k0 + kr;
+      const bool ok = rr < Tk;
+      ARow wk = arow(g, 1, h, ok ? rr : 0, kd), wv = arow(g, 2, h, ok ? rr : 0, kd);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool e = ok && kd + i < dh;
+        ks[kr * LD + kd + i] = e ? bf2f(kb[wk.cur()]) : 0.f;
+        vs[kr * LD + kd + i] = e ? bf2f(kb[wv.cur()]) : 0.f;
+        wk.next();
+        wv.next();
+      }
     }
     __syncthreads();
-    const int nk = min(64, Tk - k0);
-    for (int j = 0; j < nk; ++j) {
+    const int nk = min(KB, Tk - k0);
+    for (int jj = 0; jj < nk; ++jj) {
+      const float* kr = ks + jj * LD + d0;
       float sc = 0.f;
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d)
-        if (d < dh) sc += q[d] * ks[j][d];
+      for (int i = 0; i < 16; i += 4) {
+        const float4 kv = *(const float4*)(kr + i);
+        sc += q[i] * kv.x + q[i + 1] * kv.y + q[i + 2] * kv.z + q[i + 3] * kv.w;
+      }
+      sc += __shfl_xor(sc, 1);
+      sc += __shfl_xor(sc, 2);
       const float mn = fmaxf(m, sc);
-      const float corr = __expf(m - mn);
-      const float p = __expf(sc - mn);
+      const float corr = __expf(m - mn), p = __expf(sc - mn);
       l = l * corr + p;
+      const float* vr = vs + jj * LD + d0;
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d)
-        if (d < dh) acc[d] = acc[d] * corr + p * vs[j][d];
+      for (int i = 0; i < 16; i += 4) {
+        const float4 vv = *(const float4*)(vr + i);
+        acc[i] = acc[i] * corr + p * vv.x;
+        acc[i + 1] = acc[i + 1] * corr + p * vv.y;
+        acc[i + 2] = acc[i + 2] * corr + p * vv.z;
+        acc[i + 3] = acc[i + 3] * corr + p * vv.w;
+      }
       m = mn;
     }
   }
   if (!live) return;
   const float inv = 1.f / l;
   bf16r* ob = o + b * g.ostride();
+  ARow w = arow(g, 3, h, r, d0);
 #pragma unroll
-  for (int d = 0; d < DMAX; ++d)
-    if (d < dh) ob[g.off(3, h, r, d)] = (bf16r)f2bf(acc[d] * inv);
-  lse[((size_t)b * g.heads + h) * g.Tq + r] = m + logf(l);
+  for (int i = 0; i < 16; ++i) {
+    if (d0 + i < dh) ob[w.cur()] = (bf16r)f2bf(acc[i] * inv);
+    w.next();
+  }
+  if ((t & 3) == 0) lse[((size_t)b * g.heads + h) * g.Tq + r] = m + logf(l);
 }
 
 // pass 1 (per query row): delta = sum_d dO*O, dQ = scale * sum_k dS K
@@ -537,7 +566,7 @@ extern "C" int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t 
   const AGeo g{T, T, heads, dh, heads * dh, raw, 0};
   if (!g.fits()) return -1;
   dim3 grid((T + 63) / 64, heads, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(64), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)qkv, g,
+  hipLaunchKernelGGL(attn_fwd_blocked, grid, dim3(256), 0, (hipStream_t)s, (const bf16r*)qkv, (const bf16r*)qkv, g,
                      (bf16r*)o, lse);
   return (int)hipGetLastError();
 }
@@ -1036,8 +1065,8 @@ extern "C" int fmd_cross_attention_fwd(const void* q, const void* kv, int32_t B,
   if (B < 1 || !geo_ok(g)) return -1;
   if (linear)
     return la_fwd((const bf16r*)q, (const bf16r*)kv, g, B, eps, (bf16r*)o, lse_or_state, ws, (hipStream_t)s);
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((Tq + 63) / 64, heads, B), dim3(64), 0, (hipStream_t)s, (const bf16r*)q,
-                     (const bf16r*)kv, g, (bf16r*)o, lse_or_state);
+  hipLaunchKernelGGL(attn_fwd_blocked, dim3((Tq + 63) / 64, heads, B), dim3(256), 0, (hipStream_t)s,
+                     (const bf16r*)q, (const bf16r*)kv, g, (bf16r*)o, lse_or_state);
   return (int)hipGetLastError();
 }
 

@@ -297,7 +297,8 @@ def test_groupnorm_deferred_gamma_beta_fold():
         assert torch.equal(a0, a1) and torch.equal(b0, b1)
 
 
-@pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32), (1, 64, 2, 16)])
+@pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32), (1, 64, 2, 16),
+                                         (1, 1024, 4, 64), (0, 300, 2, 40)])
 def test_attention(raw, T, heads, dh):
     O = ops()
     B = 2
