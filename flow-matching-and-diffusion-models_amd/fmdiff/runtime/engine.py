@@ -564,7 +564,7 @@ class UNetEngine:
             qparts = None
         elif isinstance(m, DiffusersAttentionND):
             if m.context_dim is not None:
-                raise NotImplementedError("cross-attention DiffusersAttentionND is not yet on the fmdiff engine")
+                return self.cross_attention(m, x, ctx)
             norm, heads, dh, inner, raw = m.group_norm, m.heads, m.head_dim, m.channels, 0
             qparts = (m.to_q, m.to_k, m.to_v)
             wq = self.wc.fused([l.weight for l in qparts], "w")
@@ -624,28 +624,42 @@ class UNetEngine:
             raise ValueError(f"Context channels mismatch: expected {cdim}, got {context.shape}.")
         return context.float().reshape(context.shape[0], cdim, -1).contiguous(), False
 
-    def cross_attention(self, m: SpatialCrossAttention, x: Act, ctx: Ctx):
-        """SpatialCrossAttention (attention.py:157-189): GN(x) folded into the q 1x1 gather; context_norm of the
-        context into the kv 1x1 operand (fmd_context_norm_fwd); raw head split; softmax or linear attention
-        over the context tokens; proj_out + residual in one epilogue.  No gradient flows into the context."""
+    def cross_attention(self, m, x: Act, ctx: Ctx):
+        """SpatialCrossAttention (attention.py:157-189) or DiffusersAttentionND with a context (:236-274):
+        GN(x) folded into the q projection's gather; context_norm of the context into the k|v projection
+        operand (fmd_context_norm_fwd); raw (Spatial) or view/transpose (Diffusers) head split; softmax or
+        linear attention over the context tokens; output projection + residual in one epilogue.  No gradient
+        flows into the context."""
         if ctx.cca is None:
-            raise ValueError("SpatialCrossAttention requires a non-empty context tensor.")
+            raise ValueError(f"{type(m).__name__} cross-attention requires a non-empty context tensor.")
+        if isinstance(m, SpatialCrossAttention):
+            norm, cnm, heads, dh, inner, raw = m.norm, m.context_norm, m.heads, m.dim_head, m.inner_dim, 1
+            lin = m.attention.eps if m.use_linear else None
+            wq, bq = m.q_proj.weight, m.q_proj.bias
+            kvp = [(m.kv_proj.weight, m.kv_proj.bias)]          # one projection: k | v
+            wo, bo = m.proj_out.weight, m.proj_out.bias
+        else:
+            norm, cnm, heads, dh, inner, raw = m.group_norm, m.context_norm, m.heads, m.head_dim, m.channels, 0
+            lin = None
+            wq, bq = m.to_q.weight, m.to_q.bias
+            kvp = [(m.to_k.weight, m.to_k.bias), (m.to_v.weight, m.to_v.bias)]
+            wo, bo = m.to_out[0].weight, m.to_out[0].bias
+        if len(kvp) == 1:
+            wkv, bkv = kvp[0]
+        else:   # to_k / to_v as one fused projection
+            wkv, bkv = self.wc.fused([w for w, _ in kvp], "w"), self.wc.fused([b for _, b in kvp], "b")
         cf, tok = self._context_flat(ctx.cca, m.context_dim)
         Tk = cf.shape[1] if tok else cf.shape[2]
         N, Cc, sp = x.t.shape[0], x.t.shape[-1], tuple(x.t.shape[1:-1])
         T = math.prod(sp)
         H, W = T // sp[-1], sp[-1]
         x4 = x.t.view(N, H, W, Cc)
-        norm, cnm, heads, dh, inner = m.norm, m.context_norm, m.heads, m.dim_head, m.inner_dim
-        lin = m.attention.eps if m.use_linear else None
         Cp = max(8, -(-m.context_dim // 8) * 8)
-        wq, bq, wkv, bkv = m.q_proj.weight, m.q_proj.bias, m.kv_proj.weight, m.kv_proj.bias
-        wo, bo = m.proj_out.weight, m.proj_out.bias
         a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
         q, _ = ops.conv(x4, inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
         cn, cmr = ops.context_norm_fwd(cf, tok, cnm.num_groups, cnm.eps, cnm.weight, cnm.bias, Cp)
         kv, _ = ops.conv(cn, 2 * inner, self.wc.get(wkv, 0, None, Cp), ks=1, pad=0, bias=bkv)
-        o, saved = ops.cross_attention_fwd(q, kv, T, Tk, heads, dh, lin)
+        o, saved = ops.cross_attention_fwd(q, kv, T, Tk, heads, dh, lin, raw)
         o4 = o.view(N, H, W, inner)
         out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
         y = Act(out.view(x.t.shape), st)
@@ -656,13 +670,19 @@ class UNetEngine:
             dy = y.grad.view(N, H, W, Cc)
             self._wg(lambda: ops.wgrad(o4, dy, wo.grad, ks=1, pad=0, db=bo.grad))
             do, _ = ops.conv(dy, inner, self.wc.get(wo, 1), ks=1, pad=0, transposed=True, out_hw_=(H, W))
-            dq, dkv = ops.cross_attention_bwd(q, kv, o, do, saved, T, Tk, heads, dh, lin)
+            dq, dkv = ops.cross_attention_bwd(q, kv, o, do, saved, T, Tk, heads, dh, lin, raw)
 
             def wg():
                 ops.wgrad(x4, dq, wq.grad, ks=1, pad=0, pro=(a, b, False), db=bq.grad)
-                tgt = self._wgrad_target(m.kv_proj, Cp)
-                ops.wgrad(cn, dkv, tgt, ks=1, pad=0, db=bkv.grad)
-                self._wgrad_finish(m.kv_proj, Cp, tgt)
+                off = 0
+                for w_, b_ in kvp:   # context channels padded to Cp: through a temporary unless they match
+                    Ki = w_.shape[0]
+                    tgt = w_.grad if w_.shape[1] == Cp else torch.zeros((Ki, Cp, *w_.shape[2:]), device=w_.device,
+                                                                       dtype=F32)
+                    ops.wgrad(cn, dkv, tgt, ks=1, pad=0, db=b_.grad, dy_offset=off)
+                    if tgt is not w_.grad:
+                        w_.grad.add_(tgt[:, :m.context_dim])
+                    off += Ki
             self._wg(wg)
             dcn, _ = ops.conv(dkv, Cp, self.wc.get(wkv, 1, None, Cp), ks=1, pad=0, transposed=True, out_hw_=(Tk, 1))
             ops.context_norm_bwd(cf, tok, cnm.num_groups, cmr, dcn, cnm.weight.grad, cnm.bias.grad)

@@ -581,7 +581,7 @@ def linear_attention_bwd(qkv, dout, state, T, heads, dh, raw, eps=1e-6):
     return dqkv
 
 
-def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None):
+def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None, raw=1):
     """SpatialCrossAttention core (csrc/attention.hip): q [B][Tq][inner], kv [B][Tk][2*inner] -> (o, saved),
     softmax (saved = lse) or LinearQKVAttention when ``linear_eps`` is given (saved = state)."""
     B = q.shape[0]
@@ -593,18 +593,18 @@ def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None):
     else:
         saved = torch.empty((B, heads, Tq), device=q.device, dtype=F32)
         ws = None
-    _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, 1, int(lin),
+    _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, int(raw), int(lin),
               float(linear_eps or 0.0), _p(o), _p(saved), _p(ws), stream())
     return o, saved
 
 
-def cross_attention_bwd(q, kv, o, dout, saved, Tq, Tk, heads, dh, linear_eps=None):
+def cross_attention_bwd(q, kv, o, dout, saved, Tq, Tk, heads, dh, linear_eps=None, raw=1):
     B = q.shape[0]
     lin = linear_eps is not None
     ws = _la_workspace(B, heads, q.device) if lin else torch.empty((B, heads, Tq), device=q.device, dtype=F32)
     dq, dkv = torch.empty_like(q), torch.empty_like(kv)
-    _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(ws), B, Tq, Tk, heads, dh, 1,
-              int(lin), float(linear_eps or 0.0), _p(dq), _p(dkv), stream())
+    _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(ws), B, Tq, Tk, heads, dh,
+              int(raw), int(lin), float(linear_eps or 0.0), _p(dq), _p(dkv), stream())
     return dq, dkv
 
 

@@ -225,8 +225,9 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
     assert worst[0] > 0.99, worst
 
 
-@pytest.mark.parametrize("ctx_layout", ["nchw", "tokens_last"])
-def test_cross_attention_unet_vs_oracle(ctx_layout):
+@pytest.mark.parametrize("ctx_layout,impl", [("nchw", "efficient"), ("tokens_last", "efficient"),
+                                             ("nchw", "diffusers")])
+def test_cross_attention_unet_vs_oracle(ctx_layout, impl):
     """conditioning "attention" (configs/LDCT/PixelAttention/*): EfficientUNetND with linear self- and
     cross-attention at ds 2 and softmax cross-attention in the middle, context_ca = a 4-channel latent;
     forward and FM train-step parameter gradients vs the oracle (context_norm gamma/beta included)."""
@@ -234,9 +235,15 @@ def test_cross_attention_unet_vs_oracle(ctx_layout):
     from fmdiff.models.generators import DiffusionUNetFactory
     from oracle import spec as S
     from oracle import unet as U
-    cfg = dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64], sample_size=32,
-               cross_attention_dim=4, attention_resolutions=[2], cross_attention_resolutions=[2],
-               cross_attention_in_middle=True)
+    if impl == "efficient":
+        cfg = dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64], sample_size=32,
+                   cross_attention_dim=4, attention_resolutions=[2], cross_attention_resolutions=[2],
+                   cross_attention_in_middle=True)
+    else:   # configs/LDCT/PixelAttention/*_diffusers_nd.json layout: DiffusersAttentionND with a context
+        cfg = dict(unet_impl="diffusers_nd", in_channels=1, out_channels=1, layers_per_block=1,
+                   block_out_channels=[32, 64], down_block_types=["DownBlock2D", "AttnDownBlock2D"],
+                   up_block_types=["AttnUpBlock2D", "UpBlock2D"], sample_size=32, norm_num_groups=8,
+                   cross_attention_dim=4, attention_head_dim=8)
     model = DiffusionUNetFactory().build(cfg, "attention", 1).to(DEV)
     spec = S.derive_spec(cfg, "attention", 1)
     sd = U.seeded_state_dict(spec, 21)
