@@ -293,7 +293,7 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 __global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                    float* __restrict__ v, long long n, const int* __restrict__ step_ctr,
                                    float base_lr, int warmup, int total, float b1, float b2, float eps, float wd,
-                                   float grad_scale) {
+                                   float grad_scale, int vec) {
   const int step = step_ctr[0] + 1;          // optimizer.step() count, 1-based
   const int s = step - 1;                    // lr_scheduler.step() calls so far
   double lam;
@@ -307,18 +307,36 @@ __global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restric
   const float lr = (float)(base_lr * lam);
   const float bc1 = (float)(1.0 - pow((double)b1, step));
   const float bc2s = sqrtf((float)(1.0 - pow((double)b2, step)));
-  GRID_STRIDE(i, n) {
-    float pv = p[i];
-    const float gv = g[i] * grad_scale;
+  auto upd = [&](float& pv, float gv, float& mv, float& vv) {
+    gv *= grad_scale;
     pv = pv * (1.f - lr * wd);
-    float mv = m[i];
     mv = mv + (gv - mv) * (1.f - b1);
-    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
-    m[i] = mv;
-    v[i] = vv;
+    vv = vv * b2 + (1.f - b2) * gv * gv;
     const float denom = sqrtf(vv) / bc2s + eps;
     pv = pv - (lr / bc1) * (mv / denom);
+  };
+  // 16-byte accesses over the (16-byte aligned) flat buffers; the n % 4 tail element-wise
+  const long long n4 = vec ? n >> 2 : 0;
+  GRID_STRIDE(i, n4) {
+    f32x4 pv = ((const f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], me = mv[e], ve = vv[e];
+      upd(pe, gv[e], me, ve);
+      pv[e] = pe;
+      mv[e] = me;
+      vv[e] = ve;
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+  }
+  for (long long i = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float pv = p[i], mv = m[i], vv = v[i];
+    upd(pv, g[i], mv, vv);
     p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
   }
 }
 
@@ -829,8 +847,10 @@ int fmd_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
 int fmd_adamw_sched(float* p, const float* g, float* m, float* v, int64_t n, const int32_t* step_ctr, float base_lr,
                     int32_t warmup, int32_t total, float beta1, float beta2, float eps, float wd, float grad_scale,
                     fmd_stream_t s) {
-  LAUNCH(adamw_sched_kernel, grid_for(n, 256, 8192), p, g, m, v, (long long)n, step_ctr, base_lr, warmup, total,
-         beta1, beta2, eps, wd, grad_scale);
+  const int vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                    reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+  LAUNCH(adamw_sched_kernel, grid_for(vec ? n / 4 : n, 256, 8192), p, g, m, v, (long long)n, step_ctr, base_lr, warmup,
+         total, beta1, beta2, eps, wd, grad_scale, vec);
 }
 
 int fmd_flow_euler(float* x, const float* v, int32_t Kpad, const float* sigmas, const int32_t* index, int32_t N,

@@ -908,3 +908,27 @@ def test_wgrad3d_depth_halo_matches_generic(pro, concat, up):
         outs.append((dw, db))
     _close(outs[0][0], outs[1][0], rel=1e-2)
     _close(outs[0][1], outs[1][1], rel=1e-3)
+
+
+@pytest.mark.parametrize("n,offset", [(10001, 0), (4096, 1)])
+def test_adamw_sched_matches_torch_with_cosine_warmup(n, offset):
+    """fmd_adamw_sched (device-side step counter, get_cosine_schedule_with_warmup LR) vs torch.optim.AdamW +
+    transformers' schedule, on a length with a tail and on a misaligned (element-offset) buffer."""
+    from transformers import get_cosine_schedule_with_warmup
+    O = ops()
+    torch.manual_seed(1)
+    p0 = torch.randn(n)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=2e-3, weight_decay=0.01, foreach=False)
+    sch = get_cosine_schedule_with_warmup(opt, 2, 6)
+    buf = lambda t: torch.cat([torch.zeros(offset), t]).to(DEV)[offset:]
+    p, m, v = buf(p0), buf(torch.zeros(n)), buf(torch.zeros(n))
+    ctr = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(5):
+        g = torch.randn(n)
+        ref.grad = g.clone()
+        opt.step()
+        sch.step()
+        O.adamw_sched(p, buf(g), m, v, ctr, 2e-3, 2, 6, wd=0.01)
+        O.counter_add(ctr)
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
