@@ -21,6 +21,12 @@
 // 8 consecutive positions per channel group, so the 8-lane groups of
 // ds_write_b128 are conflict-free too.
 //
+// 3-D (3x3x3, stride 1, optionally nearest-x2): the N*D output depth slices are the images and the main
+// reduction runs over (depth tap kz, 32-channel block) chunks; chunk kz stages the 18x18 halo of input slice
+// z + kz - 1 (zeros past either end of a sample; slice >> 1 under nearest-x2), so all 27 taps accumulate in
+// one launch with the same prologue / epilogue, and the per-sample tables are indexed by slice / D.  The
+// weights are pre-tiled as a 2-D conv over 3 * C32 input channels (engine WeightCache.dtiled).
+//
 // Same epilogue contract as csrc/conv.hip (bias, per-sample bias, residual,
 // second 1x1 GEMM over src2|src3, data-gradient SiLU' + GN-backward sums,
 // channel statistics).

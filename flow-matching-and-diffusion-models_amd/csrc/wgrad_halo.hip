@@ -16,6 +16,10 @@
 // MFMAs run; one barrier per tile.  Partial sums go to a split-K slab reduced by
 // wgrad_reduce (csrc/wgrad.hip), which writes the reference [K][C][3][3] layout.
 //
+// 3-D (3x3x3): tiles run over the N*D output slices and a workgroup's input chunk is a (depth tap kz,
+// 64-channel block) pair staging slice z + kz - 1 (zeros outside the sample, >> 1 under nearest-x2); its
+// 9 accumulated taps land at taps kz*9 .. kz*9+8 of a 27-tap slab, so wgrad_reduce writes [K][C][3][3][3].
+//
 // Replaces: autograd of nn.Conv2d weight/bias (src/nn/ops/convolution.py:53) for
 // the ResBlock 3x3 convs (src/nn/blocks/residual.py:71-76).
 #include "common.h"
