@@ -224,6 +224,21 @@ __global__ void noise_prepare_kernel(const float* __restrict__ x0, const float* 
   }
 }
 
+// diffusers DDPMScheduler.add_noise in fp32: out = sa[t[n]] * x0 + sb[t[n]] * noise with both products
+// rounded before the add (no FMA contraction), which is torch's eager operation order: bit-exact.
+__global__ void add_noise_kernel(const float* __restrict__ x0, const float* __restrict__ noise,
+                                 const float* __restrict__ sa, const float* __restrict__ sb,
+                                 const long long* __restrict__ ts, long long per, int N, float* __restrict__ out) {
+  const long long total = (long long)N * per;
+  GRID_STRIDE(i, total) {
+#pragma clang fp contract(off)
+    const long long t = ts[i / per];
+    const float a = sa[t] * x0[i];
+    const float b = sb[t] * noise[i];
+    out[i] = a + b;
+  }
+}
+
 // partial sums of (pred - target)^2; dpred = scale * 2 (pred - target) / numel (bf16, NHWC, Kpad channels)
 __global__ void mse_kernel(const float* __restrict__ pred, int Kpad, const float* __restrict__ ta,
                            const float* __restrict__ tb, float tb_sign, int N, int Cx, int HW, float inv_numel,
@@ -344,6 +359,7 @@ __global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restric
 __global__ void flow_euler_kernel(float* __restrict__ x, const float* __restrict__ vout, int Kpad,
                                   const float* __restrict__ sigmas, const int* __restrict__ index, int N, int Cx,
                                   int HW, const float* __restrict__ cond, int Cc, int Cpad, bf16r* __restrict__ next) {
+#pragma clang fp contract(off)
   const int idx = index[0];
   const float ds = sigmas[idx + 1] - sigmas[idx];
   const long long total = (long long)N * HW;
@@ -351,7 +367,7 @@ __global__ void flow_euler_kernel(float* __restrict__ x, const float* __restrict
     const int n = (int)(p / HW), hw = (int)(p % HW);
     for (int c = 0; c < Cx; ++c) {
       const size_t xi = ((size_t)n * Cx + c) * HW + hw;
-      const float nv = x[xi] + ds * vout[p * Kpad + c];
+      const float nv = x[xi] + ds * vout[p * Kpad + c];   // eager order (no FMA): bit-exact
       x[xi] = nv;
       if (next) next[p * Cpad + c] = (bf16r)f2bf(nv);
     }
@@ -368,6 +384,7 @@ __global__ void ddpm_step_kernel(float* __restrict__ x, const float* __restrict_
                                  const float* __restrict__ coef, const int* __restrict__ index,
                                  const float* __restrict__ noise, int N, int Cx, int HW, const float* __restrict__ cond,
                                  int Cc, int Cpad, bf16r* __restrict__ next) {
+#pragma clang fp contract(off)
   const int idx = index[0];
   const float* cf = coef + idx * 7;
   const float sqrt_b = cf[0], sqrt_a = cf[1], cx0 = cf[2], cxt = cf[3], sd = cf[4], clip = cf[5], ceps = cf[6];
@@ -378,9 +395,11 @@ __global__ void ddpm_step_kernel(float* __restrict__ x, const float* __restrict_
       const size_t xi = ((size_t)n * Cx + c) * HW + hw;
       const float e = eps[p * Kpad + c];
       const float xv = x[xi];
+      // every product / sum rounded on its own (no FMA contraction, correctly rounded division): diffusers'
+      // eager operation order, so the step is bit-exact with the fp32 torch expression
       float x0 = (xv - sqrt_b * e) / sqrt_a;
       if (clip > 0.f) x0 = fminf(fmaxf(x0, -clip), clip);
-      float pv = cx0 * x0 + cxt * xv;
+      float pv = cxt != 0.f ? cx0 * x0 + cxt * xv : cx0 * x0;
       if (ceps != 0.f) pv = pv + ceps * e;
       if (noise && sd > 0.f) pv = pv + sd * noise[(size_t)idx * N * Cx * HW + xi];
       x[xi] = pv;
@@ -823,6 +842,13 @@ int fmd_noise_prepare(const float* x0, const float* noise, const float* ca, cons
                       int32_t N, int32_t HW, int32_t Cx, int32_t Cc, int32_t Cpad, void* inp, fmd_stream_t s) {
   LAUNCH(noise_prepare_kernel, grid_for((long long)N * HW * Cpad), x0, noise, ca, cb, cond, N, HW, Cx, Cc, Cpad,
          (bf16r*)inp);
+}
+
+int fmd_add_noise(const float* x0, const float* noise, const float* sqrt_acp, const float* sqrt_1m_acp,
+                  const int64_t* timesteps, int32_t N, int64_t per_sample, float* out, fmd_stream_t s) {
+  if (N <= 0 || per_sample <= 0) return N == 0 ? 0 : -1;
+  LAUNCH(add_noise_kernel, grid_for((long long)N * per_sample), x0, noise, sqrt_acp, sqrt_1m_acp,
+         (const long long*)timesteps, (long long)per_sample, N, out);
 }
 
 int fmd_mse(const float* pred, int32_t Kpad, const float* ta, const float* tb, float tb_sign, int32_t N, int32_t Cx,

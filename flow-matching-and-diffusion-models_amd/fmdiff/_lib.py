@@ -111,6 +111,7 @@ SIGNATURES = {
     "fmd_linear_attention_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, p, p],
     "fmd_linear_attention_bwd": [p, p, p, p, i32, i32, i32, i32, i32, f32, p, p],
     "fmd_noise_prepare": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_add_noise": [p, p, p, p, p, i32, i64, p, p],
     "fmd_mse": [p, i32, p, p, f32, i32, i32, i32, f32, p, i32, p, p, p],
     "fmd_adamw": [p, p, p, p, i64, f32, f32, f32, f32, f32, f32, f32, p],
     "fmd_flow_euler": [p, p, i32, p, p, i32, i32, i32, p, i32, i32, p, p],

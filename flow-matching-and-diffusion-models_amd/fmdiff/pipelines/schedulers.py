@@ -128,6 +128,7 @@ class DDPMScheduler:
         self.timesteps = torch.from_numpy(np.arange(0, N)[::-1].copy())
         self.num_inference_steps = None
         self._dev = {}
+        self._noise_tables = {}
 
     def set_timesteps(self, num_inference_steps: int, device=None):
         N = self.config.num_train_timesteps
@@ -183,16 +184,29 @@ class DDPMScheduler:
         return SchedulerOutput(out) if return_dict else (out,)
 
     def add_noise(self, original_samples, noise, timesteps):
-        """sqrt(a_t) x0 + sqrt(1-a_t) eps (diffusers add_noise; training input of diffusion_lib.py:158)."""
+        """sqrt(a_t) x0 + sqrt(1-a_t) eps (diffusers add_noise; training input of diffusion_lib.py:158), fp32,
+        bit-exact with the eager torch expression (fmd_add_noise).  The sqrt tables are the host's fp32
+        ``alphas_cumprod ** 0.5`` / ``(1 - alphas_cumprod) ** 0.5``, gathered per sample on the device."""
         ops._need_cuda(original_samples, "add_noise")
-        ac = self.alphas_cumprod.to(device=original_samples.device, dtype=torch.float32)
-        sel = ac[timesteps.to(original_samples.device)]
-        ca = (sel ** 0.5).contiguous()
-        cb = ((1 - sel) ** 0.5).contiguous()
-        N, Cx = original_samples.shape[:2]
-        buf = ops.noise_prepare(original_samples.float().contiguous(), noise.float().contiguous(), ca, cb, None,
-                                max(8, -(-Cx // 8) * 8))
-        return ops.nhwc_to_nchw(buf, Cx).to(original_samples.dtype)
+        dev = original_samples.device
+        if dev not in self._noise_tables:
+            ac = self.alphas_cumprod.to(torch.float32)
+            self._noise_tables[dev] = ((ac ** 0.5).to(dev), ((1 - ac) ** 0.5).to(dev))
+        sa, sb = self._noise_tables[dev]
+        x0 = original_samples.float().contiguous()
+        nz = noise.to(device=dev, dtype=torch.float32).contiguous()
+        N = x0.shape[0]
+        ts = torch.as_tensor(timesteps).to(device=dev, dtype=torch.int64).reshape(-1)
+        if ts.numel() == 1 and N > 1:
+            ts = ts.expand(N)
+        ts = ts.contiguous()
+        if ts.numel() != N or nz.shape != x0.shape:
+            raise ValueError("add_noise: one timestep per sample and noise of the samples' shape")
+        out = torch.empty_like(x0)
+        from .. import _lib
+        _lib.call("fmd_add_noise", x0.data_ptr(), nz.data_ptr(), sa.data_ptr(), sb.data_ptr(), ts.data_ptr(), N,
+                  x0[0].numel() if N else 0, out.data_ptr(), ops.stream())
+        return out.to(original_samples.dtype)
 
 
 class DDIMScheduler(DDPMScheduler):

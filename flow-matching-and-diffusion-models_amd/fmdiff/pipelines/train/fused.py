@@ -168,20 +168,34 @@ class FusedTrainStep:
 
     # ---------------------------------------------------------- hipGraph
     def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None,
-                context_ca=None):
+                context_ca=None, noise=None, t=None):
         """Capture one step into a hipGraph.  Single process: the whole step (RNG, forward, loss, backward,
         AdamW).  With several ranks (``split_collectives``, default: world > 1) the graph holds RNG +
         forward + backward, and each replay is followed by the bucketed RCCL all-reduce and the AdamW
-        launch issued eagerly: no collective is ever recorded into a graph."""
+        launch issued eagerly: no collective is ever recorded into a graph.
+
+        ``noise`` / ``t`` (optional): inject the step's random draws (static buffers, refreshed by
+        ``replay(noise=..., t=...)``) instead of drawing them inside the graph.
+
+        The ``warmup_iters`` eager steps that precede the capture (allocator and kernel warm-up) leave no
+        trace: parameters, Adam moments and the step counter are restored afterwards, so the first replay
+        is optimizer step 1 with the schedule's first LR, as in the reference loop
+        (flow_matching_lib.py:148-182)."""
         self._split = self.world > 1 if split_collectives is None else bool(split_collectives)
-        self._static = (clean.clone(), ldct.clone() if ldct is not None else None, None, None,
+        self._static = (clean.clone(), ldct.clone() if ldct is not None else None,
+                        noise.clone() if noise is not None else None, t.clone() if t is not None else None,
                         context_ca.clone() if context_ca is not None else None)
+        snap = (self.flat.data.clone(), self.m.clone(), self.v.clone(), self.step_ctr.clone())
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup_iters):
                 self.step(*self._static)
         torch.cuda.current_stream().wait_stream(s)
+        for dst, src in zip((self.flat.data, self.m, self.v, self.step_ctr), snap):
+            dst.copy_(src)
+        self.flat.grad.zero_()
+        del snap
         g = torch.cuda.CUDAGraph()
         # multi-rank: thread-local capture, so the process group's watchdog thread may keep querying its
         # (already completed) events while this thread records
@@ -199,13 +213,13 @@ class FusedTrainStep:
                 self._bwd_rest()
             self._graph2 = g2
 
-    def replay(self, clean=None, ldct=None, context_ca=None):
-        if clean is not None:
-            self._static[0].copy_(clean)
-        if ldct is not None:
-            self._static[1].copy_(ldct)
-        if context_ca is not None:
-            self._static[4].copy_(context_ca)
+    def replay(self, clean=None, ldct=None, context_ca=None, noise=None, t=None):
+        for i, new in ((0, clean), (1, ldct), (2, noise), (3, t), (4, context_ca)):
+            if new is None:
+                continue
+            if self._static[i] is None:
+                raise ValueError("replay: this input was not a static buffer at capture time")
+            self._static[i].copy_(new)
         self._graph.replay()
         if self._split:
             if self._graph2 is not None:

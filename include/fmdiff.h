@@ -292,6 +292,12 @@ int fmd_linear_attention_bwd(const void* qkv, const void* dout, const float* sta
  * (FM, ca = t); neither: noise (sampler input). */
 int fmd_noise_prepare(const float* x0, const float* noise, const float* ca, const float* cb, const float* cond,
                       int32_t N, int32_t HW, int32_t Cx, int32_t Cc, int32_t Cpad, void* inp, fmd_stream_t s);
+/* diffusers DDPMScheduler.add_noise (diffusion_lib.py:158, diffusion_utils.py:162/222) in fp32:
+ * out[n] = sqrt_acp[t[n]] * x0[n] + sqrt_1m_acp[t[n]] * noise[n] over per_sample elements per sample,
+ * torch's operation order (two rounded products, one rounded add): bit-exact with the eager op.
+ * sqrt_acp / sqrt_1m_acp: [num_train_timesteps] fp32 tables; timesteps: int64 [N] on the device. */
+int fmd_add_noise(const float* x0, const float* noise, const float* sqrt_acp, const float* sqrt_1m_acp,
+                  const int64_t* timesteps, int32_t N, int64_t per_sample, float* out, fmd_stream_t s);
 int fmd_mse(const float* pred, int32_t Kpad, const float* ta, const float* tb, float tb_sign, int32_t N, int32_t Cx,
             int32_t HW, float grad_scale, float* partial, int32_t max_blocks, float* loss, void* dpred,
             fmd_stream_t s);

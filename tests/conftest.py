@@ -40,3 +40,15 @@ def golden():
     tensors = torch.load(os.path.join(d, "golden.pt"), weights_only=True)
     meta = json.load(open(os.path.join(d, "golden.json")))
     return tensors, meta
+
+
+@pytest.fixture(scope="session")
+def golden_b256():
+    """Config B at its bench resolution (256x256, batch 2): tests/golden/make_golden_b256.py."""
+    import json
+
+    import torch
+    d = os.path.join(REPO, "tests", "golden")
+    tensors = torch.load(os.path.join(d, "golden_b256.pt"), weights_only=True)
+    meta = json.load(open(os.path.join(d, "golden_b256.json")))
+    return tensors, meta

@@ -461,6 +461,56 @@ def test_halo_conv_matches_generic(case):
         torch.testing.assert_close(ta, tb, rtol=2e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("case", ["fwd_pro_stats", "dgrad_ep_stats"])
+def test_halo_conv_bench_problem_vs_torch(case):
+    """The bench's roofline kernel on the bench's own problem -- non-split conv3x3_halo at 8x256^2, 128 -> 128
+    channels -- vs an fp32 torch conv of the same op (computed on the GPU, TF32 off):
+
+    * fwd_pro_stats: y = conv3x3(bf16(SiLU(a*x + b))) + bias, with the fused channel statistics;
+    * dgrad_ep_stats: the ResBlock data gradient dz = conv_transpose3x3(dy) * SiLU'(a*x + b) (flipped-tap
+      weights, mode 3) with the GroupNorm-backward sums (sum dz, sum dz*x).
+
+    Tolerance: max |err| <= 1.5e-2 * max|ref| and relative L2 <= 5e-3 (bf16 output rounding + fp32
+    accumulation order); statistics rtol 2e-3."""
+    O = ops()
+    N, H, W, C, K = 8, 256, 256, 128, 128
+    torch.backends.cudnn.allow_tf32 = False
+    g = torch.Generator(device=DEV).manual_seed(61)
+    x = torch.randn(N, H, W, C, device=DEV, generator=g).to(torch.bfloat16)
+    w = torch.randn(K, C, 3, 3, device=DEV, generator=g) / math.sqrt(C * 9)
+    a = torch.rand(N, C, device=DEV, generator=g) + 0.5
+    b = torch.randn(N, C, device=DEV, generator=g) * 0.2
+    wb = w.to(torch.bfloat16).float()
+    assert O.halo_eligible(N, H, H, W, K, Cin=C, pro=True) and O.halo_splits(N, H, W, K, C) == 1
+    if case == "fwd_pro_stats":
+        bias = torch.randn(K, device=DEV, generator=g) * 0.1
+        wt = O.tile_weights(O.prep_weights(w, 0))
+        out, st = O.conv(x, K, None, pro=(a, b, True), bias=bias, want_stats=True, wgt_tiled=wt)
+        z = F.silu(x.float() * a[:, None, None, :] + b[:, None, None, :]).to(torch.bfloat16).float()
+        ref = F.conv2d(z.permute(0, 3, 1, 2), wb, bias, padding=1).permute(0, 2, 3, 1)
+        xs = None
+    else:
+        dy = torch.randn(N, H, W, K, device=DEV, generator=g).to(torch.bfloat16)
+        wt = O.tile_weights(O.prep_weights(w, 3))
+        out, st = O.conv(dy, C, None, ks=3, pad=1, out_hw_=(H, W), wgt_tiled=wt, ep=(x, None, a, b),
+                         want_stats=True)
+        dx = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), wb, padding=1).permute(0, 2, 3, 1)
+        zz = x.float() * a[:, None, None, :] + b[:, None, None, :]
+        s = torch.sigmoid(zz)
+        ref = dx * (s * (1 + zz * (1 - s)))
+        xs = x.float()
+    got = out.float()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    print(f"{case}: max err {err:.3e} (scale {scale:.3e}), rel L2 {rel:.3e}")
+    assert err <= 1.5e-2 * scale and rel <= 5e-3
+    sums = st.slab.view(N, -1, out.shape[-1], 2).sum(1)
+    torch.testing.assert_close(sums[..., 0], got.sum((1, 2)), rtol=2e-3, atol=2e-1)
+    torch.testing.assert_close(sums[..., 1], (got * (xs if xs is not None else got)).sum((1, 2)), rtol=2e-3,
+                               atol=2e-1)
+
+
 @pytest.mark.parametrize("in_silu", [False, True])
 def test_grouped_linear_vs_torch(in_silu):
     """fmd_grouped_linear(_bwd): several emb projections (O = 256, 1024, 128) in one launch each way."""

@@ -92,6 +92,150 @@ def test_train_step_gradients_vs_oracle(golden):
     assert worst[0] > 0.99, worst
 
 
+def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), tol_sum=5e-2, tol_sq=5e-2,
+                          flip_frac=0.05, negligible=1e-5, dead_bound=1e-3):
+    """Loss, per-parameter gradient sums / sums of squares, full small gradients and post-AdamW parameter
+    sums of a finished FusedTrainStep vs a reference-generated fixture.
+
+    Tensors whose reference gradient norm is below ``negligible`` x the whole-model gradient norm are
+    mathematically ~0 (e.g. the bias of a conv feeding a GroupNorm with one channel per group): their
+    reference values are fp32 round-off, so they are only required to stay below ``dead_bound`` x the
+    whole-model norm on the GPU (bf16 round-off of an exact cancellation).
+    Gradient sums are compared relative to sqrt(numel) * ||g_ref|| (the Cauchy-Schwarz bound of a sum of
+    differences), so a tensor whose sum cancels to ~0 is not held to a relative bar it cannot meet.  The
+    first AdamW step moves every element by ~lr * sign(g): the per-tensor change of the parameter sum may
+    differ from the reference's by at most ``flip_frac`` of the elements flipping sign (2 lr each)."""
+    names = m["param_names"]
+    params = dict(model.named_parameters())
+    numel = {k: params[k].numel() for k in names}
+    ref_loss = T[f"{prefix}/loss"].item()
+    print(f"loss hip {float(loss):.6f} ref {ref_loss:.6f}")
+    assert abs(float(loss) - ref_loss) <= 5e-3 * abs(ref_loss)
+    total = math.sqrt(T[f"{prefix}/grad_sq"].sum().item())
+    live = set()
+    worst_sum = worst_sq = worst_dead = 0.0
+    for i, k in enumerate(names):
+        g = params[k].grad.double().cpu()
+        rs, rq = T[f"{prefix}/grad_sum"][i].item(), T[f"{prefix}/grad_sq"][i].item()
+        gn = math.sqrt(g.pow(2).sum().item())
+        if math.sqrt(rq) < negligible * total:
+            worst_dead = max(worst_dead, gn / total)
+            continue
+        live.add(k)
+        worst_sum = max(worst_sum, abs(g.sum().item() - rs) / math.sqrt(numel[k] * rq))
+        worst_sq = max(worst_sq, abs(gn - math.sqrt(rq)) / math.sqrt(rq))
+    print(f"grad sums over {len(live)} tensors: worst |d sum| / (sqrt(n) ||g||) {worst_sum:.3e}, worst relative "
+          f"norm error {worst_sq:.3e}; {len(names) - len(live)} ~0-gradient tensors, worst norm {worst_dead:.2e} x total")
+    assert worst_sum < tol_sum and worst_sq < tol_sq and worst_dead < dead_bound
+    worst_cos = 1.0
+    for k in small:
+        if k not in live:
+            continue
+        g = params[k].grad.double().cpu().flatten()
+        r = T[f"{prefix}/grad/{k}"].double().flatten()
+        worst_cos = min(worst_cos, ((g @ r) / (g.norm() * r.norm() + 1e-30)).item())
+    if small:
+        print(f"small-tensor gradients: worst cosine {worst_cos:.5f} over {len(small)} tensors")
+        assert worst_cos > 0.99
+    before = T[f"{prefix}/param_sum_before"]
+    worst_flip = 0.0
+    for i, k in enumerate(names):
+        if k not in live:   # lr * sign(round-off) on both sides
+            continue
+        after = params[k].detach().double().sum().item()
+        b = before[i].item()
+        d_gpu, d_ref = after - b, T[f"{prefix}/param_sum_after"][i].item() - b
+        worst_flip = max(worst_flip, abs(d_gpu - d_ref) / (2 * lr_eff * numel[k]))
+    print(f"post-AdamW parameter sums: worst sign-flip-equivalent fraction {worst_flip:.4f}")
+    assert worst_flip < flip_frac
+
+
+def test_b256_forward_vs_reference_golden(golden_b256):
+    """The benched configuration itself: config B's EfficientUNetND at 256x256 (batch 2) vs the reference
+    module's forward (tests/golden/make_golden_b256.py).  At this size the 256^2 level has 2*16*16 = 512
+    16x16 tiles, so the non-split halo kernel (the bench's roofline kernel) carries the top level."""
+    T, m = golden_b256
+    model = _build(m).to(DEV)
+    _load_seeded(model, m)
+    with torch.no_grad():
+        y = model(T["fwd/x"].to(DEV), T["fwd/t"].to(DEV), context=T["fwd/cond"].to(DEV))
+    err = _rel(y, T["fwd/y"])
+    print(f"config B 256^2 forward rel L2 {err:.3e}")
+    assert err < 2e-2
+
+
+def test_b256_fused_train_step_vs_reference_golden(golden_b256):
+    """FusedTrainStep itself -- graph-captured, concatenate conditioning, injected eps / t -- on config B
+    at 256x256: one replay = noise_prepare -> UNet fwd -> fmd_mse -> UNet bwd -> fmd_adamw_sched (lr 1e-4,
+    cosine schedule, warmup 0) vs the reference's loss, gradients and post-AdamW parameters
+    (flow_matching_lib.py:150-182)."""
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    T, m = golden_b256
+    model = _build(m).to(DEV)
+    _load_seeded(model, m)
+    tr = FusedTrainStep(model, lr=m["lr"], warmup=m["warmup"], total_steps=m["total"],
+                        num_train_timesteps=m["num_train_timesteps"], weight_decay=m["weight_decay"])
+    clean, ldct, noise, t = (T[f"step/{k}"].to(DEV) for k in ("clean", "ldct", "noise", "t"))
+    tr.capture(clean, ldct, warmup_iters=2, noise=noise, t=t)
+    assert int(tr.step_ctr.item()) == 0
+    loss = tr.replay()
+    torch.cuda.synchronize()
+    assert int(tr.step_ctr.item()) == 1
+    _check_step_vs_golden(model, T, m, "step", loss.item(), m["lr"], small=m["small_grads"])
+
+
+def test_fused_train_step_tiny_post_adamw_vs_golden(golden):
+    """The tiny LDCT config's reference train step (fm_step, torch AdamW lr 1e-3): FusedTrainStep's eager
+    step gives the same loss, gradient sums and post-AdamW parameter sums."""
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    from oracle import unet as U
+    T, M = golden
+    m = dict(M["fm_step"])
+    model = _build(m).to(DEV)
+    spec, sd = _load_seeded(model, m)
+    T = dict(T)
+    T["fm_step/param_sum_before"] = torch.stack([sd[k].double().sum() for k in m["param_names"]])
+    tr = FusedTrainStep(model, lr=m["lr"], warmup=0, total_steps=10 ** 6, num_train_timesteps=m["num_train_timesteps"])
+    clean, ldct, noise, t = (T[f"fm_step/{k}"].to(DEV) for k in ("clean", "ldct", "noise", "t"))
+    loss = tr.step(clean, ldct, noise=noise, t=t)
+    torch.cuda.synchronize()
+    _check_step_vs_golden(model, T, m, "fm_step", loss.item(), m["lr"])
+
+
+def test_capture_leaves_optimizer_state_untouched(golden):
+    """capture()'s eager warm-up steps are undone: parameters, Adam moments and the step counter are the
+    pre-capture ones, and the first replay equals one eager step from the same state."""
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    T, M = golden
+    meta = M["ldct_fm_test"]
+    x, cond = T["ldct_fm_test/x"].to(DEV), T["ldct_fm_test/cond"].to(DEV)
+    clean = x.clamp(0, 1)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    noise = torch.randn(clean.shape, device=DEV, generator=g)
+    t = torch.rand(clean.shape[0], device=DEV, generator=g)
+    out = []
+    for use_graph in (True, False):
+        model = _build(meta).to(DEV)
+        _load_seeded(model, meta)
+        p0 = {k: p.detach().clone() for k, p in model.named_parameters()}
+        tr = FusedTrainStep(model, lr=1e-3, warmup=0, total_steps=100)
+        if use_graph:
+            tr.capture(clean, cond, warmup_iters=3, noise=noise, t=t)
+            torch.cuda.synchronize()
+            for k, p in model.named_parameters():
+                assert torch.equal(p.detach(), p0[k]), k
+            assert int(tr.step_ctr.item()) == 0
+            assert not tr.m.any() and not tr.v.any() and not tr.flat.grad.any()
+            loss = tr.replay()
+        else:
+            loss = tr.step(clean, cond, noise=noise, t=t)
+        torch.cuda.synchronize()
+        out.append((loss.item(), {k: p.detach().clone() for k, p in model.named_parameters()}))
+    assert out[0][0] == out[1][0]
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k], out[1][1][k]), k
+
+
 def test_fused_sampler_matches_plain_euler_loop(golden):
     """FusedFlowSampler (hipGraph-replayed step, per-schedule time-embedding table selected by the device
     step counter) == the plain FlowMatchEuler loop x += (sigma[i+1] - sigma[i]) * model(x | cond, t_i)

@@ -55,6 +55,38 @@ def test_fm_train_step(golden):
     torch.testing.assert_close(ps, T["fm_step/param_sum_after"], rtol=1e-7, atol=1e-7)
 
 
+def test_b256_forward_bit_exact(golden_b256):
+    """The benched configuration (config B, 256x256): the oracle reproduces the reference forward exactly."""
+    T, m = golden_b256
+    spec = _spec(m)
+    sd = U.seeded_state_dict(spec, m["seed"])
+    with torch.no_grad():
+        y = U.unet_forward(sd, spec, T["fwd/x"], T["fwd/t"], context=T["fwd/cond"])
+    assert torch.equal(y, T["fwd/y"]), (y - T["fwd/y"]).abs().max()
+
+
+def test_b256_fm_train_step(golden_b256):
+    """Config B at 256x256: oracle FM train step (loss, gradients) and AdamW + cosine LR vs the reference's."""
+    T, m = golden_b256
+    spec = _spec(m)
+    sd = _params(spec, m["seed"])
+    loss, scaled = OT.fm_loss(sd, spec, T["step/clean"], T["step/ldct"], T["step/noise"], T["step/t"],
+                              m["num_train_timesteps"])
+    scaled.backward()
+    assert torch.equal(loss.detach(), T["step/loss"])
+    names = m["param_names"]
+    torch.testing.assert_close(torch.stack([sd[k].grad.double().sum() for k in names]), T["step/grad_sum"],
+                               rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(torch.stack([sd[k].grad.double().pow(2).sum() for k in names]), T["step/grad_sq"],
+                               rtol=1e-9, atol=1e-12)
+    for k in m["small_grads"]:
+        assert torch.equal(sd[k].grad, T[f"step/grad/{k}"]), k
+    lr = m["lr"] * OS.cosine_with_warmup(0, m["warmup"], m["total"])
+    OT.adamw_step(sd, lr, 1, {}, weight_decay=m["weight_decay"])
+    ps = torch.stack([sd[k].detach().double().sum() for k in names])
+    torch.testing.assert_close(ps, T["step/param_sum_after"], rtol=1e-7, atol=1e-6)
+
+
 def test_self_attention_raw_reshape(golden):
     T, M = golden
     m = M["attn"]
