@@ -19,6 +19,7 @@ buckets.
 """
 from __future__ import annotations
 
+import math
 from typing import Optional
 
 import torch
@@ -43,6 +44,7 @@ class FlatParams:
         self.data = torch.empty(total, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
         self.slices = []
+        self.offsets = {}           # id(param) -> (offset, numel) in the flat buffers
         off = 0
         with torch.no_grad():
             for p in params:
@@ -51,6 +53,7 @@ class FlatParams:
                 p.data = self.data[off:off + n].view_as(p)
                 p.grad = self.grad[off:off + n].view_as(p)
                 self.slices.append((off, n))
+                self.offsets[id(p)] = (off, n)
                 off += n
         self.numel = total
 
@@ -72,6 +75,9 @@ class FusedTrainStep:
         self.v = torch.zeros_like(self.flat.data)
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        # sum over chunks of loss * chunk size (flow_matching_lib.py:174), kept on the device so the step never
+        # synchronises with the host; read once per epoch (epoch_loss_sum)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
         self.partial = torch.empty(4096, dtype=torch.float32, device=dev)
         self.objective = objective
         self.hp = dict(lr=lr, wd=weight_decay, warmup=warmup, total=total_steps, betas=betas, eps=eps)
@@ -106,6 +112,7 @@ class FusedTrainStep:
             ta, tb, sign = noise, None, 0.0                                        # target eps
         dpred = torch.empty(out.shape, device=out.device, dtype=torch.bfloat16)
         ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
+        self.loss_sum.add_(self.loss, alpha=float(N))
         if self.overlap:
             self.eng.backward(ctx, dpred, part=1)   # part 2 in _bwd_rest, after the decoder all-reduce starts
             self._ctx = ctx
@@ -166,6 +173,70 @@ class FusedTrainStep:
             loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt, cc)
         return loss
 
+    # ------------------------------------------------- bookkeeping / state
+    def epoch_loss_sum(self, reset: bool = True) -> torch.Tensor:
+        """Device fp64 sum of (chunk loss x chunk size) since the last reset (the reference's ``epoch_loss``)."""
+        out = self.loss_sum.clone()
+        if reset:
+            self.loss_sum.zero_()
+        return out
+
+    def lr_multiplier(self, s: int) -> float:
+        """get_cosine_schedule_with_warmup's multiplier after ``s`` scheduler steps (same formula as
+        fmd_adamw_sched)."""
+        w, total = self.hp["warmup"], self.hp["total"]
+        if s < w:
+            return float(s) / float(max(1, w))
+        prog = float(s - w) / float(max(1, total - w))
+        return max(0.0, 0.5 * (1.0 + math.cos(math.pi * 2.0 * 0.5 * prog)))
+
+    def steps_done(self) -> int:
+        return int(self.step_ctr.item())
+
+    def optimizer_state_dict(self) -> dict:
+        """The step's AdamW state in ``torch.optim.AdamW.state_dict()`` form (state keyed by the index in
+        ``model.parameters()``), so a checkpoint written here resumes the reference's optimizer and back."""
+        s = self.steps_done()
+        b1, b2 = self.hp["betas"]
+        state = {}
+        params = list(self.model.parameters())
+        if s > 0:
+            for i, p in enumerate(params):
+                off, n = self.flat.offsets[id(p)]
+                state[i] = {"step": torch.tensor(float(s)), "exp_avg": self.m[off:off + n].view_as(p).detach().cpu().clone(),
+                            "exp_avg_sq": self.v[off:off + n].view_as(p).detach().cpu().clone()}
+        group = {"lr": self.hp["lr"] * self.lr_multiplier(s), "betas": (b1, b2), "eps": self.hp["eps"],
+                 "weight_decay": self.hp["wd"], "amsgrad": False, "maximize": False, "foreach": None,
+                 "capturable": False, "differentiable": False, "fused": None, "decoupled_weight_decay": True,
+                 "initial_lr": self.hp["lr"], "params": list(range(len(params)))}
+        return {"state": state, "param_groups": [group]}
+
+    def lr_scheduler_state_dict(self) -> dict:
+        """``LambdaLR`` state of get_cosine_schedule_with_warmup after the steps taken."""
+        s = self.steps_done()
+        return {"base_lrs": [self.hp["lr"]], "last_epoch": s, "_step_count": s + 1, "_is_initial": False,
+                "_get_lr_called_within_step": False, "_last_lr": [self.hp["lr"] * self.lr_multiplier(s)],
+                "lr_lambdas": [{}]}
+
+    def load_optimizer_state_dict(self, opt_state: dict, sched_state: Optional[dict] = None) -> None:
+        """Inverse of optimizer_state_dict (also accepts a torch AdamW checkpoint of the reference).  The step
+        count comes from the optimizer state (else the LR scheduler's ``last_epoch``)."""
+        params = list(self.model.parameters())
+        st = opt_state.get("state", {}) if opt_state else {}
+        steps = 0
+        with torch.no_grad():
+            for i, p in enumerate(params):
+                e = st.get(i) if i in st else st.get(str(i))
+                if not e:
+                    continue
+                off, n = self.flat.offsets[id(p)]
+                self.m[off:off + n].copy_(torch.as_tensor(e["exp_avg"]).reshape(-1))
+                self.v[off:off + n].copy_(torch.as_tensor(e["exp_avg_sq"]).reshape(-1))
+                steps = max(steps, int(float(torch.as_tensor(e["step"]))))
+        if steps == 0 and sched_state:
+            steps = int(sched_state.get("last_epoch", 0))
+        self.step_ctr.fill_(steps)
+
     # ---------------------------------------------------------- hipGraph
     def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None,
                 context_ca=None, noise=None, t=None):
@@ -185,14 +256,14 @@ class FusedTrainStep:
         self._static = (clean.clone(), ldct.clone() if ldct is not None else None,
                         noise.clone() if noise is not None else None, t.clone() if t is not None else None,
                         context_ca.clone() if context_ca is not None else None)
-        snap = (self.flat.data.clone(), self.m.clone(), self.v.clone(), self.step_ctr.clone())
+        snap = (self.flat.data.clone(), self.m.clone(), self.v.clone(), self.step_ctr.clone(), self.loss_sum.clone())
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup_iters):
                 self.step(*self._static)
         torch.cuda.current_stream().wait_stream(s)
-        for dst, src in zip((self.flat.data, self.m, self.v, self.step_ctr), snap):
+        for dst, src in zip((self.flat.data, self.m, self.v, self.step_ctr, self.loss_sum), snap):
             dst.copy_(src)
         self.flat.grad.zero_()
         del snap

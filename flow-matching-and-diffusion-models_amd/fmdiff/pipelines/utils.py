@@ -138,6 +138,15 @@ def normalize_latent_conditioning(condition, mode):
     raise ValueError(f"Unknown latent_norm mode: {mode}")
 
 
+def _prepare_attention_context(condition):
+    """Cross-attention context as the UNet takes it: (B, C, T) tokens or (B, C, *spatial) maps pass through."""
+    if condition is None:
+        return None
+    if condition.dim() >= 3:
+        return condition
+    raise ValueError(f"Unsupported conditioning shape for attention: {tuple(condition.shape)}")
+
+
 def select_timesteps(timesteps: torch.Tensor, start_step=None, last_n_steps=None) -> torch.Tensor:
     """Tail selection of ``sample_with_scheduler`` (reference ``pipelines/utils.py:182-192``)."""
     if start_step is not None:

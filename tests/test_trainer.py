@@ -1,0 +1,236 @@
+"""Trainer bookkeeping on the CPU (no GPU): the real ``run_training`` loop with a stand-in step.
+
+The step object is injected (``step_factory``), the way the reference's own tests swap in fakes
+(``tests/test_run_model_dispatch.py`` ``_DummyHandler``): everything else -- config parsing and fallbacks,
+``setup_distributed`` over gloo, ``DistributedSampler`` sharding + ``set_epoch``, the LR horizon
+``epochs * ceil(len(ds) / bs)``, the epoch-end loss / count all-reduces, rank-0 checkpoints and
+metrics, ``_runN`` directories and resume -- is the product code (reference
+``flow_matching_lib.py:33-248``).
+"""
+import json
+import math
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+UNET = {"sample_size": 8, "in_channels": 1, "out_channels": 1, "layers_per_block": 1, "block_out_channels": [32, 64],
+        "attention_resolutions": []}
+
+
+class FakeStep:
+    """Records what the loop hands it; loss of a batch = mean of its targets (sample i has value i)."""
+
+    def __init__(self, model, **kw):
+        self.kw = kw
+        self.seen = []
+        self.loss_sum = torch.zeros(1, dtype=torch.float64)
+        self.steps = 0
+        self.loaded = None
+
+    def step(self, clean, ldct, noise=None, t=None, context_ca=None):
+        assert ldct is not None and torch.equal(ldct, clean)   # concatenate: image falls back to target
+        ids = clean.flatten(1)[:, 0].round().long().tolist()
+        self.seen.append(ids)
+        loss = clean.mean().double()
+        self.loss_sum += loss * clean.shape[0]
+        self.steps += 1
+        return loss
+
+    def epoch_loss_sum(self, reset=True):
+        out = self.loss_sum.clone()
+        if reset:
+            self.loss_sum.zero_()
+        return out
+
+    def optimizer_state_dict(self):
+        return {"state": {}, "param_groups": [{"lr": self.kw["lr"], "params": [], "steps": self.steps}]}
+
+    def lr_scheduler_state_dict(self):
+        return {"last_epoch": self.steps}
+
+    def load_optimizer_state_dict(self, opt, sched=None):
+        self.loaded = (opt, sched)
+        self.steps = sched["last_epoch"]
+
+
+def _dataset(n, hw=8):
+    from fmdiff.data import TensorPairDataset
+    tgt = torch.arange(n, dtype=torch.float32).view(n, 1, 1, 1).expand(n, 1, hw, hw).contiguous()
+    return TensorPairDataset(tgt)
+
+
+def _config(tmp, epochs, bs=2, **extra):
+    cfg = {"training": {"batch_size": bs, "num_epochs": epochs, "learning_rate": 1e-4, "lr_warmup_steps": 3,
+                        "conditioning": "concatenate", "channels": 1, "num_workers": 0, "seed": 1,
+                        "save_images": False, "save_model_epochs": 1, "output_dir": os.path.join(tmp, "runs", "fm"),
+                        "dist_backend": "gloo", **extra},
+           "model": {"unet": UNET, "scheduler": {"name": "flow_match_euler", "num_train_timesteps": 1000},
+                     "model_type": "flow_matching"}}
+    path = os.path.join(tmp, "cfg.json")
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    return path
+
+
+def _worker(rank, world, tmp, n, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "flow-matching-and-diffusion-models_amd")]
+    from fmdiff.pipelines.train.flow_matching_lib import train
+    made = []
+
+    def factory(model, **kw):
+        made.append(FakeStep(model, **kw))
+        return made[-1]
+
+    out = None
+    try:
+        from fmdiff.pipelines.train import loop
+        out = loop.run_training(_dataset(n), _config(tmp, 2), objective="flow_matching", step_factory=factory)
+        st = made[0]
+        q.put((rank, str(out), st.kw["total_steps"], st.kw["process_group"] is not None, st.seen))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_trainer_sharding_lr_horizon_and_epoch_reduce_world2(tmp_path):
+    """gloo world 2, 11 samples, batch 2, 2 epochs: each rank gets its DistributedSampler shard (6 samples,
+    one padded), shards differ per epoch (set_epoch), the LR horizon is 2 * ceil(11 / 2) = 12 on both ranks,
+    metrics.csv holds the global mean from the epoch-end all-reduces, rank 0 alone writes checkpoints into
+    the one run directory both ranks agree on."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    n, world = 11, 2
+    port = 29500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_worker, args=(r, world, str(tmp_path), n, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs = {r[1] for r in res}
+    assert len(outs) == 1, outs                       # one run directory
+    out = outs.pop()
+    assert out.endswith("fm_run1")
+    assert all(r[2] == 2 * math.ceil(n / 2) for r in res)   # LR horizon: global length
+    assert all(r[3] for r in res)                     # the step got the process group (gradient all-reduce)
+    per_epoch = []
+    for e in range(2):
+        ids = []
+        for r in res:
+            batches = r[4][3 * e:3 * e + 3]           # 6 samples per rank per epoch = 3 batches
+            assert sum(len(b) for b in batches) == 6
+            ids += [i for b in batches for i in b]
+        assert sorted(set(ids)) == list(range(n))     # the two shards cover the dataset (one padded repeat)
+        per_epoch.append(ids)
+    assert per_epoch[0] != per_epoch[1]               # set_epoch reshuffles
+    rows = open(os.path.join(out, "metrics.csv")).read().strip().splitlines()
+    assert rows[0] == "epoch,train_loss" and len(rows) == 3
+    for e in range(2):
+        ids = per_epoch[e]
+        assert abs(float(rows[1 + e].split(",")[1]) - sum(ids) / len(ids)) < 1e-5
+    for f in ("flow_last.pt", "flow_best.pt", "epochs/epoch0001/epoch.pt", "epochs/epoch0002/epoch.pt",
+              "train_config.json"):
+        assert os.path.exists(os.path.join(out, f)), f
+    ck = torch.load(os.path.join(out, "flow_last.pt"), weights_only=True)
+    assert ck["epoch"] == 2 and set(ck) == {"model", "optimizer", "lr_scheduler", "scaler", "epoch", "best_metric"}
+
+
+def test_trainer_resume_and_batch_size_fallbacks(tmp_path):
+    """Single process: ``train_batch_size`` wins over ``batch_size``; a resumed run starts at saved epoch + 1,
+    hands the saved optimizer / LR-scheduler state to the step, appends to the same run's metrics."""
+    from fmdiff.pipelines.train import loop
+    made = []
+
+    def factory(model, **kw):
+        made.append(FakeStep(model, **kw))
+        return made[-1]
+
+    cfg = _config(str(tmp_path), 1, bs=2, train_batch_size=3)
+    out = loop.run_training(_dataset(7), cfg, objective="flow_matching", step_factory=factory)
+    assert made[0].kw["total_steps"] == math.ceil(7 / 3)
+    assert [len(b) for b in made[0].seen] == [3, 3, 1]
+    with open(cfg) as f:
+        c = json.load(f)
+    c["training"]["num_epochs"] = 2
+    c["training"]["output_dir"] = str(out)
+    with open(cfg, "w") as f:
+        json.dump(c, f)
+    loop.run_training(_dataset(7), cfg, resume=os.path.join(out, "flow_last.pt"), objective="flow_matching",
+                      step_factory=factory)
+    st = made[1]
+    assert st.loaded is not None and st.loaded[1]["last_epoch"] == 3
+    assert len(st.seen) == 3                       # only epoch 2 ran
+    rows = open(os.path.join(out, "metrics.csv")).read().strip().splitlines()
+    assert [r.split(",")[0] for r in rows[1:]] == ["1", "2"]
+
+
+def test_trainer_rejects_wrong_model_type(tmp_path):
+    from fmdiff.pipelines.train import diffusion_lib
+    with pytest.raises(ValueError, match="Expected model_type 'diffusion'"):
+        diffusion_lib.train(_dataset(4), _config(str(tmp_path), 1), step_factory=FakeStep)
+
+
+def test_legacy_diffusers_key_remap_roundtrip():
+    """build_diffusion_model's legacy path (diffusion_utils.py:15-90): a diffusers-named state dict of a
+    UNetDiffusersND (time_emb_proj / conv_shortcut / query-key-value / unwrapped conv names) loads into the
+    fmdiff model and reproduces its parameters; a shape mismatch is an error."""
+    from fmdiff.utils.model_utils.diffusion_utils import _LEGACY_RENAMES, _load_legacy_unet_state
+    from fmdiff.models.generators import DiffusionUNetFactory
+    cfg = {"unet_impl": "diffusers_nd", "in_channels": 1, "out_channels": 1, "layers_per_block": 1,
+           "block_out_channels": [32, 64], "down_block_types": ["DownBlock2D", "AttnDownBlock2D"],
+           "up_block_types": ["AttnUpBlock2D", "UpBlock2D"], "norm_num_groups": 8}
+    src = DiffusionUNetFactory().build(cfg, "concatenate", 1)
+    g = torch.Generator().manual_seed(0)
+    ref = {k: torch.randn(v.shape, generator=g) for k, v in src.state_dict().items()}
+
+    def to_legacy(k):
+        for old, new in reversed(_LEGACY_RENAMES):
+            if new in k and not (new == ".to_out.0." and ".to_out.0." not in k):
+                k = k.replace(new, old)
+        return k
+    legacy = {to_legacy(k): v for k, v in ref.items()}
+    assert any(".time_emb_proj." in k for k in legacy) and any(".query." in k for k in legacy)
+    dst = DiffusionUNetFactory().build(cfg, "concatenate", 1)
+    _load_legacy_unet_state(dst, legacy)
+    for k, v in dst.state_dict().items():
+        assert torch.equal(v, ref[k]), k
+    bad = dict(legacy)
+    k0 = next(k for k in bad if k.endswith(".time_emb_proj.weight"))
+    bad[k0] = torch.zeros(3, 3)
+    with pytest.raises(RuntimeError, match="shape mismatches"):
+        _load_legacy_unet_state(DiffusionUNetFactory().build(cfg, "concatenate", 1), bad)
+
+
+def test_tensor_cache_paths_and_dataset(tmp_path):
+    """cache_path_for_entry (dataset_utils.py:398-449) and LDCTCacheDataset over a split file + cache."""
+    from fmdiff.data import LDCTCacheDataset, cache_path_for_entry, save_tensor_cache
+    root = tmp_path
+    assert cache_path_for_entry(root, root / "cache", "case1/sdct/img_001.dcm") == root / "cache/case1/sdct/img_001.pt"
+    assert cache_path_for_entry(root, root / "cache", str(root / "a/b.npy"), 2, 4) == root / "cache/a/b_split_2.pt"
+    assert cache_path_for_entry(root, root / "cache", ["x/y.dcm", "x/z.dcm"]) == root / "cache/x/y.pt"
+    assert cache_path_for_entry(root, root / "cache", {"paths": ["p/q.dcm"]}) == root / "cache/p/q.pt"
+    assert cache_path_for_entry(root, None, "a.dcm") is None
+    rows = []
+    for i in range(3):
+        s, l_ = f"c{i}/sdct/{i}.dcm", f"c{i}/ldct/{i}.dcm"
+        save_tensor_cache(torch.full((1, 4, 4), float(i)), cache_path_for_entry(root, root / "cache", s))
+        save_tensor_cache(torch.full((1, 4, 4), 10.0 + i), cache_path_for_entry(root, root / "cache", l_))
+        rows.append(f"c{i}\t{s}\t{l_}")
+    (root / "train.txt").write_text("\n".join(rows) + "\n")
+    ds = LDCTCacheDataset(str(root), train=True, load_ldct=True)
+    assert len(ds) == 3
+    it = ds[2]
+    assert it["target"].shape == (1, 4, 4) and it["target"][0, 0, 0] == 2.0 and it["image"][0, 0, 0] == 12.0
+    assert it["img_id"] == "c2"
+    assert torch.equal(LDCTCacheDataset(str(root), load_ldct=False)[1]["image"], torch.full((1, 4, 4), 1.0))
+    (root / "test.txt").write_text("c9\tc9/sdct/9.dcm\tc9/ldct/9.dcm\n")
+    with pytest.raises(FileNotFoundError, match="tensor cache entry missing"):
+        LDCTCacheDataset(str(root), train=False)[0]
