@@ -110,6 +110,12 @@ int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_st
 /* Halo conv workgroup size: 512 (8 waves x 64 pixels each, default) or 256 (4 waves x 128 pixels,
  * 256 VGPRs per wave).  Returns -1 for other values.  Also settable with FMD_HALO_NT at load time. */
 int fmd_halo_set_workgroup(int32_t nt);
+/* 2-D halo conv main loop: 1 (default) = v_mfma_f32_16x16x32_bf16 (v1) everywhere; 2 = v2
+ * (v_mfma_f32_32x32x16_bf16) for GroupNorm-prologue problems, v1 otherwise; 3 = v2 everywhere (testing). */
+int fmd_halo_set_variant(int32_t v);
+/* v2 dispatch: wgs = workgroups resident in the first round (2 per CU), stagger = s_sleep(127) rounds by
+ * which the second first-round workgroup of each CU starts late (0 = off).  Also FMD_HALO_STAGGER at load. */
+int fmd_halo_set_persist(int32_t wgs, int32_t stagger);
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--hw", type=int, default=256)
     ap.add_argument("--c", type=int, default=128)
     ap.add_argument("--dbg", default="", help="comma list of halo ablation flag values to time as well")
+    ap.add_argument("--variants", default="2", help="comma list of halo kernel variants to time (1, 2)")
+    ap.add_argument("--staggers", default="", help="comma list of v2 stagger values to time (default: library's)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N, H, W, C, K = 8, a.hw, a.hw, a.c, a.c
@@ -82,8 +84,13 @@ def main():
     from fmdiff import _lib
     L = _lib.lib()
     flagsets = [0] + [int(f) for f in a.dbg.split(",") if f]
-    todo = [(name, fl) for name in probs for fl in flagsets]
-    for name, fl in todo:
+    stg = [int(x) for x in a.staggers.split(",") if x] or [None]
+    todo = [(name, fl, v, sg) for name in probs for fl in flagsets for v in [int(x) for x in a.variants.split(",")]
+            for sg in stg]
+    for name, fl, var, sg in todo:
+        L.fmd_halo_set_variant(ctypes.c_int(var))
+        if sg is not None:
+            L.fmd_halo_set_persist(512, sg)
         fn, flops = probs[name]
         if a.only and name not in a.only.split(","):
             continue
@@ -98,7 +105,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
-        print(f"{name:6s} dbg={fl:2d} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        print(f"{name:6s} v{var} stagger={sg} dbg={fl:2d} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s",
+              flush=True)
     L.fmd_debug_halo_flags(ctypes.c_int(0))
 
 
