@@ -104,6 +104,11 @@ SIGNATURES = {
     "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
     "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_conv_combine": [C.POINTER(ConvDesc), p],
+    "fmd_attn_head_pad": [i32],
+    "fmd_attn_pack": [p, p, i32, i32, i32, i32, i32, i32, i32, i32, i32, p, p, p, p],
+    "fmd_attn_unpack": [p, p, p, i32, i32, i32, i32, i32, i32, i32, i32, i32, p, p, p],
+    "fmd_attn_mfma_fwd": [p, p, p, i32, i32, i32, i32, p, p, p],
+    "fmd_attn_mfma_bwd": [p, p, p, p, p, p, p, i32, i32, i32, i32, p, p, p, p],
     "fmd_cross_attention_fwd": [p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p, p],
     "fmd_cross_attention_bwd": [p, p, p, p, p, p, i32, i32, i32, i32, i32, i32, i32, f32, p, p, p],
     "fmd_context_norm_fwd": [p, i32, i32, i32, i32, i32, f32, p, p, i32, p, p, p],

@@ -7,6 +7,7 @@ captured into a hipGraph.  Activations are NHWC bf16 ``[N, H, W, C]``.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -551,8 +552,56 @@ def silu_bwd(x, dy):
     return dx
 
 
+# softmax attention: MFMA kernels over canonical [B*heads][rows][head_pad] planes (csrc/attention_mfma.hip);
+# FMD_ATTN=valu selects the older VALU kernels of csrc/attention.hip (A/B measurements only)
+_ATTN_VALU = os.environ.get("FMD_ATTN", "") == "valu"
+
+
+def _attn_planes(B, heads, rows, dh, dev):
+    D = int(_lib.lib().fmd_attn_head_pad(dh))
+    if D < 0:
+        raise ValueError(f"attention head dim {dh} > 64 is not supported")
+    return torch.empty((B * heads, rows, D), device=dev, dtype=BF16)
+
+
+def _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, which0, which1, cq, ck=None, cv=None):
+    _lib.call("fmd_attn_pack", _p(src_q), _p(src_kv), B, Tq, Tk, heads, dh, int(raw), int(cross), which0, which1,
+              _p(cq), _p(ck), _p(cv), stream())
+
+
+def _attn_softmax_fwd(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross):
+    dev = src_q.device
+    cq, ck, cv = _attn_planes(B, heads, Tq, dh, dev), _attn_planes(B, heads, Tk, dh, dev), _attn_planes(B, heads, Tk, dh, dev)
+    _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, 0, 2, cq, ck, cv)
+    co = torch.empty_like(cq)
+    lse = torch.empty((B, heads, Tq), device=dev, dtype=F32)
+    _lib.call("fmd_attn_mfma_fwd", _p(cq), _p(ck), _p(cv), B * heads, Tq, Tk, dh, _p(co), _p(lse), stream())
+    o = torch.empty((B, Tq, heads * dh), device=dev, dtype=BF16)
+    _lib.call("fmd_attn_unpack", _p(co), None, None, B, Tq, Tk, heads, dh, int(raw), int(cross), 3, 3, _p(o), None,
+              stream())
+    return o, lse
+
+
+def _attn_softmax_bwd(src_q, src_kv, o, dout, lse, B, Tq, Tk, heads, dh, raw, cross, dst_q, dst_kv):
+    dev = src_q.device
+    cq, ck, cv = _attn_planes(B, heads, Tq, dh, dev), _attn_planes(B, heads, Tk, dh, dev), _attn_planes(B, heads, Tk, dh, dev)
+    _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, 0, 2, cq, ck, cv)
+    co, cdo = torch.empty_like(cq), torch.empty_like(cq)
+    _attn_pack(o, o, B, Tq, Tk, heads, dh, raw, cross, 3, 3, co)
+    _attn_pack(dout.contiguous(), dout, B, Tq, Tk, heads, dh, raw, cross, 3, 3, cdo)
+    cdq, cdk, cdv = torch.empty_like(cq), torch.empty_like(ck), torch.empty_like(cv)
+    delta = torch.empty_like(lse)
+    _lib.call("fmd_attn_mfma_bwd", _p(cq), _p(ck), _p(cv), _p(co), _p(cdo), _p(lse), _p(delta), B * heads, Tq, Tk,
+              dh, _p(cdq), _p(cdk), _p(cdv), stream())
+    _lib.call("fmd_attn_unpack", _p(cdq), _p(cdk), _p(cdv), B, Tq, Tk, heads, dh, int(raw), int(cross), 0, 2,
+              _p(dst_q), _p(dst_kv), stream())
+
+
 def attention_fwd(qkv, T, heads, dh, raw):
+    """Softmax self-attention over the fused qkv projection [B][T][3*inner] -> (o [B][T][inner], lse)."""
     B = qkv.shape[0]
+    if not _ATTN_VALU:
+        return _attn_softmax_fwd(qkv, qkv, B, T, T, heads, dh, raw, 0)
     o = torch.empty((B, T, heads * dh), device=qkv.device, dtype=BF16)
     lse = torch.empty((B, heads, T), device=qkv.device, dtype=F32)
     _lib.call("fmd_attention_fwd", _p(qkv), B, T, heads, dh, int(raw), _p(o), _p(lse), stream())
@@ -591,6 +640,8 @@ def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None, raw=1):
         saved = torch.empty((int(_lib.lib().fmd_linear_attention_state(B, heads)),), device=q.device, dtype=F32)
         ws = _la_workspace(B, heads, q.device)
     else:
+        if not _ATTN_VALU:
+            return _attn_softmax_fwd(q, kv, B, Tq, Tk, heads, dh, raw, 1)
         saved = torch.empty((B, heads, Tq), device=q.device, dtype=F32)
         ws = None
     _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, int(raw), int(lin),
@@ -601,8 +652,11 @@ def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None, raw=1):
 def cross_attention_bwd(q, kv, o, dout, saved, Tq, Tk, heads, dh, linear_eps=None, raw=1):
     B = q.shape[0]
     lin = linear_eps is not None
-    ws = _la_workspace(B, heads, q.device) if lin else torch.empty((B, heads, Tq), device=q.device, dtype=F32)
     dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+    if not lin and not _ATTN_VALU:
+        _attn_softmax_bwd(q, kv, o, dout, saved, B, Tq, Tk, heads, dh, raw, 1, dq, dkv)
+        return dq, dkv
+    ws = _la_workspace(B, heads, q.device) if lin else torch.empty((B, heads, Tq), device=q.device, dtype=F32)
     _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(ws), B, Tq, Tk, heads, dh,
               int(raw), int(lin), float(linear_eps or 0.0), _p(dq), _p(dkv), stream())
     return dq, dkv
@@ -631,6 +685,9 @@ def context_norm_bwd(ctx, tok_major, groups, mr, dout, dgamma, dbeta):
 def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
     B = qkv.shape[0]
     dqkv = torch.empty_like(qkv)
+    if not _ATTN_VALU:
+        _attn_softmax_bwd(qkv, qkv, o, dout, lse, B, T, T, heads, dh, raw, 0, dqkv, dqkv)
+        return dqkv
     delta = torch.empty_like(lse)
     _lib.call("fmd_attention_bwd", _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), B, T, heads, dh, int(raw),
               _p(dqkv), stream())

@@ -272,6 +272,27 @@ int fmd_cross_attention_fwd(const void* q, const void* kv, int32_t B, int32_t Tq
 int fmd_cross_attention_bwd(const void* q, const void* kv, const void* o, const void* dout, const float* lse_or_state,
                             float* ws_or_delta, int32_t B, int32_t Tq, int32_t Tk, int32_t heads, int32_t dh,
                             int32_t raw, int32_t linear, float eps, void* dq, void* dkv, fmd_stream_t s);
+/* Softmax attention on MFMA (csrc/attention_mfma.hip), the path behind every softmax attention block
+ * (attention.py:42-44, 115, 185, 269).  The reference's head split (raw reshape or view/transpose; self:
+ * src_q = src_kv = qkv [B][T][3*inner]; cross: src_q = q [B][Tq][inner], src_kv = kv [B][Tk][2*inner];
+ * which 3 = the attention output o [B][Tq][inner]) is undone into canonical bf16 planes
+ * [B*heads][rows][fmd_attn_head_pad(dh)] (q/o/dq plane cq, k plane ck, v plane cv; pad zero-filled).
+ * fmd_attn_pack gathers planes which0..which1 (0 q, 1 k, 2 v, 3 o/dout into cq); fmd_attn_unpack scatters
+ * them back (0..2 into dst_q for self attention = dqkv, into dst_q / dst_kv for cross; 3 into dst_q).
+ * fmd_attn_mfma_fwd: co = softmax(cq ck^T / sqrt(dh)) cv, lse [B*heads][Tq] (natural log).
+ * fmd_attn_mfma_bwd: delta [B*heads][Tq] scratch, writes cdq, cdk, cdv.  dh <= 64. */
+int32_t fmd_attn_head_pad(int32_t dh);
+int fmd_attn_pack(const void* src_q, const void* src_kv, int32_t B, int32_t Tq, int32_t Tk, int32_t heads,
+                  int32_t dh, int32_t raw, int32_t cross, int32_t which0, int32_t which1, void* cq, void* ck,
+                  void* cv, fmd_stream_t s);
+int fmd_attn_unpack(const void* cq, const void* ck, const void* cv, int32_t B, int32_t Tq, int32_t Tk,
+                    int32_t heads, int32_t dh, int32_t raw, int32_t cross, int32_t which0, int32_t which1,
+                    void* dst_q, void* dst_kv, fmd_stream_t s);
+int fmd_attn_mfma_fwd(const void* cq, const void* ck, const void* cv, int32_t BH, int32_t Tq, int32_t Tk,
+                      int32_t dh, void* co, float* lse, fmd_stream_t s);
+int fmd_attn_mfma_bwd(const void* cq, const void* ck, const void* cv, const void* co, const void* cdo,
+                      const float* lse, float* delta, int32_t BH, int32_t Tq, int32_t Tk, int32_t dh, void* cdq,
+                      void* cdk, void* cdv, fmd_stream_t s);
 /* context_norm of SpatialCrossAttention: GroupNorm over the fp32 context ((N, C, T) or token-major (N, T, C))
  * -> bf16 [N][T][Cpad] (zero pad channels); mr [N][groups][2] = mean, rstd.  The backward accumulates
  * dgamma / dbeta only (the context is conditioning data). */
