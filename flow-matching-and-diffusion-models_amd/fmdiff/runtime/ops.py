@@ -569,6 +569,15 @@ def _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, which0, which1, 
               _p(cq), _p(ck), _p(cv), stream())
 
 
+class AttnSaved:
+    """What the MFMA softmax attention forward keeps for its backward: lse [B][heads][Tq] and the canonical
+    q, k, v, o planes (so the backward packs only dout)."""
+    __slots__ = ("lse", "cq", "ck", "cv", "co")
+
+    def __init__(self, lse, cq, ck, cv, co):
+        self.lse, self.cq, self.ck, self.cv, self.co = lse, cq, ck, cv, co
+
+
 def _attn_softmax_fwd(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross):
     dev = src_q.device
     cq, ck, cv = _attn_planes(B, heads, Tq, dh, dev), _attn_planes(B, heads, Tk, dh, dev), _attn_planes(B, heads, Tk, dh, dev)
@@ -579,15 +588,22 @@ def _attn_softmax_fwd(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross):
     o = torch.empty((B, Tq, heads * dh), device=dev, dtype=BF16)
     _lib.call("fmd_attn_unpack", _p(co), None, None, B, Tq, Tk, heads, dh, int(raw), int(cross), 3, 3, _p(o), None,
               stream())
-    return o, lse
+    return o, AttnSaved(lse, cq, ck, cv, co)
 
 
-def _attn_softmax_bwd(src_q, src_kv, o, dout, lse, B, Tq, Tk, heads, dh, raw, cross, dst_q, dst_kv):
+def _attn_softmax_bwd(src_q, src_kv, o, dout, saved, B, Tq, Tk, heads, dh, raw, cross, dst_q, dst_kv):
+    """``saved``: the forward's AttnSaved, or a bare lse tensor (q, k, v, o are then packed again)."""
     dev = src_q.device
-    cq, ck, cv = _attn_planes(B, heads, Tq, dh, dev), _attn_planes(B, heads, Tk, dh, dev), _attn_planes(B, heads, Tk, dh, dev)
-    _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, 0, 2, cq, ck, cv)
-    co, cdo = torch.empty_like(cq), torch.empty_like(cq)
-    _attn_pack(o, o, B, Tq, Tk, heads, dh, raw, cross, 3, 3, co)
+    if isinstance(saved, AttnSaved):
+        lse, cq, ck, cv, co = saved.lse, saved.cq, saved.ck, saved.cv, saved.co
+    else:
+        lse = saved
+        cq, ck = _attn_planes(B, heads, Tq, dh, dev), _attn_planes(B, heads, Tk, dh, dev)
+        cv = _attn_planes(B, heads, Tk, dh, dev)
+        _attn_pack(src_q, src_kv, B, Tq, Tk, heads, dh, raw, cross, 0, 2, cq, ck, cv)
+        co = torch.empty_like(cq)
+        _attn_pack(o, o, B, Tq, Tk, heads, dh, raw, cross, 3, 3, co)
+    cdo = torch.empty_like(cq)
     _attn_pack(dout.contiguous(), dout, B, Tq, Tk, heads, dh, raw, cross, 3, 3, cdo)
     cdq, cdk, cdv = torch.empty_like(cq), torch.empty_like(ck), torch.empty_like(cv)
     delta = torch.empty_like(lse)

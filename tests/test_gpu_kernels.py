@@ -298,7 +298,8 @@ def test_groupnorm_deferred_gamma_beta_fold():
 
 
 @pytest.mark.parametrize("raw,T,heads,dh", [(1, 64, 4, 64), (0, 256, 16, 8), (0, 64, 8, 32), (1, 64, 2, 16),
-                                         (1, 1024, 4, 64), (0, 300, 2, 40)])
+                                         (1, 1024, 4, 64), (0, 300, 2, 40), (1, 100, 3, 24), (0, 17, 2, 64),
+                                         (0, 1000, 1, 12), (1, 4096, 2, 32)])
 def test_attention(raw, T, heads, dh):
     O = ops()
     B = 2
@@ -321,6 +322,9 @@ def test_attention(raw, T, heads, dh):
     _close(og, o_tok.detach())
     dq = O.attention_bwd(qkv.to(DEV), og, do.contiguous().to(torch.bfloat16).to(DEV), lse, T, heads, dh, raw)
     _close(dq, f.grad, rel=2e-2)
+    if hasattr(lse, "lse"):   # MFMA path: the backward from a bare lse re-packs q, k, v, o -- same result
+        dq2 = O.attention_bwd(qkv.to(DEV), og, do.contiguous().to(torch.bfloat16).to(DEV), lse.lse, T, heads, dh, raw)
+        assert torch.equal(dq, dq2)
 
 
 @pytest.mark.parametrize("raw,T,heads,dh", [(1, 256, 4, 64), (1, 4160, 2, 64), (0, 777, 2, 32), (1, 100, 3, 24)])
@@ -347,7 +351,8 @@ def test_linear_attention(raw, T, heads, dh):
     _close(dq, f.grad, rel=2e-2)
 
 
-@pytest.mark.parametrize("linear,Tq,Tk,heads,dh", [(0, 256, 1024, 4, 64), (0, 70, 33, 2, 32), (1, 256, 1024, 4, 64),
+@pytest.mark.parametrize("linear,Tq,Tk,heads,dh", [(0, 256, 1024, 4, 64), (0, 70, 33, 2, 32), (0, 1, 300, 2, 16),
+                                                  (0, 600, 5, 3, 48), (1, 256, 1024, 4, 64),
                                                   (1, 1500, 2100, 2, 24)])
 def test_cross_attention(linear, Tq, Tk, heads, dh):
     """SpatialCrossAttention core (reference attention.py:179-184: raw q / kv reshapes, chunk(2)) vs fp32 autograd,
