@@ -97,10 +97,24 @@ def pmc_traffic():
         return float(json.load(f)["traffic_bytes_per_launch"])
 
 
-def cpu_baseline(iters=2):
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(iters=3, batch=2, sampler_steps=3):
     """The oracle (fp32 PyTorch-CPU restatement of the reference, proven bit-exact in
-    tests/test_oracle_golden.py) timed on this host: one FM train step (fwd+bwd+AdamW) at
-    batch 1 on the config-B model, median of ``iters`` after one warm-up."""
+    tests/test_oracle_golden.py) timed on this host, per BASELINE.md section 3: one FM train step
+    (fwd+bwd+AdamW) at batch ``batch`` on the config-B model, median of ``iters`` after one warm-up; and a
+    bounded sample of the 50-step FlowMatchEuler sampler (the last ``sampler_steps`` steps of the 50-step
+    schedule at the same batch, one UNet forward + Euler update each, timed after one warm-up step)."""
+    from oracle import schedulers as OS
     from oracle import spec as S
     from oracle import train_step as OT
     from oracle import unet as U
@@ -110,7 +124,7 @@ def cpu_baseline(iters=2):
     spec = S.derive_spec(LDCT_FM_UNET, "concatenate", 1)
     sd = {k: v.requires_grad_() for k, v in U.seeded_state_dict(spec, 0).items()}
     g = torch.Generator().manual_seed(0)
-    B = 1
+    B = batch
     clean = torch.rand(B, 1, 256, 256, generator=g)
     ldct = (clean + 0.05 * torch.randn(B, 1, 256, 256, generator=g)).clamp(0, 1)
     state = {}
@@ -125,14 +139,26 @@ def cpu_baseline(iters=2):
         sc.backward()
         OT.adamw_step(sd, 1e-4, i + 1, state)
         dt = time.perf_counter() - t0
-        log(f"[bench] cpu baseline iter {i}: {dt:.2f} s ({threads} threads)")
+        log(f"[bench] cpu baseline train iter {i}: {dt:.2f} s ({threads} threads)")
         if i:
             times.append(dt)
     times.sort()
     med = times[len(times) // 2]
-    return dict(value=B / med, unit="train images/s", cores=threads, kind="port",
+    # sampler: warm-up step, then the timed last `sampler_steps` steps of the 50-step schedule
+    sched = OS.FlowMatchEuler(1000, 1.0)
+    init = torch.randn(B, 1, 256, 256, generator=g)
+    sdd = {k: v.detach() for k, v in sd.items()}
+    OT.sample(sdd, spec, sched, 50, init, ldct, last_n_steps=1)
+    t0 = time.perf_counter()
+    OT.sample(sdd, spec, sched, 50, init, ldct, last_n_steps=sampler_steps)
+    ds = (time.perf_counter() - t0) / sampler_steps
+    log(f"[bench] cpu baseline sampler: {ds:.2f} s per step at batch {B}")
+    return dict(value=B / med, unit="train images/s", cores=threads, kind="port", cpu_model=_cpu_model(),
+                sampler_steps_per_sec=1.0 / ds, sampler_images_per_sec=B / (50 * ds),
                 sample=f"oracle FM train step (fwd+bwd+AdamW), batch {B}, 256x256, config-B EfficientUNetND fp32, "
-                       f"median of {iters} after 1 warm-up ({med:.2f} s/step)")
+                       f"median of {iters} after 1 warm-up ({med:.2f} s/step); sampler: last {sampler_steps} of 50 "
+                       f"FlowMatchEuler steps at batch {B} after 1 warm-up ({ds:.2f} s/step, images/s extrapolated "
+                       f"to the 50-step loop)")
 
 
 def main():

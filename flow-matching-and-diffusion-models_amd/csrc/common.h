@@ -24,7 +24,13 @@ FMD_DEV unsigned int f2bf(float f) {
   __bf16 b = (__bf16)f;
   return (unsigned int)__builtin_bit_cast(unsigned short, b);
 }
-FMD_DEV unsigned int pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (the f2bf(lo) | f2bf(hi) << 16 form compiles to two
+// single-operand converts + shift + or)
+typedef __attribute__((ext_vector_type(2))) float f32x2_;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_;
+FMD_DEV unsigned int pack2(float lo, float hi) {
+  return __builtin_bit_cast(unsigned int, __builtin_convertvector(f32x2_{lo, hi}, bf16x2_));
+}
 
 // v_exp_f32 + v_rcp_f32 (1 ulp): no IEEE division sequence in the hot prologues
 FMD_DEV float sigmoidf_(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }

@@ -39,6 +39,7 @@ class FlatParams:
             ids = {id(p) for p in first}
             params = list(first) + [p for p in params if id(p) not in ids]
         self.split_at = sum(p.numel() for p in first) if first else 0
+        self.order = params
         dev = params[0].device
         total = sum(p.numel() for p in params)
         self.data = torch.empty(total, device=dev, dtype=torch.float32)
@@ -58,6 +59,35 @@ class FlatParams:
         self.numel = total
 
 
+def _segment_buckets(sizes, buckets: int):
+    """Cut backward segments (element counts, in backward order) into contiguous all-reduce buckets: the
+    first segment (head + decoder, final first) alone, the middle segments merged into ``buckets - 2`` runs of
+    about equal size, and the last segment (time MLP + grouped emb projections, final only at the very end:
+    the one exposed exchange) alone.  Returns [((first_seg, last_seg), (lo, hi) flat range)], backward order."""
+    n = len(sizes)
+    if n <= 2 or buckets <= 2:
+        cuts = [(0, 0), (1, n - 1)] if n > 1 else [(0, 0)]
+    else:
+        mid = sizes[1:-1]
+        k = max(1, min(buckets - 2, len(mid)))
+        target = sum(mid) / k
+        cuts, first, acc = [(0, 0)], 1, 0
+        for j, m in enumerate(mid):
+            acc += m
+            seg = j + 1
+            runs_left = k - (len(cuts) - 1) - 1
+            if seg == n - 2 or (acc >= target and runs_left > 0 and (n - 2 - seg) >= runs_left):
+                cuts.append((first, seg))
+                first, acc = seg + 1, 0
+        cuts.append((n - 1, n - 1))
+    out, lo = [], 0
+    for f, l in cuts:
+        hi = lo + sum(sizes[f:l + 1])
+        out.append(((f, l), (lo, hi)))
+        lo = hi
+    return out
+
+
 class FusedTrainStep:
     def __init__(self, model, *, objective: str = "flow_matching", lr: float = 1e-4, weight_decay: float = 0.0,
                  warmup: int = 500, total_steps: int = 10 ** 9, num_train_timesteps: int = 1000,
@@ -69,7 +99,16 @@ class FusedTrainStep:
         # data parallel: the decoder's gradients (final after backward part 1) go first in the flat buffer
         # and are all-reduced while the encoder's backward runs
         self.overlap = (world > 1 if overlap_allreduce is None else bool(overlap_allreduce)) and grad_accum <= 1
-        self.flat = FlatParams(model, self.eng.decoder_params() if self.overlap else None)
+        # overlapped exchange: the flat buffer is laid out in backward-segment order and cut into
+        # ``allreduce_buckets`` contiguous buckets of whole segments; bucket b is all-reduced (async) while
+        # the segments of the later buckets run, only the last bucket's exchange is exposed
+        self.seg_buckets = None
+        first = None
+        if self.overlap:
+            groups = self.eng.backward_param_groups()
+            first = [p for g in groups for p in g]
+            self.seg_buckets = _segment_buckets([sum(p.numel() for p in g) for g in groups], allreduce_buckets)
+        self.flat = FlatParams(model, first)
         dev = self.flat.data.device
         self.m = torch.zeros_like(self.flat.data)
         self.v = torch.zeros_like(self.flat.data)
@@ -114,15 +153,21 @@ class FusedTrainStep:
         ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
         self.loss_sum.add_(self.loss, alpha=float(N))
         if self.overlap:
-            self.eng.backward(ctx, dpred, part=1)   # part 2 in _bwd_rest, after the decoder all-reduce starts
+            # bucket 0's segments now; the rest in _bwd_bucket, each after the previous bucket's all-reduce started
+            self.eng.backward(ctx, dpred, segs=self.seg_buckets[0][0])
             self._ctx = ctx
         else:
             self.eng.backward(ctx, dpred)
         return self.loss
 
+    def _bwd_bucket(self, b):
+        self.eng.backward(self._ctx, None, segs=self.seg_buckets[b][0])
+        if b == len(self.seg_buckets) - 1:
+            self._ctx = None
+
     def _bwd_rest(self):
-        self.eng.backward(self._ctx, None, part=2)
-        self._ctx = None
+        for b in range(1, len(self.seg_buckets)):
+            self._bwd_bucket(b)
 
     def _allreduce(self):
         bucketed_allreduce(self.flat.grad, self.buckets, self.pg)
@@ -132,20 +177,34 @@ class FusedTrainStep:
         ``context_ca``: cross-attention conditioning (conditioning "attention", e.g. VAE latents)."""
         loss = self._fwd_bwd(clean, ldct, noise, t, context_ca)
         if self.overlap:
-            self._overlapped_tail(self._bwd_rest)
+            self._overlapped_tail(self._bwd_bucket)
         else:
             self._allreduce()
         self._adamw()
         return loss
 
-    def _overlapped_tail(self, rest):
-        """Decoder gradients all-reduced (async) while ``rest`` (the encoder backward) runs, then the rest."""
-        k = self.flat.split_at
-        works = bucketed_allreduce_async(self.flat.grad[:k], max(1, self.buckets // 2), self.pg)
-        rest()
-        bucketed_allreduce(self.flat.grad[k:], max(1, self.buckets // 2), self.pg)
+    def _overlapped_tail(self, run_bucket):
+        """Bucket b's gradients (final after its backward segments) all-reduced asynchronously while
+        ``run_bucket(b + 1)`` runs the next bucket's segments; the last bucket's exchange is the only exposed
+        one.  ``run_bucket``: eager segments (_bwd_bucket) or their captured graphs."""
+        works = []
+        nb = len(self.seg_buckets)
+        for b in range(nb):
+            lo, hi = self.seg_buckets[b][1]
+            if b == nb - 1:
+                bucketed_allreduce(self.flat.grad[lo:hi], 1, self.pg)
+            else:
+                works += bucketed_allreduce_async(self.flat.grad[lo:hi], 1, self.pg)
+                run_bucket(b + 1)
         for w in works:
             w.wait()
+
+    def exposed_allreduce_elems(self) -> int:
+        """fp32 gradient elements whose all-reduce is not overlapped with backward compute."""
+        if not self.overlap:
+            return self.flat.numel
+        lo, hi = self.seg_buckets[-1][1]
+        return hi - lo
 
     def _adamw(self):
         b1, b2 = self.hp["betas"]
@@ -277,12 +336,13 @@ class FusedTrainStep:
             else:
                 self._graph_loss = self.step(*self._static)
         self._graph = g
-        self._graph2 = None
-        if self._split and self.overlap:   # the encoder backward as a second graph in the same pool
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=g.pool(), capture_error_mode=mode):
-                self._bwd_rest()
-            self._graph2 = g2
+        self._graphs = []
+        if self._split and self.overlap:   # each later bucket's backward segments as a graph in the same pool
+            for b in range(1, len(self.seg_buckets)):
+                gb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb, pool=g.pool(), capture_error_mode=mode):
+                    self._bwd_bucket(b)
+                self._graphs.append(gb)
 
     def replay(self, clean=None, ldct=None, context_ca=None, noise=None, t=None):
         for i, new in ((0, clean), (1, ldct), (2, noise), (3, t), (4, context_ca)):
@@ -293,8 +353,8 @@ class FusedTrainStep:
             self._static[i].copy_(new)
         self._graph.replay()
         if self._split:
-            if self._graph2 is not None:
-                self._overlapped_tail(self._graph2.replay)
+            if self._graphs:
+                self._overlapped_tail(lambda b: self._graphs[b - 1].replay())
             else:
                 self._allreduce()
             self._adamw()

@@ -28,7 +28,7 @@ from __future__ import annotations
 import math
 import os
 import weakref
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -257,7 +257,7 @@ class WeightCache:
 
 
 class Ctx:
-    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark", "cca")
+    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark", "cca", "marks")
 
     def __init__(self, emb, save, N):
         self.emb = emb
@@ -267,6 +267,7 @@ class Ctx:
         self.eo_all = None      # [N][sum O] grouped emb projections of all ResBlocks
         self.demb_all = None
         self.mark = 0           # tape length when the decoder started (backward part 1 = tape[mark:])
+        self.marks: List[int] = []   # tape length before each encoder stage (backward segments, see seg_ranges)
         self.cca = None         # cross-attention context (context_ca), fp32 as passed to the model
 
 
@@ -811,9 +812,13 @@ class UNetEngine:
             hs = []
             h = x
             for blk in m.input_blocks:
+                if ctx.tape is not None:
+                    ctx.marks.append(len(ctx.tape))
                 for layer in blk:
                     h = self._apply(layer, h, ctx)
                 hs.append(h)
+            if ctx.tape is not None:
+                ctx.marks.append(len(ctx.tape))
             for layer in m.middle_block:
                 h = self._apply(layer, h, ctx)
             if ctx.tape is not None:
@@ -826,9 +831,13 @@ class UNetEngine:
                     h = self._apply(layer, h, ctx)
             out = self.head(m.out[0], m.out[2].conv, h, ctx)
         else:
+            if ctx.tape is not None:
+                ctx.marks.append(len(ctx.tape))
             h = self.conv_layer(m.conv_in, x, ctx)
             res = [h]
             for blk in m.down_blocks:
+                if ctx.tape is not None:
+                    ctx.marks.append(len(ctx.tape))
                 for j, r in enumerate(blk.resnets):
                     h = self.res_block(r, [h], ctx)
                     if blk.attentions is not None:
@@ -837,6 +846,8 @@ class UNetEngine:
                 if blk.downsamplers is not None:
                     h = self._apply(blk.downsamplers[0], h, ctx)
                     res.append(h)
+            if ctx.tape is not None:
+                ctx.marks.append(len(ctx.tape))
             if m.mid_block is not None:
                 h = self.res_block(m.mid_block.resnets[0], [h], ctx)
                 if m.mid_block.attentions is not None:
@@ -873,55 +884,89 @@ class UNetEngine:
             return self.cross_attention(layer, h, ctx)
         raise NotImplementedError(type(layer).__name__)
 
-    def backward(self, ctx: Ctx, dpred: torch.Tensor, part: int = 0):
+    # Backward segments, in backward order: 0 = output head + decoder, 1 = middle block, then the encoder
+    # stages deepest first (EfficientUNetND input_blocks / UNetDiffusersND conv_in + down_blocks), and last the
+    # grouped ResBlock emb projections + time MLP.  The parameters of segment k (backward_param_groups()[k])
+    # have their final gradients once segments 0..k ran, so a data-parallel step can all-reduce them while
+    # the later segments run.
+    def _stage_modules(self) -> List[List[torch.nn.Module]]:
+        m = self.m
+        if self.kind == "efficient":
+            return [[blk] for blk in m.input_blocks]
+        return [[m.conv_in]] + [[blk] for blk in m.down_blocks]
+
+    def _late_ids(self) -> set:
+        late = set()
+        if self.gl is not None:
+            for sub in self.m.modules():
+                if isinstance(sub, ResBlockND) and id(sub) in self.gl_slot and sub.emb_layers is not None:
+                    late.update(id(p) for p in sub.emb_layers.parameters())
+        return late
+
+    def backward_param_groups(self) -> List[List[torch.nn.Parameter]]:
+        """Parameters per backward segment (see above); the last group holds every parameter not in an
+        earlier one (time MLP, grouped emb projections, anything unused)."""
+        m = self.m
+        if self.kind == "efficient":
+            head = [[m.output_blocks, m.out], [m.middle_block]]
+        else:
+            head = [[m.up_blocks, m.conv_norm_out, m.conv_out], [m.mid_block] if m.mid_block is not None else []]
+        mods = head + list(reversed(self._stage_modules()))
+        late = self._late_ids()
+        seen, groups = set(), []
+        for ms in mods:
+            g = []
+            for mod in ms:
+                for p in mod.parameters():
+                    if id(p) not in late and id(p) not in seen:
+                        seen.add(id(p))
+                        g.append(p)
+            groups.append(g)
+        groups.append([p for p in m.parameters() if id(p) not in seen])
+        return groups
+
+    @staticmethod
+    def seg_ranges(ctx: Ctx) -> List[Tuple[int, int]]:
+        """Tape ranges [lo, hi) of the backward segments (segment 0 additionally runs the output head)."""
+        mk = ctx.marks
+        out = [(ctx.mark, len(ctx.tape)), (mk[-1], ctx.mark)]
+        for i in range(len(mk) - 1, 0, -1):
+            out.append((mk[i - 1], mk[i]))
+        out.append((0, mk[0]))
+        return out
+
+    def backward(self, ctx: Ctx, dpred: torch.Tensor, part: int = 0, segs: Optional[Tuple[int, int]] = None):
         """Run the written-out backward. ``dpred``: bf16 NHWC [N,H,W,Kpad] gradient of the output.
 
-        ``part`` 1 runs the head and the decoder (tape[mark:]) and folds their GroupNorm gamma/beta, so
-        every ``decoder_params()`` gradient is final when it returns; ``part`` 2 runs the rest (middle,
-        encoder, grouped emb projections, time MLP).  A data-parallel step all-reduces the decoder's
-        gradients while part 2 runs.  ``part`` 0 = both."""
-        if part in (0, 1):
-            ops.gb_defer()   # GroupNorm gamma/beta folds: batched launches
-            try:
-                self._head_bwd(dpred)
-                for fn in reversed(ctx.tape[ctx.mark:] if part == 1 else ctx.tape):
+        ``segs`` = (first, last): run backward segments first..last (inclusive, see backward_param_groups);
+        their parameter gradients (GroupNorm gamma/beta folds included) are final on return, and the tape is
+        released after the last segment.  ``part`` (older interface): 1 = segment 0 (head + decoder), 2 = the
+        rest, 0 = everything."""
+        nseg = len(ctx.marks) + 2
+        if segs is None:
+            segs = {0: (0, nseg - 1), 1: (0, 0), 2: (1, nseg - 1)}[part]
+        lo, hi = segs
+        ranges = self.seg_ranges(ctx)
+        ops.gb_defer()   # GroupNorm gamma/beta folds: batched launches
+        try:
+            for k in range(lo, hi + 1):
+                if k == 0:
+                    self._head_bwd(dpred)
+                a, b = ranges[k]
+                for fn in reversed(ctx.tape[a:b]):
                     fn()
-            finally:
-                ops.gb_flush()
-            if part == 1:
-                self._join()
-                return
-        if part == 2:
-            ops.gb_defer()
-            try:
-                for fn in reversed(ctx.tape[:ctx.mark]):
-                    fn()
-            finally:
-                ops.gb_flush()
-        self._join()   # every weight gradient has landed before anyone reads .grad
-        ctx.tape = None
-        self._head_bwd = None
+        finally:
+            ops.gb_flush()
+        self._join()   # every weight gradient of these segments has landed before anyone reads .grad
+        if hi == nseg - 1:
+            ctx.tape = None
+            self._head_bwd = None
 
     def decoder_params(self) -> List[torch.nn.Parameter]:
         """Parameters whose gradients are final after ``backward(part=1)``: the decoder blocks and the
         output head, minus the ResBlock emb projections (their gradients come from the grouped linear
         backward, which runs last)."""
-        m = self.m
-        mods = ([m.output_blocks, m.out] if self.kind == "efficient"
-                else [m.up_blocks, m.conv_norm_out, m.conv_out])
-        late = set()
-        if self.gl is not None:
-            for mod in mods:
-                for sub in mod.modules():
-                    if isinstance(sub, ResBlockND) and id(sub) in self.gl_slot and sub.emb_layers is not None:
-                        late.update(id(p) for p in sub.emb_layers.parameters())
-        out, seen = [], set()
-        for mod in mods:
-            for p in mod.parameters():
-                if id(p) not in late and id(p) not in seen:
-                    seen.add(id(p))
-                    out.append(p)
-        return out
+        return self.backward_param_groups()[0]
 
     # ----------------------------------------------------------- utilities
     def stage_input(self, x: torch.Tensor, context: Optional[torch.Tensor]):

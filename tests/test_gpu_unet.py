@@ -266,14 +266,14 @@ def test_fused_sampler_matches_plain_euler_loop(golden):
         assert err < 2e-3
 
 
-def test_fused_train_step_split_capture_matches_full_graph(golden):
+@pytest.mark.parametrize("name", ["ldct_fm_test", "ldct_fm_diffusers_b64"])
+def test_fused_train_step_split_capture_matches_full_graph(golden, name):
     """FusedTrainStep.capture(split_collectives=True) -- the multi-rank form: forward+backward graph,
     then the (bucketed) all-reduce and AdamW issued eagerly -- reproduces the single-graph step; so does
-    the overlapped form (decoder gradients first in the flat buffer, backward in two graphs with the
-    decoder all-reduce issued between them)."""
+    the overlapped form (flat buffer in backward-segment order, the backward captured as one graph per
+    all-reduce bucket with each bucket's all-reduce issued between them), replayed and eager."""
     from fmdiff.pipelines.train.fused import FusedTrainStep
     T, M = golden
-    name = "ldct_fm_test"
     meta = M[name]
     x, cond = T[f"{name}/x"].to(DEV), T[f"{name}/cond"].to(DEV)
     clean = x.clamp(0, 1)
@@ -283,11 +283,30 @@ def test_fused_train_step_split_capture_matches_full_graph(golden):
         _load_seeded(model, meta)
         tr = FusedTrainStep(model, lr=1e-3, warmup=1, overlap_allreduce=overlap)
         assert (tr.flat.split_at > 0) == overlap
+        if overlap:
+            nb = len(tr.seg_buckets)
+            assert nb >= 3 and tr.seg_buckets[-1][1][1] == tr.flat.numel
+            assert tr.exposed_allreduce_elems() < tr.flat.numel // 2
         torch.manual_seed(11)
         tr.capture(clean, cond, warmup_iters=2, split_collectives=split)
+        if overlap:
+            assert len(tr._graphs) == nb - 1
         losses = [float(tr.replay().item()) for _ in range(2)]
         torch.cuda.synchronize()
         res.append((losses, {k: p.detach().clone() for k, p in model.named_parameters()}))
+    # eager overlapped stepping against an eager non-overlapped run from the same start
+    eager = []
+    for overlap in (False, True):
+        model = _build(meta).to(DEV)
+        _load_seeded(model, meta)
+        tr = FusedTrainStep(model, lr=1e-3, warmup=1, overlap_allreduce=overlap)
+        torch.manual_seed(5)
+        ls = [float(tr.step(clean, cond).item()) for _ in range(2)]
+        torch.cuda.synchronize()
+        eager.append((ls, {k: p.detach().clone() for k, p in model.named_parameters()}))
+    assert eager[0][0] == eager[1][0]
+    for k in eager[0][1]:
+        assert torch.equal(eager[0][1][k], eager[1][1][k]), k
     la, pa = res[0]
     assert all(math.isfinite(v) for v in la)
     for lb, pb in res[1:]:

@@ -234,3 +234,31 @@ def test_tensor_cache_paths_and_dataset(tmp_path):
     (root / "test.txt").write_text("c9\tc9/sdct/9.dcm\tc9/ldct/9.dcm\n")
     with pytest.raises(FileNotFoundError, match="tensor cache entry missing"):
         LDCTCacheDataset(str(root), train=False)[0]
+
+
+@pytest.mark.parametrize("impl", ["efficient", "diffusers"])
+def test_backward_segments_partition_parameters(impl):
+    """The overlapped gradient exchange's bookkeeping (fused.py _segment_buckets, engine
+    backward_param_groups): every parameter in exactly one backward segment, buckets contiguous over the flat
+    buffer in backward order, only the last segment (time MLP + grouped emb projections) exposed."""
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.pipelines.train.fused import _segment_buckets
+    from fmdiff.runtime.engine import get_engine
+    cfg = {"block_out_channels": [32, 64, 64], "layers_per_block": 1, "attention_resolutions": [2]}
+    if impl == "diffusers":
+        cfg = {"unet_impl": "diffusers_nd", "block_out_channels": [32, 64], "layers_per_block": 1,
+               "down_block_types": ["DownBlock2D", "AttnDownBlock2D"], "up_block_types": ["AttnUpBlock2D", "UpBlock2D"],
+               "norm_num_groups": 8}
+    model = DiffusionUNetFactory().build(cfg, "concatenate", 1)
+    groups = get_engine(model).backward_param_groups()
+    ids = [id(p) for g in groups for p in g]
+    assert len(ids) == len(set(ids)) == len(list(model.parameters()))
+    sizes = [sum(p.numel() for p in g) for g in groups]
+    for nb in (1, 2, 3, 4, 8):
+        bk = _segment_buckets(sizes, nb)
+        assert bk[0][0][0] == 0 and bk[-1][0][1] == len(sizes) - 1
+        assert bk[0][1][0] == 0 and bk[-1][1][1] == sum(sizes)
+        for (a, b), (c, d) in zip(bk, bk[1:]):
+            assert a[1] + 1 == c[0] and b[1] == d[0]
+        if nb >= 3:
+            assert bk[-1][0] == (len(sizes) - 1, len(sizes) - 1)

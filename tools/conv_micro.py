@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--dbg", default="", help="comma list of halo ablation flag values to time as well")
     ap.add_argument("--variants", default="2", help="comma list of halo kernel variants to time (1, 2)")
     ap.add_argument("--staggers", default="", help="comma list of v2 stagger values to time (default: library's)")
+    ap.add_argument("--warm", type=int, default=300, help="back-to-back launches before the first timing (clock ramp)")
+    ap.add_argument("--cold", action="store_true", help="evict L2 / Infinity Cache (512 MiB write) before every call")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     N, H, W, C, K = 8, a.hw, a.hw, a.c, a.c
@@ -83,10 +85,12 @@ def main():
     import ctypes
     from fmdiff import _lib
     L = _lib.lib()
+    flush = torch.zeros(128 << 20, device=dev) if a.cold else None   # 512 MiB
     flagsets = [0] + [int(f) for f in a.dbg.split(",") if f]
     stg = [int(x) for x in a.staggers.split(",") if x] or [None]
     todo = [(name, fl, v, sg) for name in probs for fl in flagsets for v in [int(x) for x in a.variants.split(",")]
             for sg in stg]
+    warmed = False
     for name, fl, var, sg in todo:
         L.fmd_halo_set_variant(ctypes.c_int(var))
         if sg is not None:
@@ -95,17 +99,29 @@ def main():
         if a.only and name not in a.only.split(","):
             continue
         L.fmd_debug_halo_flags(ctypes.c_int(fl))
-        for _ in range(3):
+        for _ in range(3 if warmed else a.warm):   # the chip ramps its clock over the first few hundred ms
             fn()
+        warmed = True
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / a.iters
-        print(f"{name:6s} v{var} stagger={sg} dbg={fl:2d} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s",
+        if a.cold:
+            ms = 0.0
+            for _ in range(a.iters):
+                flush.add_(1.0)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ms += e0.elapsed_time(e1) / a.iters
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+        print(f"{name:6s} v{var} stagger={sg} dbg={fl:2d} {'cold' if a.cold else 'hot '} {ms * 1e3:8.1f} us/call  {flops / ms / 1e9:7.1f} TFLOP/s",
               flush=True)
     L.fmd_debug_halo_flags(ctypes.c_int(0))
 
