@@ -467,6 +467,46 @@ __global__ void sum_pool2_kernel(const bf16r* __restrict__ src, int N, int H, in
   }
 }
 
+// Parameter-free resampling by 2 along the dims with factor 2 (1-, 2- or 3-D, NDHWC bf16, fp32 math):
+//   up = 0 (AvgPoolND kernel=stride=2, src/nn/ops/pooling.py:33-53; also the nearest-x2 data gradient):
+//        dst[low] (+)= scale * sum of the 2^d block of src[high] (odd high extents: the last index is dropped)
+//   up = 1 (nearest-x2 F.interpolate of UpsampleND(use_conv=False), upsampling.py:24-29; also the avg-pool
+//        data gradient): dst[high] (+)= scale * src[high >> 1] (0 past the low extent)
+// low = (Dl, Hl, Wl), high = (Dh, Hh, Wh); a dim with factor 1 has equal extents.
+__global__ void resample2_kernel(const bf16r* __restrict__ src, int N, int Dl, int Hl, int Wl, int Dh, int Hh, int Wh,
+                                 int C, int fz, int fy, int fx, int up, float scale, bf16r* __restrict__ dst,
+                                 int acc) {
+  const long long total = (long long)N * (up ? (long long)Dh * Hh * Wh : (long long)Dl * Hl * Wl) * C;
+  GRID_STRIDE(i, total) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    if (up) {
+      const int x = (int)(r % Wh); r /= Wh;
+      const int y = (int)(r % Hh); r /= Hh;
+      const int z = (int)(r % Dh);
+      const int n = (int)(r / Dh);
+      const int zl = fz == 2 ? z >> 1 : z, yl = fy == 2 ? y >> 1 : y, xl = fx == 2 ? x >> 1 : x;
+      float v = 0.f;
+      if (zl < Dl && yl < Hl && xl < Wl) v = scale * bf2f(src[((((size_t)n * Dl + zl) * Hl + yl) * Wl + xl) * C + c]);
+      if (acc) v += bf2f(dst[i]);
+      dst[i] = (bf16r)f2bf(v);
+    } else {
+      const int x = (int)(r % Wl); r /= Wl;
+      const int y = (int)(r % Hl); r /= Hl;
+      const int z = (int)(r % Dl);
+      const int n = (int)(r / Dl);
+      float v = 0.f;
+      for (int dz = 0; dz < fz; ++dz)
+        for (int dy = 0; dy < fy; ++dy)
+          for (int dx = 0; dx < fx; ++dx)
+            v += bf2f(src[((((size_t)n * Dh + fz * z + dz) * Hh + fy * y + dy) * Wh + fx * x + dx) * C + c]);
+      v *= scale;
+      if (acc) v += bf2f(dst[i]);
+      dst[i] = (bf16r)f2bf(v);
+    }
+  }
+}
+
 __global__ void sum_pool2_3d_kernel(const bf16r* __restrict__ src, int N, int D, int H, int W, int C,
                                     bf16r* __restrict__ dst, int acc) {
   // dst[n][z][y][x][c] (+)= sum of the 2x2x2 block of src (dst D x H x W, src 2D x 2H x 2W)
@@ -925,6 +965,18 @@ int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, v
 int fmd_sum_pool2_3d(const void* src, int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, void* dst,
                      int32_t acc, fmd_stream_t s) {
   LAUNCH(sum_pool2_3d_kernel, grid_for((long long)N * D * H * W * C), (const bf16r*)src, N, D, H, W, C,
+         (bf16r*)dst, acc);
+}
+
+int fmd_resample2(const void* src, int32_t N, int32_t Dl, int32_t Hl, int32_t Wl, int32_t Dh, int32_t Hh, int32_t Wh,
+                  int32_t C, int32_t fz, int32_t fy, int32_t fx, int32_t up, float scale, void* dst, int32_t acc,
+                  fmd_stream_t s) {
+  if (N < 1 || C < 1 || Dl < 1 || Hl < 1 || Wl < 1 || fz < 1 || fz > 2 || fy < 1 || fy > 2 || fx < 1 || fx > 2)
+    return -1;
+  if (Dh < fz * Dl || Hh < fy * Hl || Wh < fx * Wl || Dh > fz * Dl + 1 || Hh > fy * Hl + 1 || Wh > fx * Wl + 1)
+    return -1;
+  const long long work = (long long)N * (up ? (long long)Dh * Hh * Wh : (long long)Dl * Hl * Wl) * C;
+  LAUNCH(resample2_kernel, grid_for(work), (const bf16r*)src, N, Dl, Hl, Wl, Dh, Hh, Wh, C, fz, fy, fx, up, scale,
          (bf16r*)dst, acc);
 }
 

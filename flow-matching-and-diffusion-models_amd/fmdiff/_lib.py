@@ -91,6 +91,7 @@ SIGNATURES = {
     "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
     "fmd_nhwc_to_nchw": [p, i32, i32, i32, i32, i32, p, p],
     "fmd_sum_pool2": [p, i32, i32, i32, i32, p, i32, p],
+    "fmd_resample2": [p, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, f32, p, i32, p],
     "fmd_sum_pool2_3d": [p, i32, i32, i32, i32, i32, p, i32, p],
     "fmd_add_bf16": [p, p, i64, p],
     "fmd_timestep_embedding": [p, i32, i32, i32, i32, f32, f32, i32, p, p],

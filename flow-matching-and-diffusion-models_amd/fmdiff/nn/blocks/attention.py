@@ -67,6 +67,10 @@ class SpatialCrossAttention(ContextBlock):
         self.attention = LinearQKVAttention() if use_linear else QKVAttention(efficient_attn=use_efficient_attn)
         self.proj_out = zero_module(Conv(1, self.inner_dim, self.dim, 1))
 
+    def forward(self, x, context):
+        from ...runtime.standalone import block_forward
+        return block_forward(self, x, None, context)
+
 
 class DiffusersAttentionND(nn.Module):
     def __init__(self, channels: int, heads: int = 1, context_dim: int | None = None, norm_num_groups: int = 32,
@@ -93,4 +97,4 @@ class DiffusersAttentionND(nn.Module):
 
     def forward(self, hidden_states, context=None):
         from ...runtime.standalone import block_forward
-        return block_forward(self, hidden_states, None)
+        return block_forward(self, hidden_states, None, context if self.context_dim is not None else None)

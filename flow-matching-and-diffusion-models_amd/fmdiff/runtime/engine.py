@@ -365,6 +365,26 @@ class UNetEngine:
             ctx.tape.append(bwd)
         return o
 
+    def resample_layer(self, x: Act, ctx: Ctx, up: bool):
+        """Parameter-free resampling (fmd_resample2): AvgPoolND(kernel=stride=2) of DownsampleND(use_conv=False)
+        (src/nn/ops/upsampling.py:52-58, pooling.py:33-53) or the nearest-x2 F.interpolate of
+        UpsampleND(use_conv=False) (upsampling.py:24-29).  Output statistics are computed where a GroupNorm
+        consumes them."""
+        N, sp, C = x.t.shape[0], tuple(x.t.shape[1:-1]), x.C
+        osp = tuple(2 * v for v in sp) if up else tuple(v // 2 for v in sp)
+        scale = 1.0 if up else 1.0 / (2 ** len(sp))
+        out = torch.empty((N, *osp, C), device=x.t.device, dtype=torch.bfloat16)
+        ops.resample2(x.t, out, up, scale)
+        o = Act(out)
+        if ctx.tape is not None and x.need_grad:
+            def bwd():
+                if o.grad is None:
+                    return
+                g, acc = _gdest(x)
+                ops.resample2(o.grad, g, not up, 1.0 if up else scale, acc=bool(acc))
+            ctx.tape.append(bwd)
+        return o
+
     def _wg(self, fn):
         """Issue ``fn`` (weight-gradient work) on the side stream after everything queued so far on the
         current stream; ``fn`` (and so every tensor it references) is kept alive until ``_join``."""
@@ -872,11 +892,11 @@ class UNetEngine:
             return self.conv_layer(layer.conv, h, ctx)
         if isinstance(layer, DownsampleND):
             if not layer.use_conv:
-                raise NotImplementedError("average-pool DownsampleND is not yet on the fmdiff engine")
+                return self.resample_layer(h, ctx, up=False)
             return self.conv_layer(layer.op.conv, h, ctx, stride=2)
         if isinstance(layer, UpsampleND):
             if not layer.use_conv:
-                raise NotImplementedError("conv-less UpsampleND is not yet on the fmdiff engine")
+                return self.resample_layer(h, ctx, up=True)
             return self.conv_layer(layer.conv.conv, h, ctx, upsample=True)
         if isinstance(layer, (SpatialSelfAttention, DiffusersAttentionND)):
             return self.attention(layer, h, ctx)

@@ -710,6 +710,26 @@ def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
     return dqkv
 
 
+def _dhw(t):
+    """(N, D, H, W, C) view extents of an N(D)(H)WC tensor (missing leading spatial dims = 1)."""
+    N, C = t.shape[0], t.shape[-1]
+    sp = list(t.shape[1:-1])
+    sp = [1] * (3 - len(sp)) + sp
+    return N, sp, C
+
+
+def resample2(src, dst, up: bool, scale: float, acc: bool = False):
+    """dst (+)= avg/sum-pool-by-2 (up=False) or nearest-x2 (up=True) of src, every spatial dim resampled."""
+    _need_cuda(src, "resample2")
+    N, s_sp, C = _dhw(src)
+    _, d_sp, _ = _dhw(dst)
+    lo, hi = (s_sp, d_sp) if up else (d_sp, s_sp)
+    nd = src.dim() - 2
+    f = [1] * (3 - nd) + [2] * nd
+    _lib.call("fmd_resample2", _p(src), N, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], C, f[0], f[1], f[2], int(up),
+              float(scale), _p(dst), int(acc), stream())
+
+
 def sum_pool2(src, dst, acc):
     N, H, W, Cc = dst.shape
     _lib.call("fmd_sum_pool2", _p(src), N, H, W, Cc, _p(dst), int(acc), stream())

@@ -1,10 +1,17 @@
 """Calling a single block outside a UNet.
 
 The fused engine executes whole UNets (``fmdiff.runtime.engine``).  A lone
-``Conv`` runs through the same implicit-GEMM kernel (forward only); lone
-ResBlock / attention modules are executed by the UNet engine only.
+``Conv`` runs through the same implicit-GEMM kernel (forward only).  A lone
+``ResBlockND`` / ``SpatialSelfAttention`` / ``SpatialCrossAttention`` /
+``DiffusersAttentionND`` runs through the same engine layer methods (the fused
+HIP kernels of the UNet path) on a one-block engine, differentiable w.r.t. its
+input, its time embedding and its parameters -- the reference's block
+self-tests call the blocks this way (``src/nn/blocks/residual.py:160-215``,
+``attention.py:277-341``).
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 
@@ -43,6 +50,98 @@ def linear_forward(lin, x: torch.Tensor) -> torch.Tensor:
     return ops.linear(x.float().contiguous(), lin.weight.detach(), lin.bias.detach() if lin.bias is not None else None)
 
 
-def block_forward(block, x, emb):
-    raise NotImplementedError(f"{type(block).__name__} runs inside a UNet through fmdiff.runtime.engine; "
-                              "standalone block execution is not provided")
+def _block_engine_cls():
+    from .engine import UNetEngine, WeightCache
+
+    class BlockEngine(UNetEngine):
+        """One-block engine: the UNet engine's layer methods (res_block / attention / cross_attention) on a
+        lone block module (no grouped emb projections, no time MLP)."""
+
+        def __init__(self, block):   # UNetEngine.__init__'s UNet-model checks do not apply
+            self._model = weakref.ref(block)
+            self.kind = "block"
+            self.wc = WeightCache()
+            self._tt = None
+            self.gl, self.gl_slot = None, {}
+            self.side_stream_wgrad = False
+            self._side = None
+            self._side_keep = []
+            self._head_bwd = None
+
+    return BlockEngine
+
+
+def _block_engine(block):
+    eng = getattr(block, "_fmd_block_engine", None)
+    if eng is None:
+        eng = _block_engine_cls()(block)
+        object.__setattr__(block, "_fmd_block_engine", eng)
+    return eng
+
+
+def _run_block(eng, block, x_nhwc, emb, context, save):
+    from ..nn.blocks.attention import DiffusersAttentionND, SpatialCrossAttention, SpatialSelfAttention
+    from ..nn.blocks.residual import ResBlockND
+    from .engine import Act, Ctx
+    N = x_nhwc.shape[0]
+    e = emb.float().contiguous() if emb is not None else torch.zeros((N, 1), device=x_nhwc.device)
+    ctx = Ctx(e, save, N)
+    ctx.cca = context
+    xa = Act(x_nhwc, need_grad=save)
+    if isinstance(block, ResBlockND):
+        if block.uses_embedding and emb is None:
+            raise ValueError("ResBlockND with emb_channels needs the time embedding")
+        y = eng.res_block(block, [xa], ctx)
+    elif isinstance(block, (SpatialSelfAttention, DiffusersAttentionND)):
+        y = eng.attention(block, xa, ctx)
+    elif isinstance(block, SpatialCrossAttention):
+        y = eng.cross_attention(block, xa, ctx)
+    else:
+        raise NotImplementedError(type(block).__name__)
+    return xa, y, ctx
+
+
+class _BlockFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, x, emb, context, block, *params):
+        eng = _block_engine(block)
+        xin = ops.nchw_to_nhwc(x)
+        xa, y, ctx = _run_block(eng, block, xin, emb, context, True)
+        fctx.state = (eng, xa, y, ctx, x.shape[1], emb is not None)
+        return ops.nhwc_to_nchw(y.t, y.C)
+
+    @staticmethod
+    def backward(fctx, gout):
+        eng, xa, y, ctx, C, has_emb = fctx.state
+        fctx.state = None
+        for p in eng.m.parameters():
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        y.grad = ops.nchw_to_nhwc(gout.contiguous())
+        ops.gb_defer()
+        try:
+            for fn in reversed(ctx.tape):
+                fn()
+        finally:
+            ops.gb_flush()
+        eng._join()
+        dx = ops.nhwc_to_nchw(xa.grad, C) if xa.grad is not None else None
+        demb = ctx.demb.clone() if has_emb else None
+        return (dx, demb, None, None) + tuple(None for _ in eng.m.parameters())
+
+
+def block_forward(block, x, emb, context=None):
+    """NC(D)HW fp32 -> NC(D)HW fp32 through the fused HIP layer kernels; channels must be multiples of 8.
+    Gradients flow to ``x``, ``emb`` and the block's parameters (accumulated into ``.grad``), not to
+    ``context``."""
+    ops._need_cuda(x, type(block).__name__)
+    if x.shape[1] % 8:
+        raise NotImplementedError(f"{type(block).__name__}: standalone execution needs channels % 8 == 0")
+    ctxt = context.float().contiguous() if context is not None else None
+    params = list(block.parameters())
+    if torch.is_grad_enabled() and (x.requires_grad or (emb is not None and emb.requires_grad)
+                                    or any(p.requires_grad for p in params)):
+        return _BlockFunction.apply(x.float(), emb, ctxt, block, *params)
+    eng = _block_engine(block)
+    _, y, _ = _run_block(eng, block, ops.nchw_to_nhwc(x), emb, ctxt, False)
+    return ops.nhwc_to_nchw(y.t, y.C)

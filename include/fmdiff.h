@@ -219,6 +219,15 @@ int fmd_prep_weights_batch(const void* jobs, int32_t njobs, int32_t nblocks, fmd
 int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s);
 int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
                      fmd_stream_t s);
+/* Parameter-free resampling by 2 along the dims whose factor (fz, fy, fx) is 2, NDHWC bf16 (2-D: D = 1; 1-D:
+ * D = H = 1).  up = 0: dst[low] (+)= scale * sum of src's 2^d block -- AvgPoolND(kernel=stride=2)
+ * (src/nn/ops/pooling.py:33-53, scale 1/2^d; DownsampleND(use_conv=False), upsampling.py:52-58) and the
+ * nearest-x2 data gradient (scale 1).  up = 1: dst[high] (+)= scale * src[high >> 1] -- UpsampleND(use_conv=
+ * False)'s F.interpolate(scale_factor=2, mode="nearest") (upsampling.py:24-29, scale 1) and the avg-pool data
+ * gradient (scale 1/2^d).  High extents are 2*low or 2*low + 1 (floor pooling of an odd extent). */
+int fmd_resample2(const void* src, int32_t N, int32_t Dl, int32_t Hl, int32_t Wl, int32_t Dh, int32_t Hh, int32_t Wh,
+                  int32_t C, int32_t fz, int32_t fy, int32_t fx, int32_t up, float scale, void* dst, int32_t acc,
+                  fmd_stream_t s);
 int fmd_sum_pool2(const void* src, int32_t N, int32_t H, int32_t W, int32_t C, void* dst, int32_t acc, fmd_stream_t s);
 /* dst[n][z][y][x][c] (+)= sum of the 2x2x2 block of src (bf16 NDHWC, src 2D x 2H x 2W): the data gradient
  * of a nearest-x2 3-D upsample. */

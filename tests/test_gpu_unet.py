@@ -327,6 +327,12 @@ UNET3D_CASES = {
     "diffusers": dict(unet_impl="diffusers_nd", spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
                       block_out_channels=[32, 64], down_block_types=["DownBlock2D", "AttnDownBlock2D"],
                       up_block_types=["AttnUpBlock2D", "UpBlock2D"], sample_size=16, norm_num_groups=8),
+    # conv_resample=False: AvgPoolND DownsampleND + conv-less nearest-x2 UpsampleND (fmd_resample2), 2-D and 3-D
+    "efficient_avgpool_2d": dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64, 64],
+                                 attention_resolutions=[], conv_resample=False, sample_size=64),
+    "efficient_avgpool_3d": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
+                                 block_out_channels=[32, 64], attention_resolutions=[], conv_resample=False,
+                                 sample_size=16),
 }
 
 
