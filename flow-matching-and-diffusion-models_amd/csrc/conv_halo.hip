@@ -61,8 +61,8 @@ struct HArgs {
                           // kz, 32-channel block cb) = kz*ncb + cb, reading logical input slice z + kz - 1
                           // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
-  int ntiles;                  // v2: workgroups of the first dispatch round (those that take part in the stagger)
-  int stagger;                 // v2: s_sleep(127) rounds the second first-round workgroup of a CU waits
+  int ntiles;                  // workgroups of the first dispatch round (those that take part in the stagger)
+  int stagger;                 // s_sleep(127) rounds the second first-round workgroup of a CU waits
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
 };
@@ -110,6 +110,28 @@ struct HaloCfg {
   static constexpr int EPW = NT == 512 ? 4 : 2;
 };
 
+// per-CU arrival counters of the first-round stagger (monotonic; parity only)
+__device__ unsigned g_cu_ticket[2048];
+
+// First-round stagger: the second workgroup of each CU in the first dispatch round (blockIdx < first_round,
+// the odd ticket of a per-CU arrival counter) starts `stagger` s_sleep(127) rounds late.  Every later workgroup
+// takes the CU slot its predecessor frees, so the two slots of a CU stay out of phase and one slot's
+// prologue / epilogue (exposed loads, HBM-bound store and side-load bursts) overlaps the other's MFMAs.
+FMD_DEV void first_round_stagger(int first_round, int stagger, int* flag) {
+  if (stagger <= 0 || (int)blockIdx.x >= first_round || blockIdx.y != 0) return;
+  if (threadIdx.x == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: cu 11:8, sh 12, se 15:13
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // XCC_ID 3:0
+    const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
+    *flag = (int)(atomicAdd(&g_cu_ticket[key], 1u) & 1u);
+  }
+  __syncthreads();
+  const int late = *(volatile int*)flag;
+  __syncthreads();
+  if (late)
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
 template <bool UP, int PRO, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(HaloCfg<NT>::EPW, HaloCfg<NT>::EPW)))
 void conv3x3_halo(const HArgs A) {
@@ -136,6 +158,7 @@ void conv3x3_halo(const HArgs A) {
   const fmd_conv_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid / NWH, wpx = wid % NWH;   // 2 x NWH waves: 64 couts x WR pixel rows each
+  first_round_stagger(A.ntiles, A.stagger, (int*)(smem + SM_EPI));
   const int l16 = lane & 15, lq = lane >> 4;
   const int kc = piece_kc(tid);              // staged pieces start at multiples of 32: the channel group is fixed
 
@@ -678,7 +701,6 @@ FMD_DEV float half32_sum_to_last(float v) {
   return v;
 }
 
-__device__ unsigned g_cu_ticket[2048];   // per-CU arrival counters of the v2 stagger (monotonic; parity only)
 
 template <bool UP, int PRO>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
@@ -711,20 +733,7 @@ void conv3x3_halo_v2(const HArgs A) {
   //      odd ticket of a per-CU arrival counter) starts A.stagger s_sleep(127) rounds late.  Every later
   //      workgroup takes the CU slot its predecessor frees, so the two slots of a CU stay half a tile apart
   //      and reach their epilogues (HBM-bound store / side-load bursts) while the other slot runs MFMAs.
-  if (A.stagger > 0 && (int)blockIdx.x < A.ntiles) {
-    int* flag = (int*)(smem + SM_EPI);
-    if (tid == 0) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: cu 11:8, sh 12, se 15:13
-      const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // XCC_ID 3:0
-      const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
-      *flag = (int)(atomicAdd(&g_cu_ticket[key], 1u) & 1u);
-    }
-    __syncthreads();
-    const int late = *(volatile int*)flag;
-    __syncthreads();
-    if (late)
-      for (int i = 0; i < A.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
+  first_round_stagger(A.ntiles, A.stagger, (int*)(smem + SM_EPI));
   const int per_img = A.tiles_x * A.tiles_y;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int tco = b % A.ntc;
@@ -1178,7 +1187,7 @@ void conv3x3_halo_v2(const HArgs A) {
 
 static int g_halo_variant = 1;   // fmd_halo_set_variant: 1 = v1 (16x16x32, default), 2 = v2 (32x32x16) for GN-prologue 2-D problems
 static int g_persist = 512;      // v2: workgroups resident in the first dispatch round (2 per CU)
-static int g_stagger = 4;        // v2 stagger of a CU's second workgroup (s_sleep(127) rounds)
+static int g_stagger = 0;        // stagger of a CU's second workgroup (s_sleep(127) rounds); measured: no gain
 static int g_v2_all = 0;         // variant 3: v2 for every 2-D problem (testing)
 
 // [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
@@ -1240,12 +1249,12 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);
+  A.ntiles = g_persist;   // first dispatch round: 2 workgroups per CU (81 KB LDS each)
+  A.stagger = (A.splits == 1 && nwg > 2 * g_persist) ? g_stagger : 0;   // >= 2 full rounds: a phase to keep
   // v2 (32x32x16) wins where the staging carries the GroupNorm(+SiLU) transform (VALU-bound v1 loop); without a
   // prologue the v1 loop is not VALU-bound and its cheaper epilogue wins (tools/conv_micro.py)
   if (g_halo_variant == 2 && !d3 && (pro != 0 || g_v2_all)) {
     const dim3 blk(512);
-    A.ntiles = g_persist;   // 2 workgroups per CU (81 KB LDS each)
-    A.stagger = (A.splits == 1 && nwg > 2 * g_persist) ? g_stagger : 0;   // >= 2 full rounds: a phase to keep
     const dim3 g2(nwg, A.splits);
 #define g g2
     if (d->upsample) {

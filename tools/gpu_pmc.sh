@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 ONLY=${PMC_ONLY:-fwd,wgrad}
-timeout -k 10 120 python tools/conv_micro.py --only $ONLY --iters 20 > $OUT/plain.txt 2>&1 || exit 1
+timeout -k 10 120 python tools/conv_micro.py --only $ONLY --iters 20 --variants ${PMC_VARIANTS:-1} > $OUT/plain.txt 2>&1 || exit 1
 cat $OUT/plain.txt
 PASSES=${PMC_PASSES:-1 2 3 4}
 i=0
@@ -17,6 +17,6 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   i=$((i+1))
   case " $PASSES " in *" $i "*) ;; *) continue ;; esac
   timeout -k 10 300 rocprofv3 --pmc $pass --output-format csv -d $OUT/p$i -o run -- \
-    python tools/conv_micro.py --only $ONLY --iters 5 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+    python tools/conv_micro.py --only $ONLY --iters 20 --warm 300 --variants ${PMC_VARIANTS:-1} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   echo "pass $i ok"
 done
