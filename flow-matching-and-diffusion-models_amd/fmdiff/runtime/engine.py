@@ -665,6 +665,9 @@ class UNetEngine:
             wq, bq = m.to_q.weight, m.to_q.bias
             kvp = [(m.to_k.weight, m.to_k.bias), (m.to_v.weight, m.to_v.bias)]
             wo, bo = m.to_out[0].weight, m.to_out[0].bias
+        if any(w.shape[0] % 8 for w, _ in kvp) or inner % 8:
+            raise NotImplementedError(f"{type(m).__name__}: the fused k|v projection needs projection widths that "
+                                      f"are multiples of 8 (got {[w.shape[0] for w, _ in kvp]})")
         if len(kvp) == 1:
             wkv, bkv = kvp[0]
         else:   # to_k / to_v as one fused projection

@@ -52,3 +52,15 @@ def golden_b256():
     tensors = torch.load(os.path.join(d, "golden_b256.pt"), weights_only=True)
     meta = json.load(open(os.path.join(d, "golden_b256.json")))
     return tensors, meta
+
+
+@pytest.fixture(scope="session")
+def golden_attn():
+    """Reference SpatialCrossAttention / DiffusersAttentionND(context_dim) fixtures: make_golden_attn.py."""
+    import json
+
+    import torch
+    d = os.path.join(REPO, "tests", "golden")
+    tensors = torch.load(os.path.join(d, "golden_attn.pt"), weights_only=True)
+    meta = json.load(open(os.path.join(d, "golden_attn.json")))
+    return tensors, meta

@@ -215,3 +215,33 @@ def test_vae_module_state_dict_drop_in():
     assert list(own.keys()) == list(ref.keys())
     assert all(own[k].shape == ref[k].shape for k in own)
     vae.load_state_dict(ref)
+
+
+@pytest.mark.parametrize("name", ["spatial_cross", "diffusers_cross"])
+@pytest.mark.parametrize("layout", ["bct", "btc"])
+def test_cross_attention_blocks_vs_reference(golden_attn, name, layout):
+    """oracle cross_attention / diffusers_attention (context_norm, raw vs view/transpose head split, both
+    context layouts) vs the reference modules' own forward and autograd gradients (make_golden_attn.py)."""
+    T, M = golden_attn
+    m = M[name]
+    import oracle.unet as UU
+    from fmdiff.nn.blocks.attention import DiffusersAttentionND, SpatialCrossAttention
+    if m["kind"] == "spatial":
+        mod = SpatialCrossAttention(m["dim"], context_dim=m["context_dim"], heads=m["heads"], dim_head=m["dim_head"])
+        L = dict(prefix="p", heads=m["heads"], dim_head=m["dim_head"], linear=False, ctx=m["context_dim"])
+        fn = UU.cross_attention
+    else:
+        mod = DiffusersAttentionND(m["channels"], heads=m["heads"], context_dim=m["context_dim"],
+                                   norm_num_groups=m["norm_num_groups"])
+        L = dict(prefix="p", heads=m["heads"], groups=m["norm_num_groups"], eps=1e-5, ctx=m["context_dim"])
+        fn = UU.diffusers_attention
+    shapes = {k: tuple(v.shape) for k, v in mod.state_dict().items()}
+    sd = {f"p.{k}": v.requires_grad_() for k, v in UU.seeded_tensors(shapes, m["seed"]).items()}
+    ctx = T[f"{name}/ctx"] if layout == "bct" else T[f"{name}/ctx"].transpose(1, 2).contiguous()
+    x = T[f"{name}/x"].clone().requires_grad_()
+    y = fn(sd, L, x, ctx)
+    torch.testing.assert_close(y, T[f"{name}/{layout}/y"], rtol=1e-5, atol=1e-6)
+    y.backward(T[f"{name}/gout"])
+    torch.testing.assert_close(x.grad, T[f"{name}/{layout}/dx"], rtol=1e-4, atol=1e-5)
+    for k in m["params"]:
+        torch.testing.assert_close(sd[f"p.{k}"].grad, T[f"{name}/{layout}/grad/{k}"], rtol=1e-4, atol=1e-5)
