@@ -152,11 +152,18 @@ def out_hw(Hs, ks, stride, pad, upsample):
     return (Hin + 2 * pad - ks) // stride + 1
 
 
+# split-K of the generic implicit GEMM on small grids: >= SPLIT_MIN_STEPS k-steps per split, about
+# SPLIT_CU_MULT workgroups per CU, at most SPLIT_CAP splits (env overrides for A/B measurements)
+SPLIT_MIN_STEPS = int(os.environ.get("FMD_SPLIT_MIN_STEPS", "4"))
+SPLIT_CU_MULT = int(os.environ.get("FMD_SPLIT_CU_MULT", "2"))
+SPLIT_CAP = int(os.environ.get("FMD_SPLIT_CAP", "32"))
+
+
 def _choose_splits(M, K, nk, bpx=128, bco=128):
     tiles = -(-M // bpx) * -(-K // bco)
     if tiles >= NUM_CU or nk < 8:
         return 1
-    return max(1, min(nk // 4, -(-2 * NUM_CU // tiles), 32))
+    return max(1, min(nk // SPLIT_MIN_STEPS, -(-SPLIT_CU_MULT * NUM_CU // tiles), SPLIT_CAP))
 
 
 HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
