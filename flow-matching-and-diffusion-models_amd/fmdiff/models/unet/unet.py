@@ -12,6 +12,7 @@ from ...nn.blocks.residual import ResBlockND
 from ...nn.blocks.timestep import TimestepBlock
 from ...nn.ops.convolution import ConvND
 from ...nn.ops.normalization import make_group_norm
+from ...nn.ops.pooling import PoolND, UnPoolND
 from ...nn.ops.upsampling import DownsampleND, UpsampleND
 from ...nn.params import Identity, Linear, SiLU, zero_module
 from .base import BaseUNetND
@@ -32,8 +33,6 @@ class EfficientUNetND(BaseUNetND):
         super().__init__()
         if spatial_dims not in (1, 2, 3):
             raise ValueError("spatial_dims must be 1, 2 or 3")
-        if pool_factor > 1:
-            raise NotImplementedError("pool_factor > 1 (patchify PoolND/UnPoolND) is not on the fmdiff hot path")
         self.spatial_dims = spatial_dims
         self.in_channels = in_channels
         self.model_channels = model_channels
@@ -52,7 +51,13 @@ class EfficientUNetND(BaseUNetND):
 
         ted = model_channels * 4
         self.time_embed = nn.Sequential(Linear(model_channels, ted), SiLU(), Linear(ted, ted))
-        self.pool = Identity()
+        # optional input pooling (patchify, reference unet.py:123-129)
+        if pool_factor > 1:
+            self.pool = PoolND(spatial_dims, in_channels, model_channels, pool_factor)
+            start_channels = model_channels
+        else:
+            self.pool = Identity()
+            start_channels = in_channels
 
         def res(cin, cout=None):
             return ResBlockND(spatial_dims=spatial_dims, channels=cin, emb_channels=ted, out_channels=cout,
@@ -69,8 +74,8 @@ class EfficientUNetND(BaseUNetND):
                                                  dim_head=dim_head, use_linear=linear, use_efficient_attn=True))
             return out
 
-        self.input_blocks = nn.ModuleList([TimestepEmbedSequential(ConvND(spatial_dims, in_channels, model_channels,
-                                                                          3, padding=1))])
+        self.input_blocks = nn.ModuleList([TimestepEmbedSequential(ConvND(spatial_dims, start_channels,
+                                                                          model_channels, 3, padding=1))])
         chans = [model_channels]
         ch = model_channels
         ds = 1
@@ -103,9 +108,14 @@ class EfficientUNetND(BaseUNetND):
                     layers.append(UpsampleND(spatial_dims, ch, use_conv=conv_resample))
                     ds //= 2
                 self.output_blocks.append(TimestepEmbedSequential(*layers))
-        self.out = nn.Sequential(make_group_norm(ch, groups=32), SiLU(),
-                                 zero_module(ConvND(spatial_dims, model_channels, out_channels, 3, padding=1)))
-        self.unpool = Identity()
+        if pool_factor > 1:   # reference unet.py:280-287: the head keeps model_channels, UnPoolND projects
+            self.out = nn.Sequential(make_group_norm(ch, groups=32), SiLU(),
+                                     ConvND(spatial_dims, model_channels, model_channels, 3, padding=1))
+            self.unpool = UnPoolND(spatial_dims, model_channels, out_channels, pool_factor)
+        else:
+            self.out = nn.Sequential(make_group_norm(ch, groups=32), SiLU(),
+                                     zero_module(ConvND(spatial_dims, model_channels, out_channels, 3, padding=1)))
+            self.unpool = Identity()
 
     def _prepare_input(self, x, context, context_ca):
         if context_ca is not None and not (self.cross_attention_resolutions or self.cross_attention_in_middle):

@@ -57,6 +57,36 @@ class Conv(nn.Module):
                 f"stride={self.stride}, padding={self.padding}")
 
 
+class ConvT(nn.Module):
+    """Holds ``weight`` [in, out, *k] / ``bias`` [out] of an N-d transposed convolution (reference
+    ``nn.ConvTranspose{1,2,3}d``); executed by the UNet engine (UnPoolND)."""
+
+    def __init__(self, dims: int, in_channels: int, out_channels: int, kernel_size: SizeArg = 2,
+                 stride: SizeArg = 2, padding: SizeArg = 0, output_padding: SizeArg = 0, groups: int = 1,
+                 bias: bool = True):
+        super().__init__()
+        if groups != 1:
+            raise NotImplementedError("grouped transposed convolution is not on the fmdiff hot path")
+        self.dims = dims
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.kernel_size = _tuple(kernel_size, dims)
+        self.stride = _tuple(stride, dims)
+        self.padding = _tuple(padding, dims)
+        self.output_padding = _tuple(output_padding, dims)
+        self.weight = nn.Parameter(torch.empty(in_channels, out_channels, *self.kernel_size))
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        # torch.nn.modules.conv._ConvNd.reset_parameters (fan_in of the [in, out, *k] weight = out * prod(k))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            fan_in, _ = nn.init._calculate_fan_in_and_fan_out(self.weight)
+            bound = 1 / math.sqrt(fan_in) if fan_in > 0 else 0
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        raise NotImplementedError("ConvTranspose runs inside the UNet engine (UnPoolND of pool_factor > 1)")
+
+
 class Linear(nn.Module):
     """Holds ``weight`` [out, in] / ``bias`` (reference ``nn.Linear``)."""
 

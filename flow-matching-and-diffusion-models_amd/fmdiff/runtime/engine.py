@@ -365,6 +365,57 @@ class UNetEngine:
             ctx.tape.append(bwd)
         return o
 
+    def pool_layer(self, conv: Conv, x: Act, ctx: Ctx):
+        """PoolND (reference nn/ops/pooling.py:10-30, unet.py:124-126): conv with kernel = stride = pool_factor,
+        no padding, on the (channel-padded) model input; weight gradient only (the input is data)."""
+        pf = conv.stride[0]
+        if conv.kernel_size != (pf,) * conv.dims or conv.padding != (0,) * conv.dims:
+            raise NotImplementedError(f"PoolND geometry {conv.kernel_size}/{conv.stride}/{conv.padding}")
+        Cin = x.C
+        out, _ = ops.conv(x.t, conv.out_channels, self.wc.get(conv.weight, 0, None, Cin), ks=pf, stride=pf, pad=0,
+                          bias=conv.bias)
+        o = Act(out)
+        if ctx.tape is not None:
+            def bwd():
+                def wg():
+                    tgt = self._wgrad_target(conv, Cin)
+                    ops.wgrad(x.t, o.grad, tgt, ks=pf, stride=pf, pad=0,
+                              db=conv.bias.grad if conv.bias is not None else None)
+                    self._wgrad_finish(conv, Cin, tgt)
+                self._wg(wg)
+            ctx.tape.append(bwd)
+        return o
+
+    def unpool_layer(self, ct, hb: torch.Tensor, ctx: Ctx):
+        """UnPoolND (reference pooling.py:87-105, unet.py:280-287): ConvTranspose with kernel = stride =
+        pool_factor = the transposed gather of the conv F (hi -> lo) whose weight is ct.weight [in, out, *k],
+        to the fp32 NHWC model output with CPAD-padded channels.  Backward: dx = F(dy), dW = F's weight
+        gradient with dy in F's input role, db = channel sums of dy."""
+        pf = ct.stride[0]
+        if ct.kernel_size != (pf,) * ct.dims or ct.padding != (0,) * ct.dims or any(ct.output_padding):
+            raise NotImplementedError(f"UnPoolND geometry {ct.kernel_size}/{ct.stride}/{ct.padding}")
+        K, mc = ct.out_channels, ct.in_channels
+        Kp = max(CPAD, -(-K // 8) * 8)
+        sp_hi = tuple(pf * v for v in hb.shape[1:-1])
+        bias = self.wc.padded(ct.bias, Kp) if ct.bias is not None else None
+        out, _ = ops.conv(hb, Kp, self.wc.get(ct.weight, 1, None, Kp), ks=pf, stride=pf, pad=0, transposed=True,
+                          out_hw_=sp_hi, bias=bias, out_f32=True)
+        if ctx.tape is not None:
+            head_bwd = self._head_bwd
+
+            def bwd(dpred):
+                def wg():
+                    tmp = torch.zeros((mc, Kp, *ct.kernel_size), device=hb.device, dtype=F32)
+                    ops.wgrad(dpred, hb, tmp, ks=pf, stride=pf, pad=0, accumulate=False)
+                    ct.weight.grad.add_(tmp[:, :K])
+                    if ct.bias is not None:
+                        ct.bias.grad.add_(ops.channel_stats(dpred).slab[..., 0].sum(0)[:K])
+                self._wg(wg)
+                dh, _ = ops.conv(dpred, mc, self.wc.get(ct.weight, 0, None, Kp), ks=pf, stride=pf, pad=0)
+                head_bwd(dh)
+            self._head_bwd = bwd
+        return out
+
     def resample_layer(self, x: Act, ctx: Ctx, up: bool):
         """Parameter-free resampling (fmd_resample2): AvgPoolND(kernel=stride=2) of DownsampleND(use_conv=False)
         (src/nn/ops/upsampling.py:52-58, pooling.py:33-53) or the nearest-x2 F.interpolate of
@@ -719,15 +770,16 @@ class UNetEngine:
         ctx.tape.append(bwd)
         return y
 
-    def head(self, norm, conv: Conv, h: Act, ctx: Ctx):
-        """GroupNorm -> SiLU -> 3x3 conv to an fp32 NHWC output with CPAD channels."""
+    def head(self, norm, conv: Conv, h: Act, ctx: Ctx, bf16_out: bool = False):
+        """GroupNorm -> SiLU -> 3x3 conv to an fp32 NHWC output with CPAD channels (``bf16_out``: a bf16
+        intermediate with K channels, the input of UnPoolND when pool_factor > 1)."""
         _check_conv(conv, 3, 1, 1)
         N, Cc, sp = h.t.shape[0], h.t.shape[-1], tuple(h.t.shape[1:-1])
         HW = math.prod(sp)
         K = conv.out_channels
         Kp = max(CPAD, -(-K // 8) * 8)
         a, b, mr = ops.gn_prep(_stats(h), None, N, HW, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
-        if Kp == CPAD and len(sp) == 2 and ops.head_eligible(*sp, Cc, K):
+        if not bf16_out and Kp == CPAD and len(sp) == 2 and ops.head_eligible(*sp, Cc, K):
             # VALU head kernels (csrc/head.hip): the GN/SiLU transform once per element, no MFMA padding
             out = ops.head_fwd(h.t, (a, b), conv.weight, conv.bias, K, Kp)
             if ctx.tape is not None:
@@ -743,7 +795,7 @@ class UNetEngine:
             return out
         w = self.wc.get(conv.weight, 0, Kp, None)
         bias = self.wc.padded(conv.bias, Kp)
-        out, _ = ops.conv(h.t, Kp, w, pro=(a, b, True), bias=bias, out_f32=True)
+        out, _ = ops.conv(h.t, Kp, w, pro=(a, b, True), bias=bias, out_f32=not bf16_out)
         if ctx.tape is not None:
             def bwd(dpred):
                 def wgh():
@@ -834,6 +886,8 @@ class UNetEngine:
         if self.kind == "efficient":
             hs = []
             h = x
+            if m.pool_factor > 1:   # before the first encoder mark: its gradient lands in the last segment
+                h = self.pool_layer(m.pool.down.conv, x, ctx)
             for blk in m.input_blocks:
                 if ctx.tape is not None:
                     ctx.marks.append(len(ctx.tape))
@@ -852,7 +906,11 @@ class UNetEngine:
                 h = self.res_block(layers[0], [h, skip], ctx)
                 for layer in layers[1:]:
                     h = self._apply(layer, h, ctx)
-            out = self.head(m.out[0], m.out[2].conv, h, ctx)
+            if m.pool_factor > 1:
+                hb = self.head(m.out[0], m.out[2].conv, h, ctx, bf16_out=True)
+                out = self.unpool_layer(m.unpool.up.convT, hb, ctx)
+            else:
+                out = self.head(m.out[0], m.out[2].conv, h, ctx)
         else:
             if ctx.tape is not None:
                 ctx.marks.append(len(ctx.tape))
@@ -931,7 +989,7 @@ class UNetEngine:
         earlier one (time MLP, grouped emb projections, anything unused)."""
         m = self.m
         if self.kind == "efficient":
-            head = [[m.output_blocks, m.out], [m.middle_block]]
+            head = [[m.output_blocks, m.out, m.unpool], [m.middle_block]]
         else:
             head = [[m.up_blocks, m.conv_norm_out, m.conv_out], [m.mid_block] if m.mid_block is not None else []]
         mods = head + list(reversed(self._stage_modules()))

@@ -209,8 +209,9 @@ def efficient_unet(sd: SD, spec: dict, x, t, context=None, context_ca=None):
     emb = F.linear(feats, sd["time_embed.0.weight"], sd["time_embed.0.bias"])
     emb = F.linear(F.silu(emb), sd["time_embed.2.weight"], sd["time_embed.2.bias"])
     lay = S.efficient_layout(spec)
-    if lay["pool"] > 1:
-        raise NotImplementedError("pool_factor>1 is not on the benchmarked path")
+    pf = lay["pool"]
+    if pf > 1:   # PoolND: ConvND(kernel = stride = pool_factor, padding 0) (nn/ops/pooling.py:10-30, unet.py:124-126)
+        x = conv_nd(dims, x, sd["pool.down.conv.weight"], sd["pool.down.conv.bias"], stride=pf, padding=0)
     hs = []
     h = x
     for block in lay["inputs"]:
@@ -225,7 +226,11 @@ def efficient_unet(sd: SD, spec: dict, x, t, context=None, context_ca=None):
             h = _apply(sd, L, h, emb, context_ca, dims)
     h = F.group_norm(h, S.gn_groups(lay["out_ch"], 32), sd["out.0.weight"], sd["out.0.bias"], 1e-5)
     h = F.silu(h)
-    return conv_nd(dims, h, sd["out.2.conv.weight"], sd["out.2.conv.bias"], padding=1)
+    h = conv_nd(dims, h, sd["out.2.conv.weight"], sd["out.2.conv.bias"], padding=1)
+    if pf > 1:   # UnPoolND: ConvTransposeND(kernel = stride = pool_factor) (pooling.py:87-105, unet.py:280-287)
+        fn = {1: F.conv_transpose1d, 2: F.conv_transpose2d, 3: F.conv_transpose3d}[dims]
+        h = fn(h, sd["unpool.up.convT.weight"], sd["unpool.up.convT.bias"], stride=pf)
+    return h
 
 
 def diffusers_unet(sd: SD, spec: dict, x, t, context=None, context_ca=None):
@@ -376,8 +381,11 @@ def param_shapes(spec: dict) -> Dict[str, tuple]:
     mc = spec["model_channels"]
     ed = 4 * mc
     lay = S.efficient_layout(spec)
+    pf = lay["pool"]
     lin("time_embed.0", mc, ed)
     lin("time_embed.2", ed, ed)
+    if pf > 1:
+        conv("pool.down.conv", spec["in_channels"], mc, (pf,) * dims)
     for block in lay["inputs"]:
         for L in block:
             layer(L, ed)
@@ -387,7 +395,10 @@ def param_shapes(spec: dict) -> Dict[str, tuple]:
         for L in block:
             layer(L, ed)
     norm("out.0", lay["out_ch"])
-    conv("out.2.conv", mc, spec["out_channels"])
+    conv("out.2.conv", mc, mc if pf > 1 else spec["out_channels"])
+    if pf > 1:   # ConvTranspose weight layout [in, out, *k]
+        shapes["unpool.up.convT.weight"] = (mc, spec["out_channels"], *((pf,) * dims))
+        shapes["unpool.up.convT.bias"] = (spec["out_channels"],)
     return shapes
 
 

@@ -333,6 +333,11 @@ UNET3D_CASES = {
     "efficient_avgpool_3d": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
                                  block_out_channels=[32, 64], attention_resolutions=[], conv_resample=False,
                                  sample_size=16),
+    # pool_factor=2: PoolND patchify conv (kernel = stride = 2) in, UnPoolND transposed conv out
+    "efficient_pool2_2d": dict(in_channels=1, out_channels=1, layers_per_block=1, block_out_channels=[32, 64],
+                               attention_resolutions=[], pool_factor=2, sample_size=64),
+    "efficient_pool2_3d": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
+                               block_out_channels=[32, 64], attention_resolutions=[], pool_factor=2, sample_size=16),
 }
 
 

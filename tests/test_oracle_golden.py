@@ -1,5 +1,6 @@
 """Pin the CPU oracle against fixtures produced by the reference itself (tests/golden/make_golden.py)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -245,3 +246,18 @@ def test_cross_attention_blocks_vs_reference(golden_attn, name, layout):
     torch.testing.assert_close(x.grad, T[f"{name}/{layout}/dx"], rtol=1e-4, atol=1e-5)
     for k in m["params"]:
         torch.testing.assert_close(sd[f"p.{k}"].grad, T[f"{name}/{layout}/grad/{k}"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["pool2_2d", "pool2_3d"])
+def test_pool_factor_unet_vs_reference(name):
+    """EfficientUNetND(pool_factor=2): PoolND patchify conv + UnPoolND transposed conv (oracle) vs the
+    reference module's own forward (tests/golden/make_golden_pool.py), bit-exact."""
+    import json
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    T = torch.load(os.path.join(d, "golden_pool.pt"), weights_only=True)
+    m = json.load(open(os.path.join(d, "golden_pool.json")))[name]
+    spec = S.derive_spec(m["cfg"], None, 1)
+    sd = U.seeded_state_dict(spec, m["seed"])
+    with torch.no_grad():
+        y = U.unet_forward(sd, spec, T[f"{name}/x"], T[f"{name}/t"])
+    assert torch.equal(y, T[f"{name}/y"])
