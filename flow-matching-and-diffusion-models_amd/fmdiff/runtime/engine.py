@@ -120,6 +120,8 @@ class WeightCache:
                 e["buf"][: e["src"].numel()].copy_(e["src"].detach().reshape(-1))
             elif e["kind"] == "dpack":
                 self._dpack(e["src"], e["mode"], e["buf"])
+            elif e["kind"] == "e1d":
+                self._embed1d(e["src"], e["buf"])
             elif e["kind"] == "fused":
                 o = 0
                 for w in e["src"]:
@@ -171,7 +173,27 @@ class WeightCache:
         e = self._c.get(key)
         return e is not None and e["ver"] == src_ver and key not in self._force
 
+    @staticmethod
+    def _embed1d(w, buf):
+        """fp32 [K][C][k] weight of a 1-D conv -> [K][C][k][k] with the taps in column (k-1)/2: a 1-D signal runs
+        as an (L, 1) image, where that column is the only one that meets data (the others read zero padding)."""
+        buf.zero_()
+        buf[..., (w.shape[2] - 1) // 2].copy_(w.detach())
+
+    def embed1d(self, w: torch.Tensor) -> torch.Tensor:
+        key = (id(w), "e1d")
+        if not self._fresh(key, self._ver(w)):
+            e = self._c.get(key)
+            k = w.shape[2]
+            buf = e["buf"] if e is not None else torch.empty((*w.shape[:2], k, k), device=w.device, dtype=F32)
+            self._embed1d(w, buf)
+            self._c[key] = dict(kind="e1d", src=w, buf=buf, ver=self._ver(w))
+            self._force.discard(key)
+        return self._c[key]["buf"]
+
     def get(self, w: torch.Tensor, mode: int, Kpad=None, Cpad=None):
+        if w.dim() == 3 and w.shape[2] > 1:   # 1-D k-tap conv: its (L, 1)-image embedding
+            w = self.embed1d(w)
         key = (id(w), mode, Kpad, Cpad)
         if not self._fresh(key, self._ver(w)):
             e = self._c.get(key)
@@ -272,8 +294,8 @@ class Ctx:
 
 
 def _check_conv(c: Conv, ks, stride, pad):
-    if c.dims not in (2, 3):
-        raise NotImplementedError("fmdiff engine runs spatial_dims=2 and 3 (1-D: next)")
+    if c.dims not in (1, 2, 3):
+        raise NotImplementedError(f"spatial_dims={c.dims}")
     n = c.dims
     if c.kernel_size != (ks,) * n or c.stride != (stride,) * n or c.padding != (pad,) * n:
         raise NotImplementedError(f"unexpected conv geometry {c.kernel_size}/{c.stride}/{c.padding}")
@@ -300,6 +322,9 @@ class UNetEngine:
         self.side_stream_wgrad = False
         self._side = None
         self._side_keep = []
+        # spatial_dims = 1: signals run as (L, 1) images -- 1-D k-tap weights embedded as k x k
+        # (WeightCache.embed1d), resampling along the first dim only
+        self.dims1 = int(getattr(model, "spatial_dims", 2)) == 1
 
     @staticmethod
     def _group_emb_layers(model):
@@ -369,6 +394,8 @@ class UNetEngine:
         """PoolND (reference nn/ops/pooling.py:10-30, unet.py:124-126): conv with kernel = stride = pool_factor,
         no padding, on the (channel-padded) model input; weight gradient only (the input is data)."""
         pf = conv.stride[0]
+        if self.dims1:
+            raise NotImplementedError("pool_factor > 1 with spatial_dims=1")
         if conv.kernel_size != (pf,) * conv.dims or conv.padding != (0,) * conv.dims:
             raise NotImplementedError(f"PoolND geometry {conv.kernel_size}/{conv.stride}/{conv.padding}")
         Cin = x.C
@@ -422,17 +449,18 @@ class UNetEngine:
         UpsampleND(use_conv=False) (upsampling.py:24-29).  Output statistics are computed where a GroupNorm
         consumes them."""
         N, sp, C = x.t.shape[0], tuple(x.t.shape[1:-1]), x.C
-        osp = tuple(2 * v for v in sp) if up else tuple(v // 2 for v in sp)
-        scale = 1.0 if up else 1.0 / (2 ** len(sp))
+        fac = (2, 1) if self.dims1 else (2,) * len(sp)
+        osp = tuple(v * f for v, f in zip(sp, fac)) if up else tuple(v // f for v, f in zip(sp, fac))
+        scale = 1.0 if up else 1.0 / math.prod(fac)
         out = torch.empty((N, *osp, C), device=x.t.device, dtype=torch.bfloat16)
-        ops.resample2(x.t, out, up, scale)
+        ops.resample2(x.t, out, up, scale, factors=fac)
         o = Act(out)
         if ctx.tape is not None and x.need_grad:
             def bwd():
                 if o.grad is None:
                     return
                 g, acc = _gdest(x)
-                ops.resample2(o.grad, g, not up, 1.0 if up else scale, acc=bool(acc))
+                ops.resample2(o.grad, g, not up, 1.0 if up else scale, acc=bool(acc), factors=fac)
             ctx.tape.append(bwd)
         return o
 
@@ -880,6 +908,8 @@ class UNetEngine:
         Returns (out fp32 NHWC [N,H,W,Kpad], ctx) -- ctx carries the backward tape when ``save``."""
         m = self.m
         N = xin.shape[0]
+        if xin.dim() == 3:   # 1-D signal [N][L][C] -> an (L, 1) image
+            xin = xin.unsqueeze(2)
         ctx = self.time_mlp(t, save, N, t_scale, t_trunc)
         ctx.cca = context_ca
         x = Act(xin, need_grad=False)
@@ -958,6 +988,8 @@ class UNetEngine:
         if isinstance(layer, UpsampleND):
             if not layer.use_conv:
                 return self.resample_layer(h, ctx, up=True)
+            if self.dims1:   # nearest-x2 along the signal only, then the 3-tap conv
+                return self.conv_layer(layer.conv.conv, self.resample_layer(h, ctx, up=True), ctx)
             return self.conv_layer(layer.conv.conv, h, ctx, upsample=True)
         if isinstance(layer, (SpatialSelfAttention, DiffusersAttentionND)):
             return self.attention(layer, h, ctx)
@@ -1082,13 +1114,16 @@ class _UNetFunction(torch.autograd.Function):
         fctx.engine = engine
         fctx.ctx = ctx
         fctx.kpad = out.shape[-1]
-        return ops.nhwc_to_nchw(out, engine.m_out_channels)
+        y = ops.nhwc_to_nchw(out, engine.m_out_channels)
+        return y.squeeze(-1) if engine.dims1 else y
 
     @staticmethod
     def backward(fctx, gout):
         eng = fctx.engine
         eng.ensure_grads()
         dpred = ops.nchw_to_nhwc(gout.contiguous(), fctx.kpad)
+        if eng.dims1:
+            dpred = dpred.unsqueeze(2)
         eng.backward(fctx.ctx, dpred)
         fctx.ctx = None
         return (None, None, None, None, None) + tuple(None for _ in eng.params())
@@ -1105,4 +1140,5 @@ def unet_apply(model, x: torch.Tensor, t: torch.Tensor, context: Optional[torch.
         return _UNetFunction.apply(x, t, context, context_ca, eng, *params)
     xin = eng.stage_input(x, context)
     out, _ = eng.forward(xin, t, save=False, context_ca=context_ca)
-    return ops.nhwc_to_nchw(out, eng.m_out_channels)
+    y = ops.nhwc_to_nchw(out, eng.m_out_channels)
+    return y.squeeze(-1) if eng.dims1 else y

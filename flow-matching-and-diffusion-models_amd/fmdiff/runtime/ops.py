@@ -370,7 +370,19 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
           splits=None, dy_offset=0, force_generic=False):
     """dW (+)= conv weight gradient in the reference [K][C][kh][kw] fp32 layout (and db).
 
-    ``dy_offset``: use channels [dy_offset, dy_offset + dw.shape[0]) of a wider dY (fused q/k/v)."""
+    ``dy_offset``: use channels [dy_offset, dy_offset + dw.shape[0]) of a wider dY (fused q/k/v).
+    A 1-D k-tap weight ([K][C][k], k > 1) on (L, 1)-image activations: the k x k gradient of its embedding
+    is computed and its centre column (the only one that meets data) is added in."""
+    if dw.dim() == 3 and dw.shape[2] > 1 and src0.dim() == 4:
+        full = torch.zeros((*dw.shape[:2], ks, ks), device=dw.device, dtype=F32)
+        wgrad(src0, dy, full, src1=src1, ks=ks, stride=stride, pad=pad, upsample=upsample, pro=pro, db=db,
+              accumulate=accumulate, splits=splits, dy_offset=dy_offset, force_generic=force_generic)
+        col = full[..., (ks - 1) // 2]
+        if accumulate:
+            dw.add_(col)
+        else:
+            dw.copy_(col)
+        return
     d3 = src0.dim() == 5
     if d3:
         N, Ds, Hs, Ws, C0 = src0.shape
@@ -725,14 +737,15 @@ def _dhw(t):
     return N, sp, C
 
 
-def resample2(src, dst, up: bool, scale: float, acc: bool = False):
-    """dst (+)= avg/sum-pool-by-2 (up=False) or nearest-x2 (up=True) of src, every spatial dim resampled."""
+def resample2(src, dst, up: bool, scale: float, acc: bool = False, factors=None):
+    """dst (+)= avg/sum-pool-by-2 (up=False) or nearest-x2 (up=True) of src; ``factors`` (per spatial dim, 1 or
+    2; default every dim 2) -- a 1-D signal as an (L, 1) image resamples its first dim only."""
     _need_cuda(src, "resample2")
     N, s_sp, C = _dhw(src)
     _, d_sp, _ = _dhw(dst)
     lo, hi = (s_sp, d_sp) if up else (d_sp, s_sp)
     nd = src.dim() - 2
-    f = [1] * (3 - nd) + [2] * nd
+    f = [1] * (3 - nd) + (list(factors) if factors is not None else [2] * nd)
     _lib.call("fmd_resample2", _p(src), N, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], C, f[0], f[1], f[2], int(up),
               float(scale), _p(dst), int(acc), stream())
 

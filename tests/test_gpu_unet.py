@@ -338,6 +338,15 @@ UNET3D_CASES = {
                                attention_resolutions=[], pool_factor=2, sample_size=64),
     "efficient_pool2_3d": dict(spatial_dims=3, in_channels=1, out_channels=1, layers_per_block=1,
                                block_out_channels=[32, 64], attention_resolutions=[], pool_factor=2, sample_size=16),
+    # spatial_dims=1: signals [N][C][L] run as (L, 1) images, 3-tap kernels embedded as 3x3 (centre column)
+    "efficient_1d": dict(spatial_dims=1, in_channels=1, out_channels=1, layers_per_block=1,
+                         block_out_channels=[32, 64], attention_resolutions=[2], sample_size=128),
+    "efficient_avgpool_1d": dict(spatial_dims=1, in_channels=1, out_channels=1, layers_per_block=1,
+                                 block_out_channels=[32, 64, 64], attention_resolutions=[], conv_resample=False,
+                                 sample_size=128),
+    "diffusers_1d": dict(unet_impl="diffusers_nd", spatial_dims=1, in_channels=1, out_channels=1, layers_per_block=1,
+                         block_out_channels=[32, 64], down_block_types=["DownBlock2D", "AttnDownBlock2D"],
+                         up_block_types=["AttnUpBlock2D", "UpBlock2D"], sample_size=128, norm_num_groups=8),
 }
 
 
@@ -359,7 +368,7 @@ def test_unet3d_forward_and_train_gradients_vs_oracle(impl):
     model.load_state_dict(sd)
     g = torch.Generator().manual_seed(5)
     S3 = cfg.get("sample_size", 16)
-    shape = (2, 1, 64, 64) if cfg.get("spatial_dims", 2) == 2 else (2, 1, S3, S3, S3)
+    shape = {1: (2, 1, S3), 2: (2, 1, 64, 64), 3: (2, 1, S3, S3, S3)}[cfg.get("spatial_dims", 2)]
     clean, ldct, noise = (torch.randn(*shape, generator=g) for _ in range(3))
     t = torch.rand(2, generator=g)
     Ntr = 1000
