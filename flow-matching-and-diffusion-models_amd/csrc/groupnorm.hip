@@ -421,6 +421,72 @@ extern "C" int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int3
 }
 
 // ---------------------------------------------------------------------------------------------
+// ResBlockND's out_layers dropout (src/nn/blocks/residual.py:117, nn.Dropout between SiLU and conv2):
+// y = x * keep / (1 - p) over the materialised SiLU(GN(h)) operand of conv2, keep = (hash >= p * 2^32) of
+// (seed, salt, element index) -- counter-based, so the backward regenerates the forward's mask instead of
+// storing it.  seed is read from device memory (a per-forward counter: one hipGraph replay = one fresh
+// mask); salt distinguishes the blocks.  With ep_x the same launch is the backward through dropout and the
+// SiLU of the GroupNorm prologue: dz = dy * keep / (1 - p) * silu'(a[n][c] * ep_x + b[n][c]).
+namespace {
+
+FMD_HD unsigned int fmd_mix32(unsigned int x) {   // "lowbias32" integer finaliser
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ void dropout_apply_kernel(const bf16r* x, int C, long long M, int HW, unsigned int thr,
+                                     float scale, const int* __restrict__ seed, unsigned int salt,
+                                     const bf16r* __restrict__ ep_x, const float* __restrict__ a,
+                                     const float* __restrict__ b, bf16r* y) {   // y may alias x
+  const unsigned int key = fmd_mix32((unsigned int)seed[0] * 0x9e3779b9u + salt);
+  const int CH = C / 8;
+  const long long total = M * CH;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long p = i / CH;
+    const int c = (int)(i - p * CH) * 8;
+    const unsigned int e0 = (unsigned int)(p * C + c);     // flat NHWC element index (< 2^32, checked on the host)
+    const u32x4 v = *(const u32x4*)(x + p * C + c);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = fmd_mix32(key ^ (e0 + e)) >= thr ? scale : 0.f;
+    if (ep_x) {
+      const int n = (int)(p / HW);
+      const u32x4 h = *(const u32x4*)(ep_x + p * C + c);
+      const float* pa = a + (size_t)n * C + c;
+      const float* pb = b + (size_t)n * C + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        m[2 * e] *= silu_grad(bf_lo(h[e]) * pa[2 * e] + pb[2 * e]);
+        m[2 * e + 1] *= silu_grad(bf_hi(h[e]) * pa[2 * e + 1] + pb[2 * e + 1]);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(bf_lo(v[e]) * m[2 * e], bf_hi(v[e]) * m[2 * e + 1]);
+    *(u32x4*)(y + p * C + c) = o;
+  }
+}
+
+}  // namespace
+
+extern "C" int fmd_dropout_apply(const void* x, int32_t C, int64_t M, int32_t HW, float p, const int32_t* seed,
+                                 uint32_t salt, const void* ep_x, const float* ep_a, const float* ep_b, void* y,
+                                 fmd_stream_t s) {
+  if ((C % 8) || !seed || !(p >= 0.f && p < 1.f) || (ep_x && (!ep_a || !ep_b)) || HW < 1) return -1;
+  if (M * (long long)C >= (1LL << 32)) return -2;
+  const unsigned int thr = (unsigned int)fmin((double)p * 4294967296.0, 4294967295.0);
+  const long long work = M * (long long)(C / 8);
+  hipLaunchKernelGGL(dropout_apply_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)s, (const bf16r*)x, C,
+                     (long long)M, HW, thr, 1.f / (1.f - p), (const int*)seed, salt, (const bf16r*)ep_x, ep_a, ep_b,
+                     (bf16r*)y);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // SpatialCrossAttention's context_norm (src/nn/blocks/attention.py:150-151, :177): GroupNorm over the
 // flattened context (few channels: the 4-channel VAE latent of configs/LDCT/PixelAttention) straight from
 // its fp32 (N, C, Tc) channel-major or (N, Tc, C) token-major layout into the token-major bf16

@@ -15,6 +15,7 @@ p = C.c_void_p
 i32 = C.c_int32
 i64 = C.c_int64
 f32 = C.c_float
+u32 = C.c_uint32
 
 
 class ConvDesc(C.Structure):
@@ -79,6 +80,7 @@ SIGNATURES = {
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
+    "fmd_dropout_apply": [p, i32, i64, i32, f32, p, u32, p, p, p, p, p],
     "fmd_gn_gb_fold": [p, i32, p],
     "fmd_lincomb": [C.POINTER(LincombDesc), p],
     "fmd_halo_set_workgroup": [i32],

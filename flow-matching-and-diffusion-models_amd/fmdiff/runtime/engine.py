@@ -279,7 +279,7 @@ class WeightCache:
 
 
 class Ctx:
-    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark", "cca", "marks")
+    __slots__ = ("emb", "demb", "tape", "N", "eo_all", "demb_all", "mark", "cca", "marks", "drop_seeded")
 
     def __init__(self, emb, save, N):
         self.emb = emb
@@ -291,6 +291,7 @@ class Ctx:
         self.mark = 0           # tape length when the decoder started (backward part 1 = tape[mark:])
         self.marks: List[int] = []   # tape length before each encoder stage (backward segments, see seg_ranges)
         self.cca = None         # cross-attention context (context_ca), fp32 as passed to the model
+        self.drop_seeded = False   # this forward has advanced the dropout seed counter
 
 
 def _check_conv(c: Conv, ks, stride, pad):
@@ -534,8 +535,9 @@ class UNetEngine:
         H, W = sp[-2], sp[-1]
         if Cin != m.channels:
             raise ValueError(f"ResBlockND expects {m.channels} channels, got {Cin}")
-        if m.dropout and m.training:
-            raise NotImplementedError("dropout > 0 in training is not on the fmdiff engine")
+        drop = float(m.dropout) if (m.dropout and m.training) else 0.0
+        if drop:
+            seed, salt = self._dropout_seed(m, ctx, x0.t.device)
         c1, c2 = m.conv1.conv, m.conv2.conv
         _check_conv(c1, 3, 1, 1)
         _check_conv(c2, 3, 1, 1)
@@ -578,7 +580,7 @@ class UNetEngine:
         else:
             _check_conv(sk.conv, 1, 1, 0)
         halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
-        mat2 = _materialise(halo2, None, Cout, HW)
+        mat2 = _materialise(halo2, None, Cout, HW) or bool(drop)   # dropout acts on the materialised operand
         if mat2 and not halo2:
             halo2 = self._halo_ok(N, sp, Cout, Cout)
         if not isinstance(sk, Identity):
@@ -586,6 +588,8 @@ class UNetEngine:
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
         w2, w2t = self._wts(c2.weight, 0, halo2)
         t2 = ops.gn_apply_fwd(h, None, a2, b2) if mat2 else None
+        if drop:
+            ops.dropout_apply(t2, drop, seed, salt, out=t2)
         out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
                             bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
         o = Act(out, ost)
@@ -606,7 +610,12 @@ class UNetEngine:
             self._wg(wg2)
             # the skip data gradient (non-identity) is fused into the GroupNorm-1 backward below
             extra = dy if isinstance(sk, Identity) else None
-            dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, sp, ep=(h, None, a2, b2), want_stats=True)
+            if drop:   # d(conv2 input) -> through the regenerated mask and SiLU'(GN) -> GN backward statistics
+                dd, _ = self.dgrad3x3(c2.weight, dy, Cout, sp)
+                dz2 = ops.dropout_apply(dd, drop, seed, salt, ep=(h, a2, b2), out=dd)
+                s2 = ops.channel_stats(dz2, y=(h, None, Cout))
+            else:
+                dz2, s2 = self.dgrad3x3(c2.weight, dy, Cout, sp, ep=(h, None, a2, b2), want_stats=True)
             if slot is not None:
                 demb, ds_ = ctx.demb_all[:, slot[0]:slot[0] + slot[1]], self.gl.total
             elif eo is not None:
@@ -648,6 +657,19 @@ class UNetEngine:
                                in_silu=m.emb_activation_before_proj)
         ctx.tape.append(bwd)
         return o
+
+    def _dropout_seed(self, m, ctx: Ctx, dev):
+        """(device seed counter, per-block salt) for ResBlockND dropout; the counter advances once per forward
+        (a device-side add, so every replay of a captured step draws fresh masks) and the backward reuses the
+        forward's value to regenerate its masks."""
+        st = getattr(self, "_drop_state", None)
+        if st is None:
+            st = self._drop_state = (torch.zeros(1, device=dev, dtype=torch.int32), {})
+        seed, salts = st
+        if not ctx.drop_seeded:
+            ops.counter_add(seed, 1)
+            ctx.drop_seeded = True
+        return seed, salts.setdefault(id(m), len(salts) + 1)
 
     def attention(self, m, x: Act, ctx: Ctx):
         """SpatialSelfAttention (raw reshape) or DiffusersAttentionND (self-attention only)."""

@@ -118,6 +118,20 @@ def gn_apply_fwd(x0, x1, a, b, silu=True):
     return t
 
 
+def dropout_apply(x, p: float, seed: torch.Tensor, salt: int, ep=None, out=None):
+    """y = x * keep / (1 - p) over NHWC bf16 ``x``, keep regenerated from (seed[0], salt, element index)
+    (fmd_dropout_apply); ``ep=(h, a, b)``: the backward through the dropout and the GN+SiLU prologue,
+    y = x * keep / (1 - p) * silu'(a * h + b).  ``out`` may be ``x`` (in place)."""
+    _need_cuda(x, "dropout")
+    N, Cc = x.shape[0], x.shape[-1]
+    HW = x[0, ..., 0].numel()
+    y = torch.empty_like(x) if out is None else out
+    h, a, b = ep if ep is not None else (None, None, None)
+    _lib.call("fmd_dropout_apply", _p(x), Cc, N * HW, HW, float(p), _p(seed), int(salt) & 0xffffffff, _p(h), _p(a),
+              _p(b), _p(y), stream())
+    return y
+
+
 def gn_bwd_apply(dz, x0, x1, P, Q, R, extra, dx0, acc0, dx1=None, acc1=0):
     N = dz.shape[0]
     HW = dz[0, ..., 0].numel()                    # any spatial rank (N, *sp, C)

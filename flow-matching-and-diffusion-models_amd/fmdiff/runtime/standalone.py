@@ -67,6 +67,7 @@ def _block_engine_cls():
             self._side = None
             self._side_keep = []
             self._head_bwd = None
+            self.dims1 = False
 
     return BlockEngine
 
@@ -105,19 +106,20 @@ class _BlockFunction(torch.autograd.Function):
     @staticmethod
     def forward(fctx, x, emb, context, block, *params):
         eng = _block_engine(block)
-        xin = ops.nchw_to_nhwc(x)
+        xin = ops.nchw_to_nhwc(x.unsqueeze(-1) if x.dim() == 3 else x)   # 1-D signal: an (L, 1) image
         xa, y, ctx = _run_block(eng, block, xin, emb, context, True)
-        fctx.state = (eng, xa, y, ctx, x.shape[1], emb is not None)
-        return ops.nhwc_to_nchw(y.t, y.C)
+        fctx.state = (eng, xa, y, ctx, x.shape[1], emb is not None, x.dim() == 3)
+        out = ops.nhwc_to_nchw(y.t, y.C)
+        return out.squeeze(-1) if x.dim() == 3 else out
 
     @staticmethod
     def backward(fctx, gout):
-        eng, xa, y, ctx, C, has_emb = fctx.state
+        eng, xa, y, ctx, C, has_emb, d1 = fctx.state
         fctx.state = None
         for p in eng.m.parameters():
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        y.grad = ops.nchw_to_nhwc(gout.contiguous())
+        y.grad = ops.nchw_to_nhwc(gout.contiguous().unsqueeze(-1) if d1 else gout.contiguous())
         ops.gb_defer()
         try:
             for fn in reversed(ctx.tape):
@@ -126,6 +128,8 @@ class _BlockFunction(torch.autograd.Function):
             ops.gb_flush()
         eng._join()
         dx = ops.nhwc_to_nchw(xa.grad, C) if xa.grad is not None else None
+        if d1 and dx is not None:
+            dx = dx.squeeze(-1)
         demb = ctx.demb.clone() if has_emb else None
         return (dx, demb, None, None) + tuple(None for _ in eng.m.parameters())
 
@@ -143,5 +147,6 @@ def block_forward(block, x, emb, context=None):
                                     or any(p.requires_grad for p in params)):
         return _BlockFunction.apply(x.float(), emb, ctxt, block, *params)
     eng = _block_engine(block)
-    _, y, _ = _run_block(eng, block, ops.nchw_to_nhwc(x), emb, ctxt, False)
-    return ops.nhwc_to_nchw(y.t, y.C)
+    _, y, _ = _run_block(eng, block, ops.nchw_to_nhwc(x.unsqueeze(-1) if x.dim() == 3 else x), emb, ctxt, False)
+    out = ops.nhwc_to_nchw(y.t, y.C)
+    return out.squeeze(-1) if x.dim() == 3 else out

@@ -196,6 +196,13 @@ int fmd_gn_gb_fold(const fmd_gb_job* jobs, int32_t njobs, fmd_stream_t s);
  * prologue materialised once for its consumers. */
 int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,
                      const float* a, const float* b, int32_t silu, void* t, fmd_stream_t s);
+
+/* ResBlockND dropout (replaces nn.Dropout in out_layers, src/nn/blocks/residual.py:117): y = x * keep / (1-p)
+ * over NHWC bf16 [M pixels][C], keep = hash(seed[0], salt, element index) >= p * 2^32 (regenerated, not
+ * stored).  With ep_x (bf16 [M][C]) and ep_a/ep_b ([N][C] fp32, N = M / HW) it is the backward through the
+ * dropout and the GN+SiLU prologue: y = x * keep / (1-p) * silu'(ep_a * ep_x + ep_b).  x == y is allowed. */
+int fmd_dropout_apply(const void* x, int32_t C, int64_t M, int32_t HW, float p, const int32_t* seed, uint32_t salt,
+                      const void* ep_x, const float* ep_a, const float* ep_b, void* y, fmd_stream_t s);
 int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M,
                      int32_t HW, const float* P, const float* Q, const float* R, const void* extra,
                      void* dx0, int32_t acc0, void* dx1, int32_t acc1, fmd_stream_t s);

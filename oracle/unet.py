@@ -49,8 +49,10 @@ def normalize_timesteps(t, x):
     return t.expand(x.shape[0])
 
 
-def resblock(sd: SD, L: dict, x, emb, dims):
-    """``ResBlockND.forward`` (``nn/blocks/residual.py:84-120``)."""
+def resblock(sd: SD, L: dict, x, emb, dims, drop=None):
+    """``ResBlockND.forward`` (``nn/blocks/residual.py:84-120``).  ``drop=(p, keep)``: the out_layers
+    nn.Dropout (``residual.py:117``) in training mode with a given keep mask (NC(D)HW bool) --
+    F.dropout's h * keep / (1 - p)."""
     p = L["prefix"]
     g1 = S.gn_groups(L["cin"], L["groups"])
     g2 = S.gn_groups(L["cout"], L["groups"])
@@ -68,6 +70,8 @@ def resblock(sd: SD, L: dict, x, emb, dims):
     if L["scale_shift"]:
         h = h * (1 + scale) + shift
     h = F.silu(h)
+    if drop is not None:
+        h = h * drop[1].to(h.dtype) / (1.0 - drop[0])
     h = conv_nd(dims, h, sd[f"{p}.conv2.conv.weight"], sd[f"{p}.conv2.conv.bias"], padding=1)
     if L["cin"] == L["cout"]:
         skip = x
