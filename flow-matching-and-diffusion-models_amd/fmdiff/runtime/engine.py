@@ -325,7 +325,7 @@ class UNetEngine:
         self._side_keep = []
         # spatial_dims = 1: signals run as (L, 1) images -- 1-D k-tap weights embedded as k x k
         # (WeightCache.embed1d), resampling along the first dim only
-        self.dims1 = int(getattr(model, "spatial_dims", 2)) == 1
+        self.dims1 = next(c for c in model.modules() if isinstance(c, Conv)).dims == 1
 
     @staticmethod
     def _group_emb_layers(model):
