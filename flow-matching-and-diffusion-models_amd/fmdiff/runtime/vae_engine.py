@@ -35,6 +35,8 @@ class VAEEngine(UNetEngine):
         self._side_keep = []
         self._fold = None
         self._fold_key = None
+        self._head_bwd = None
+        self.dims1 = False   # the VAE engine runs 2-D models only (spatial_dims checked on entry)
 
     def _ctx(self, part, N, dev):
         emb = None
