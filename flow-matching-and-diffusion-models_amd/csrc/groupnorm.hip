@@ -411,6 +411,110 @@ extern "C" int fmd_gn_bwd_apply(const void* dz, const void* x0, const void* x1, 
   return (int)hipGetLastError();
 }
 
+// Small levels (HW * C/G <= 16384 elements per group): the whole GroupNorm forward of one
+// (n, group) in one workgroup straight from the activation -- statistics (fp32 per thread, fp64 across
+// threads, the same E[x^2] - mean^2 form as gn_prep_kernel), the folded a/b (and mean/rstd for the
+// backward), and the materialised t = SiLU(a*x + b) over the x0|x1 channel concat.  Replaces
+// channel_stats + gn_prep + gn_apply_fwd (three launches) on the generic-conv levels, where each of
+// them costs the ~5 us launch floor.  Elements are 4-channel units (8 bytes, C0 % 4 == 0), held in
+// registers between the two passes.
+namespace {
+constexpr int GN_FUSED_UNITS = 16;   // units per thread (256 threads: 4096 units = 16384 elements)
+__global__ __launch_bounds__(256) void gn_fused_apply_kernel(
+    const bf16r* __restrict__ x0, const bf16r* __restrict__ x1, int C0, int C1, int HW, int G, float eps,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ emb,
+    int emb_stride, int emb_mode, int silu, float* __restrict__ a, float* __restrict__ b,
+    float* __restrict__ mr, bf16r* __restrict__ t) {
+  const int n = blockIdx.x / G, g = blockIdx.x - (blockIdx.x / G) * G;
+  const int C = C0 + C1;
+  const int Cg = C / G, Q = Cg / 4;                  // 4-channel units per pixel of the group
+  const int U = HW * Q;
+  const int tid = threadIdx.x;
+  const int cq = tid % Q;                            // 256 % Q == 0: a thread's units share one channel quad
+  const int c = g * Cg + cq * 4;
+  const bool s0 = c < C0;
+  const bf16r* src = s0 ? x0 + c : x1 + (c - C0);
+  const int ld = s0 ? C0 : C1;
+  const size_t pix0 = (size_t)n * HW;
+  uint2 v[GN_FUSED_UNITS];
+  float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < GN_FUSED_UNITS; ++k) {
+    const int u = tid + 256 * k;
+    v[k] = make_uint2(0u, 0u);
+    if (u < U) {
+      v[k] = *(const uint2*)(src + (pix0 + u / Q) * ld);
+      const float e0 = bf_lo(v[k].x), e1 = bf_hi(v[k].x), e2 = bf_lo(v[k].y), e3 = bf_hi(v[k].y);
+      f1 += (e0 + e1) + (e2 + e3);
+      f2 += (e0 * e0 + e1 * e1) + (e2 * e2 + e3 * e3);
+    }
+  }
+  double s1 = f1, s2 = f2;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  __shared__ double r1[4], r2[4];
+  if ((tid & 63) == 0) { r1[tid >> 6] = s1; r2[tid >> 6] = s2; }
+  __syncthreads();
+  const double t1 = (r1[0] + r1[1]) + (r1[2] + r1[3]), t2 = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+  const double cnt = (double)Cg * HW;
+  const double mean = t1 / cnt;
+  double var = t2 / cnt - mean * mean;
+  if (var < 0) var = 0;
+  const float meanf = (float)mean;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (tid == 0 && mr) { mr[((size_t)n * G + g) * 2] = meanf; mr[((size_t)n * G + g) * 2 + 1] = rstd; }
+  float av[4], bv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ce = c + e;
+    const float gm = gamma ? gamma[ce] : 1.f, bt = beta ? beta[ce] : 0.f;
+    av[e] = rstd * gm;
+    bv[e] = bt - meanf * av[e];
+    if (emb_mode == 1) {
+      const float sc = 1.f + emb[(size_t)n * emb_stride + ce];
+      const float sh = emb[(size_t)n * emb_stride + C + ce];
+      av[e] *= sc;
+      bv[e] = bv[e] * sc + sh;
+    }
+  }
+  if (tid < Q) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[(size_t)n * C + c + e] = av[e];
+      b[(size_t)n * C + c + e] = bv[e];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GN_FUSED_UNITS; ++k) {
+    const int u = tid + 256 * k;
+    if (u < U) {
+      float y0 = bf_lo(v[k].x) * av[0] + bv[0], y1 = bf_hi(v[k].x) * av[1] + bv[1];
+      float y2 = bf_lo(v[k].y) * av[2] + bv[2], y3 = bf_hi(v[k].y) * av[3] + bv[3];
+      if (silu) { y0 = siluf_(y0); y1 = siluf_(y1); y2 = siluf_(y2); y3 = siluf_(y3); }
+      *(uint2*)(t + (pix0 + u / Q) * C + c) = make_uint2(pack2(y0, y1), pack2(y2, y3));
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int fmd_gn_fused_apply(const void* x0, const void* x1, int32_t C0, int32_t C1, int32_t N, int32_t HW,
+                                  int32_t G, float eps, const float* gamma, const float* beta, const float* emb,
+                                  int32_t emb_stride, int32_t emb_mode, int32_t silu, float* a, float* b,
+                                  float* mean_rstd, void* t, fmd_stream_t s) {
+  const int C = C0 + C1;
+  if (G < 1 || C % G || (C / G) % 4 || (C0 % 4) || (C1 && !x1) || (emb_mode == 1 && !emb)) return -1;
+  const int Q = C / G / 4;
+  if (256 % Q || (long long)HW * Q > 256LL * GN_FUSED_UNITS) return -2;
+  hipLaunchKernelGGL(gn_fused_apply_kernel, dim3(N * G), dim3(256), 0, (hipStream_t)s, (const bf16r*)x0,
+                     (const bf16r*)x1, C0, C1, HW, G, eps, gamma, beta, emb, emb_stride, emb_mode, silu, a, b,
+                     mean_rstd, (bf16r*)t);
+  return (int)hipGetLastError();
+}
+
 extern "C" int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,
                                 const float* a, const float* b, int32_t silu, void* t, fmd_stream_t s) {
   if ((C0 % 8) || (C1 % 8) || (C1 && !x1)) return -1;

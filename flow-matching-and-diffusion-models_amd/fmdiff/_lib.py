@@ -80,6 +80,7 @@ SIGNATURES = {
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],
+    "fmd_gn_fused_apply": [p, p, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, i32, p, p, p, p, p],
     "fmd_dropout_apply": [p, i32, i64, i32, f32, p, u32, p, p, p, p, p],
     "fmd_gn_gb_fold": [p, i32, p],
     "fmd_lincomb": [C.POINTER(LincombDesc), p],

@@ -320,7 +320,11 @@ class UNetEngine:
         # data-gradient chain (they are off its critical path until the optimizer step).  Off by default:
         # measured on MI355X the halo wgrad/dgrad kernels then contend for LDS and the step does not
         # get faster (28.9 vs 28.8 ms).
-        self.side_stream_wgrad = False
+        # FMD_SIDE_WGRAD: unset / 0 off, 1 every weight gradient, N > 1 only problems of <= N output pixels
+        # (the small levels, where both chains are launch-latency bound)
+        side = int(os.environ.get("FMD_SIDE_WGRAD", "0") or 0)
+        self.side_stream_wgrad = side > 0
+        self.side_px_max = side if side > 1 else None
         self._side = None
         self._side_keep = []
         # spatial_dims = 1: signals run as (L, 1) images -- 1-D k-tap weights embedded as k x k
@@ -373,7 +377,7 @@ class UNetEngine:
                     ops.wgrad(x.t, dy, tgt, ks=3, stride=stride, pad=1, upsample=upsample,
                               db=conv.bias.grad if conv.bias is not None else None)
                     self._wgrad_finish(conv, Cin, tgt)
-                self._wg(wg)
+                self._wg(wg, dy.numel() // dy.shape[-1])
                 if not x.need_grad:
                     return
                 g, acc = _gdest(x)
@@ -465,10 +469,11 @@ class UNetEngine:
             ctx.tape.append(bwd)
         return o
 
-    def _wg(self, fn):
+    def _wg(self, fn, px=None):
         """Issue ``fn`` (weight-gradient work) on the side stream after everything queued so far on the
-        current stream; ``fn`` (and so every tensor it references) is kept alive until ``_join``."""
-        if not self.side_stream_wgrad:
+        current stream; ``fn`` (and so every tensor it references) is kept alive until ``_join``.  ``px``:
+        output pixels of the problem (``side_px_max`` keeps larger ones on the current stream)."""
+        if not self.side_stream_wgrad or (self.side_px_max is not None and (px is None or px > self.side_px_max)):
             fn()
             return
         main = torch.cuda.current_stream()
@@ -554,19 +559,33 @@ class UNetEngine:
             es = eo.shape[1]
         else:   # the embedding projection feeds nothing (or the block has none: VAE ResBlocks)
             eo, es = None, 0
-        a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight, g1.bias)
         halo1 = self._halo_ok(N, sp, Cout, Cin, pro=True)
         mat1 = _materialise(halo1, x1, Cin, HW)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
             halo1 = self._halo_ok(N, sp, Cout, Cin)
         w1, w1t = self._wts(c1.weight, 0, halo1)
-        t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
+        if mat1 and ops.gn_fused_eligible(HW, Cin, C0, g1.num_groups):
+            # small level: statistics, affine and the materialised prologue in one launch from x0|x1
+            a1, b1, mr1, t1 = ops.gn_fused_apply(x0.t, x1.t if x1 else None, g1.num_groups, g1.eps, g1.weight,
+                                                 g1.bias)
+        else:
+            a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight,
+                                      g1.bias)
+            t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
+        halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
+        mat2 = _materialise(halo2, None, Cout, HW) or bool(drop)   # dropout acts on the materialised operand
+        fuse2 = mat2 and ops.gn_fused_eligible(HW, Cout, Cout, g2.num_groups)
         src1 = x1.t if (x1 is not None and t1 is None) else None
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
-                          bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=True,
+                          bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=add or not fuse2,
                           wgt_tiled=w1t)
-        if ss:
+        t2 = None
+        if fuse2:
+            a2, b2, mr2, t2 = ops.gn_fused_apply(h, None, g2.num_groups, g2.eps, g2.weight, g2.bias,
+                                                 emb=eo if ss else None, emb_stride=es if ss else 0,
+                                                 emb_mode=1 if ss else 0)
+        elif ss:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
                                       emb_stride=es, emb_mode=1)
         else:
@@ -579,15 +598,14 @@ class UNetEngine:
             kw["resid"] = x0.t
         else:
             _check_conv(sk.conv, 1, 1, 0)
-        halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
-        mat2 = _materialise(halo2, None, Cout, HW) or bool(drop)   # dropout acts on the materialised operand
         if mat2 and not halo2:
             halo2 = self._halo_ok(N, sp, Cout, Cout)
         if not isinstance(sk, Identity):
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
         w2, w2t = self._wts(c2.weight, 0, halo2)
-        t2 = ops.gn_apply_fwd(h, None, a2, b2) if mat2 else None
+        if mat2 and t2 is None:
+            t2 = ops.gn_apply_fwd(h, None, a2, b2)
         if drop:
             ops.dropout_apply(t2, drop, seed, salt, out=t2)
         out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
@@ -607,7 +625,7 @@ class UNetEngine:
                 if not isinstance(sk, Identity):
                     ops.wgrad(x0.t, dy, sk.conv.weight.grad, src1=x1.t if x1 else None, ks=1, pad=0,
                               db=sk.conv.bias.grad)
-            self._wg(wg2)
+            self._wg(wg2, N * HW)
             # the skip data gradient (non-identity) is fused into the GroupNorm-1 backward below
             extra = dy if isinstance(sk, Identity) else None
             if drop:   # d(conv2 input) -> through the regenerated mask and SiLU'(GN) -> GN backward statistics
@@ -637,10 +655,10 @@ class UNetEngine:
             ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
             del dz2
             if t1 is not None:
-                self._wg(lambda: ops.wgrad(t1, dh, c1.weight.grad, db=c1.bias.grad))
+                self._wg(lambda: ops.wgrad(t1, dh, c1.weight.grad, db=c1.bias.grad), N * HW)
             else:
                 self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
-                                           db=c1.bias.grad))
+                                           db=c1.bias.grad), N * HW)
             dz1, s1 = self.dgrad3x3(c1.weight, dh, Cin, sp, ep=(x0.t, x1.t if x1 else None, a1, b1),
                                     want_stats=True)
             P1, Q1, R1 = ops.gn_bwd_prep(s1, N, HW, Cin, g1.num_groups, mr1, g1.weight, g1.bias, g1.weight.grad,

@@ -118,6 +118,33 @@ def gn_apply_fwd(x0, x1, a, b, silu=True):
     return t
 
 
+GN_FUSED_MAX = 16384   # elements per (n, group) that fmd_gn_fused_apply holds in one workgroup's registers
+GN_FUSED = os.environ.get("FMD_GN_FUSED", "1") == "1"   # A/B switch (0: slab statistics + gn_prep + apply)
+
+
+def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
+    """Mirror of fmd_gn_fused_apply's applicability test (csrc/groupnorm.hip)."""
+    Cg = C // groups if C % groups == 0 else 0
+    return GN_FUSED and Cg > 0 and Cg % 4 == 0 and C0 % 4 == 0 and 256 % (Cg // 4) == 0 and HW * Cg <= GN_FUSED_MAX
+
+
+def gn_fused_apply(x0, x1, groups: int, eps: float, gamma, beta, emb=None, emb_stride=0, emb_mode=0, silu=True):
+    """GroupNorm of x0|x1 from the activations themselves (no statistics slab): returns (a, b, mean_rstd, t)
+    with t = SiLU(a*x + b) materialised -- channel_stats + gn_prep + gn_apply_fwd in one launch."""
+    N, C0 = x0.shape[0], x0.shape[-1]
+    HW = x0[0, ..., 0].numel()
+    C1 = x1.shape[-1] if x1 is not None else 0
+    Ct = C0 + C1
+    dev = x0.device
+    a = torch.empty((N, Ct), device=dev, dtype=F32)
+    b = torch.empty((N, Ct), device=dev, dtype=F32)
+    mr = torch.empty((N, groups, 2), device=dev, dtype=F32)
+    t = torch.empty((*x0.shape[:-1], Ct), device=dev, dtype=BF16)
+    _lib.call("fmd_gn_fused_apply", _p(x0), _p(x1), C0, C1, N, HW, groups, float(eps), _p(gamma), _p(beta), _p(emb),
+              emb_stride, emb_mode, int(silu), _p(a), _p(b), _p(mr), _p(t), stream())
+    return a, b, mr, t
+
+
 def dropout_apply(x, p: float, seed: torch.Tensor, salt: int, ep=None, out=None):
     """y = x * keep / (1 - p) over NHWC bf16 ``x``, keep regenerated from (seed[0], salt, element index)
     (fmd_dropout_apply); ``ep=(h, a, b)``: the backward through the dropout and the GN+SiLU prologue,

@@ -194,6 +194,13 @@ typedef struct {
 int fmd_gn_gb_fold(const fmd_gb_job* jobs, int32_t njobs, fmd_stream_t s);
 /* t = SiLU(a*x + b) (silu != 0) or a*x + b over the concat x0|x1 (bf16 [M][C0+C1]): the GroupNorm
  * prologue materialised once for its consumers. */
+/* Whole GroupNorm forward of a small level (HW * C/G <= 16384) in one launch, straight from x0|x1: per
+ * (n, group) statistics, a/b (+ emb scale/shift, emb_mode 1), mean/rstd, and t = [SiLU](a*x + b) over the
+ * channel concat (= fmd_channel_stats + fmd_gn_prep + fmd_gn_apply_fwd).  C/G % 4 == 0, C0 % 4 == 0. */
+int fmd_gn_fused_apply(const void* x0, const void* x1, int32_t C0, int32_t C1, int32_t N, int32_t HW, int32_t G,
+                       float eps, const float* gamma, const float* beta, const float* emb, int32_t emb_stride,
+                       int32_t emb_mode, int32_t silu, float* a, float* b, float* mean_rstd, void* t,
+                       fmd_stream_t s);
 int fmd_gn_apply_fwd(const void* x0, const void* x1, int32_t C0, int32_t C1, int64_t M, int32_t HW,
                      const float* a, const float* b, int32_t silu, void* t, fmd_stream_t s);
 

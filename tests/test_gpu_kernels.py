@@ -266,6 +266,40 @@ def test_groupnorm_forward_backward():
     torch.testing.assert_close(demb[:, C:].cpu(), dz.sum((2, 3)), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("H,W,C0,C1,G,ss", [(8, 8, 512, 0, 32, True), (16, 16, 256, 256, 32, False),
+                                             (4, 4, 512, 512, 32, True), (32, 32, 128, 0, 32, False),
+                                             (1, 1, 512, 0, 32, True), (2, 2, 96, 32, 8, False)])
+def test_gn_fused_apply_vs_torch(H, W, C0, C1, G, ss):
+    """fmd_gn_fused_apply (small-level GroupNorm forward in one launch, statistics straight from x0|x1) vs
+    F.group_norm (+ scale/shift) + SiLU in fp32, and its a/b/mean_rstd vs the slab path (channel_stats +
+    gn_prep) that the backward also accepts."""
+    O = ops()
+    N = 3
+    C = C0 + C1
+    g = torch.Generator().manual_seed(H * 1000 + C)
+    x = (torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3).to(torch.bfloat16)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    emb = torch.randn(N, 2 * C, generator=g) * 0.3 if ss else None
+    z = F.group_norm(x.float(), G, gamma, beta, 1e-5)
+    if ss:
+        z = z * (1 + emb[:, :C, None, None]) + emb[:, C:, None, None]
+    ref = F.silu(z).permute(0, 2, 3, 1)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x0, x1 = xn[..., :C0].contiguous(), (xn[..., C0:].contiguous() if C1 else None)
+    a, b, mr, t = O.gn_fused_apply(x0, x1, G, 1e-5, gamma.to(DEV), beta.to(DEV),
+                                   emb=emb.to(DEV) if ss else None, emb_stride=2 * C if ss else 0,
+                                   emb_mode=1 if ss else 0)
+    _close(t.float(), ref, rel=1.5e-2)
+    st0 = O.channel_stats(x0)
+    st1 = O.channel_stats(x1) if C1 else None
+    a2, b2, mr2 = O.gn_prep(st0, st1, N, H * W, C0, C1, G, 1e-5, gamma.to(DEV), beta.to(DEV),
+                            emb=emb.to(DEV) if ss else None, emb_stride=2 * C if ss else 0, emb_mode=1 if ss else 0)
+    torch.testing.assert_close(a.cpu(), a2.cpu(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(b.cpu(), b2.cpu(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(mr.cpu(), mr2.cpu(), rtol=1e-4, atol=1e-5)
+
+
 def test_groupnorm_deferred_gamma_beta_fold():
     """gb_defer/gb_flush (fmd_gn_gb_fold, one launch for many GroupNorms, incl. > FMD_GB_MAX jobs and
     dgamma-only jobs) == the per-call fold of fmd_gn_bwd_prep, bit for bit."""
