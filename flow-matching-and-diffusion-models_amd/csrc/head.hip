@@ -340,8 +340,8 @@ bool shape_ok(int N, int H, int W, int C, int K) {
          (long long)N * H * W * C < (1LL << 31);
 }
 
-constexpr int WG_WGRAD = 512;   // head_wgrad workgroups (each loops over its share of tiles)
-constexpr int RED_SPLIT = 16;   // first reduction stage: WG_WGRAD slots -> RED_SPLIT partial sums
+constexpr int WG_WGRAD = 1024;  // head_wgrad workgroups (each loops over its share of tiles; 4 per CU at 256^2)
+constexpr int RED_SPLIT = 32;   // first reduction stage: WG_WGRAD slots -> RED_SPLIT partial sums
 
 }  // namespace
 

@@ -7,9 +7,9 @@
 // (two reads give the 8 consecutive pixels a 16x16x32 fragment lane holds).
 // G is the same gather + GroupNorm-affine/SiLU prologue as the forward, so the
 // activations of the forward are recomputed on the fly, never stored.
-// The pixel range is split across workgroups (split-K); partial slabs, written
-// in the reference's [K][C][kh][kw] fp32 layout, are summed deterministically
-// (fixed order) by a second, elementwise kernel.  The bias gradient (sum of dY) rides along.
+// The pixel range is split across workgroups (split-K); partial slabs are
+// reduced deterministically by a second kernel that writes the reference's
+// [K][C][kh][kw] fp32 layout.  The bias gradient (sum of dY) rides along.
 //
 // Replaces: autograd of nn.Conv2d weight/bias (src/nn/ops/convolution.py:53).
 #include "common.h"
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
     }
   }
 
-  // partial slab: ws[split][co][ci][tap] (the reference dW layout: the reduce is an elementwise sum)
+  // partial slab: ws[split][co][tap][ci]
   float* ws = d.ws + (size_t)split * d.K * A.T * A.C;
   const int l16 = lane & 15, lq = lane >> 4;
 #pragma unroll
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 64 + 16 * i + 4 * lq + r;
-        if (co < d.K) ws[((size_t)co * A.C + ci) * A.T + ct] = acc[i][j][r];
+        if (co < d.K) ws[((size_t)co * A.T + ct) * A.C + ci] = acc[i][j][r];
       }
     }
   }
@@ -268,43 +268,41 @@ __global__ void wgrad_reduce_stage1(const WArgs A, int splits, int Q) {
   *(f32x4*)(d.ws + (size_t)s0 * per + v * 4) = (a0 + a1) + (a2 + a3);
 }
 
-// Sum the split-K slabs ws[s*sstride][k][c][tap] (s < nsl) into dW[k][c][tap] (same layout: elementwise,
-// 16-byte slab reads; dW itself may sit at any 4-byte offset of the flat gradient buffer), and db from the
-// (possibly pre-reduced) bias slabs.
+// Sum the split-K slabs ws[s*sstride][k][tap][c] (s < nsl) and write the reference layout dW[k][c][tap]
+// (+ db from the same, possibly pre-reduced, bias slabs).  A block owns (k, 64 channels): it reads
+// [tap][64 c] runs and writes the contiguous dW[k][c0:c0+64][:] run through LDS.
+constexpr int RC = 64;
+
 __global__ __launch_bounds__(256) void wgrad_reduce(const WArgs A, int splits, int nsl, int sstride) {
   const fmd_wgrad_desc& d = A.d;
+  __shared__ float res[RC * 27 + 1];   // [c][tap], T <= 27 (3x3x3)
   const size_t per = (size_t)d.K * A.T * A.C;
-  const size_t nvec = per / 4;
-  const size_t sstep = (size_t)sstride * per;
-  const bool dw_vec = ((size_t)d.dw & 15) == 0;
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {
-    const float* src = d.ws + v * 4;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  const int k = blockIdx.x, c0 = blockIdx.y * RC;
+  const int nc = min(RC, A.C - c0);
+  const int n = A.T * RC;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int tap = e / RC, cl = e - tap * RC;
+    if (cl >= nc) continue;
+    const size_t src = ((size_t)k * A.T + tap) * A.C + c0 + cl;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     int s = 0;
     for (; s + 4 <= nsl; s += 4) {
-      a0 += *(const f32x4*)(src + (size_t)s * sstep);
-      a1 += *(const f32x4*)(src + (size_t)(s + 1) * sstep);
-      a2 += *(const f32x4*)(src + (size_t)(s + 2) * sstep);
-      a3 += *(const f32x4*)(src + (size_t)(s + 3) * sstep);
+      v0 += d.ws[(size_t)s * sstride * per + src];
+      v1 += d.ws[(size_t)(s + 1) * sstride * per + src];
+      v2 += d.ws[(size_t)(s + 2) * sstride * per + src];
+      v3 += d.ws[(size_t)(s + 3) * sstride * per + src];
     }
-    for (; s < nsl; ++s) a0 += *(const f32x4*)(src + (size_t)s * sstep);
-    f32x4 r = (a0 + a1) + (a2 + a3);
-    float* out = d.dw + v * 4;
-    if (dw_vec) {
-      if (d.accumulate) r += *(const f32x4*)out;
-      *(f32x4*)out = r;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[e] = d.accumulate ? out[e] + r[e] : r[e];
-    }
+    for (; s < nsl; ++s) v0 += d.ws[(size_t)s * sstride * per + src];
+    res[cl * A.T + tap] = (v0 + v1) + (v2 + v3);
   }
-  if (d.db && blockIdx.x == 0) {
+  __syncthreads();
+  float* out = d.dw + ((size_t)k * A.C + c0) * A.T;
+  for (int e = threadIdx.x; e < nc * A.T; e += blockDim.x) out[e] = d.accumulate ? out[e] + res[e] : res[e];
+  if (d.db && blockIdx.y == 0 && threadIdx.x == 0) {
     const float* wb = d.ws + (size_t)splits * per;
-    for (int k = threadIdx.x; k < d.K; k += blockDim.x) {
-      float v = 0.f;
-      for (int s = 0; s < nsl; ++s) v += wb[(size_t)s * sstride * d.K + k];
-      d.db[k] = d.accumulate ? d.db[k] + v : v;
-    }
+    float v = 0.f;
+    for (int s = 0; s < nsl; ++s) v += wb[(size_t)s * sstride * d.K + k];
+    d.db[k] = d.accumulate ? d.db[k] + v : v;
   }
 }
 
@@ -360,7 +358,6 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
     if (rc) return rc;
   }
   if (A.T > 27) return -4;
-  const int rblocks = vblocks < 2048 ? vblocks : 2048;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(rblocks), dim3(256), 0, s, A, splits, nsl, sstride);
+  hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl, sstride);
   return (int)hipGetLastError();
 }

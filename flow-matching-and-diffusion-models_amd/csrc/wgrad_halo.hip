@@ -18,7 +18,7 @@
 //
 // 3-D (3x3x3): tiles run over the N*D output slices and a workgroup's input chunk is a (depth tap kz,
 // 64-channel block) pair staging slice z + kz - 1 (zeros outside the sample, >> 1 under nearest-x2); its
-// 9 accumulated taps land at taps kz*9 .. kz*9+8 of a 27-tap [K][C][3][3][3] slab.
+// 9 accumulated taps land at taps kz*9 .. kz*9+8 of a 27-tap slab, so wgrad_reduce writes [K][C][3][3][3].
 //
 // Replaces: autograd of nn.Conv2d weight/bias (src/nn/ops/convolution.py:53) for
 // the ResBlock 3x3 convs (src/nn/blocks/residual.py:71-76).
@@ -226,20 +226,19 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
     }
   }
 
-  // ---- partial slab ws[split][co][ci][tap], the reference dW layout (3-D tap = kz*9 + ky*3 + kx), so the
-  //      reduce is an elementwise sum; a lane's 9 taps are one contiguous 36-byte run
+  // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout; 3-D tap = kz*9 + ky*3 + kx)
   const size_t per = (size_t)d.K * T * A.C;
   float* ws = d.ws + (size_t)split * per;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
-      const int ci = ci0 + wci * 16 + l16;
-      float* dst = ws + ((size_t)co * A.C + ci) * T + kz * 9;
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) dst[tap] = acc[i][tap][r];
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
+        const int ci = ci0 + wci * 16 + l16;
+        ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[i][tap][r];
+      }
   if (do_bias) {
     // lanes of the 4 pixel groups, then the 4 cin-waves (each summed one k-step) of a cout half
     float* red = (float*)lds;    // [4 wci][128 co] floats; the tiles are done

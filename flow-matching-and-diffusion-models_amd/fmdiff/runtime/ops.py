@@ -400,6 +400,11 @@ def head_wgrad(dpred, K, h, pro, dw, db):
               stream())
 
 
+# workgroups the halo weight gradient aims for (one per CU); fewer means fewer pixel splits, i.e. smaller
+# split-K slabs (their write + reduce read) at the small levels (FMD_WGRAD_HALO_WG: A/B override)
+WGRAD_HALO_WG = int(os.environ.get("FMD_WGRAD_HALO_WG", "0") or 0) or NUM_CU
+
+
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
     """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip)."""
     return (ks == 3 and stride == 1 and pad == 1 and (Ho == 2 * Hs and Wo == 2 * Ws if upsample else
@@ -453,7 +458,7 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             zt = 3 if d3 else 1
             tiles = N * max(Do, 1) * (Ho // 8) * (Wo // 16)
             base = (K // 128) * (Ct // 64) * zt
-            splits = max(1, min(tiles, -(-NUM_CU // base), (96 << 20) // (K * Ct * 36 * zt)))
+            splits = max(1, min(tiles, -(-WGRAD_HALO_WG // base), (96 << 20) // (K * Ct * 36 * zt)))
         else:
             # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
             T = ks * ks * (ks if d3 else 1)
