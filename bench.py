@@ -177,10 +177,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; FMD_DIST_BACKEND=gloo + more ranks than GPUs rehearses the N-rank path (split graph
+    # captures, overlapped bucket all-reduces, 1/world AdamW) on a one-GPU box (ranks share the device)
+    dev_idx = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_idx)
+        dist.init_process_group(os.environ.get("FMD_DIST_BACKEND", "nccl"))
+    dev = torch.device("cuda", dev_idx)
     torch.cuda.set_device(dev)
 
     from fmdiff.models.generators import DiffusionUNetFactory
