@@ -366,7 +366,7 @@ class UNetEngine:
                 conv.out_channels, upsample=upsample, Cin=Cin, ztaps=3)
         w, wt = self._wts(conv.weight, 0, halo, None, Cin)
         out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
-                           bias=conv.bias, want_stats=True, wgt_tiled=wt)
+                           bias=conv.bias, want_stats="free", wgt_tiled=wt)
         o = Act(out, st)
         if ctx.tape is not None:
             def bwd():
@@ -609,7 +609,7 @@ class UNetEngine:
         if drop:
             ops.dropout_apply(t2, drop, seed, salt, out=t2)
         out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
-                            bias=c2.bias, want_stats=True, wgt_tiled=w2t, **kw)
+                            bias=c2.bias, want_stats="free", wgt_tiled=w2t, **kw)
         o = Act(out, ost)
         if ctx.tape is None:
             return o
@@ -720,7 +720,7 @@ class UNetEngine:
         else:
             o, lse = ops.attention_fwd(qkv, T, heads, dh, raw)
         o4 = o.view(N, H, W, inner)
-        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
+        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats="free")
         y = Act(out.view(x.t.shape), st)
         if ctx.tape is None:
             return y
@@ -804,7 +804,7 @@ class UNetEngine:
         kv, _ = ops.conv(cn, 2 * inner, self.wc.get(wkv, 0, None, Cp), ks=1, pad=0, bias=bkv)
         o, saved = ops.cross_attention_fwd(q, kv, T, Tk, heads, dh, lin, raw)
         o4 = o.view(N, H, W, inner)
-        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats=True)
+        out, st = ops.conv(o4, Cc, self.wc.get(wo, 0), ks=1, pad=0, bias=bo, resid=x4, want_stats="free")
         y = Act(out.view(x.t.shape), st)
         if ctx.tape is None:
             return y

@@ -243,7 +243,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
          out_f32=False,
          accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
          wgt2_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
-    """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``."""
+    """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``.
+    ``want_stats``: True = per-channel statistics of the output (a separate fmd_channel_stats pass when the
+    kernel cannot emit them); "free" = only when the kernel emits them (else None: Act statistics are then
+    derived on demand, and a small-level consumer that computes its own GroupNorm never pays for them)."""
     _need_cuda(src0, "conv")
     # 3-D (spatial_dims = 3): NDHWC tensors, cubic kernels; ``out_hw_`` is then (Do, Ho, Wo)
     d3 = src0.dim() == 5
@@ -328,6 +331,8 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.stats = _p(slab)
         st = Stats(slab, rows)
     _lib.call("fmd_conv", C.byref(d), stream())
+    if want_stats == "free":   # only statistics the kernel emits for free; the consumer derives others lazily
+        return out, st
     if want_stats and not fused_stats:
         if ep is not None:
             st = channel_stats(out, y=(ep[0], ep[1], ep[0].shape[-1]))

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU-box helper: config D probe per env setting.  usage: AB="FMD_X=0 FMD_X=1" bash tools/ab_latent.sh
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for setting in $AB; do
+  env $setting timeout -k 10 200 python tools/bench_latent.py ${LATENT_ARGS} > gpurun_out/abl_$setting.json 2> gpurun_out/abl_$setting.err
+  rc=$?; echo "$setting rc=$rc $(grep -o '"images_per_sec": [0-9.]*\|"sample": [0-9.]*' gpurun_out/abl_$setting.json | tr '\n' ' ')"
+  [ $rc -eq 0 ] || exit $rc
+done
