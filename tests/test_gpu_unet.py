@@ -266,6 +266,37 @@ def test_fused_sampler_matches_plain_euler_loop(golden):
         assert err < 2e-3
 
 
+def test_fused_sampler_graph_reuse_matches_fresh_capture(golden):
+    """FusedFlowSampler keeps its step graph across sample() calls of the same shapes: a second call with new
+    noise / conditioning, and a third after the weights changed in place (as an optimizer step does), each
+    equal a fresh sampler's first (capturing) call bit for bit; the returned tensors are independent."""
+    from fmdiff.pipelines.train.fused import FusedFlowSampler
+    T, M = golden
+    name = "ldct_fm_test"
+    meta = M[name]
+    model = _build(meta).to(DEV)
+    _load_seeded(model, meta)
+    g = torch.Generator().manual_seed(11)
+    shape = T[f"{name}/x"].shape
+    cond = T[f"{name}/cond"].to(DEV)
+    inits = [torch.randn(shape, generator=g).to(DEV) for _ in range(3)]
+    conds = [cond, (cond + 0.1 * torch.randn(cond.shape, generator=g).to(DEV)).contiguous(), cond]
+    cached = FusedFlowSampler(model, 5)
+    first = cached.sample(inits[0], conds[0])
+    graph = cached._graph
+    second = cached.sample(inits[1], conds[1])
+    assert cached._graph is graph, "same shapes: the captured graph is reused"
+    ref1 = FusedFlowSampler(model, 5).sample(inits[1], conds[1])
+    assert torch.equal(second, ref1)
+    with torch.no_grad():   # an in-place weight update (the fp32 masters the bf16 kernel copies derive from)
+        for p in model.parameters():
+            p.mul_(1.01)
+    third = cached.sample(inits[2], conds[2])
+    ref2 = FusedFlowSampler(model, 5).sample(inits[2], conds[2])
+    assert torch.equal(third, ref2)
+    assert not torch.equal(first, second) and first.data_ptr() != second.data_ptr()
+
+
 @pytest.mark.parametrize("name", ["ldct_fm_test", "ldct_fm_diffusers_b64"])
 def test_fused_train_step_split_capture_matches_full_graph(golden, name):
     """FusedTrainStep.capture(split_collectives=True) -- the multi-rank form: forward+backward graph,
