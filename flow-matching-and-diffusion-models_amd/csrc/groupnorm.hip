@@ -436,6 +436,15 @@ __global__ __launch_bounds__(256) void gn_fused_apply_kernel(
   const bf16r* src = s0 ? x0 + c : x1 + (c - C0);
   const int ld = s0 ? C0 : C1;
   const size_t pix0 = (size_t)n * HW;
+  // the per-channel parameters are read up front with the activations: one memory round trip, not two
+  float gm[4], bt[4], sc[4], sh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    gm[e] = gamma ? gamma[c + e] : 1.f;
+    bt[e] = beta ? beta[c + e] : 0.f;
+    sc[e] = emb_mode == 1 ? 1.f + emb[(size_t)n * emb_stride + c + e] : 1.f;
+    sh[e] = emb_mode == 1 ? emb[(size_t)n * emb_stride + C + c + e] : 0.f;
+  }
   uint2 v[GN_FUSED_UNITS];
   float f1 = 0.f, f2 = 0.f;
 #pragma unroll
@@ -469,15 +478,11 @@ __global__ __launch_bounds__(256) void gn_fused_apply_kernel(
   float av[4], bv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int ce = c + e;
-    const float gm = gamma ? gamma[ce] : 1.f, bt = beta ? beta[ce] : 0.f;
-    av[e] = rstd * gm;
-    bv[e] = bt - meanf * av[e];
+    av[e] = rstd * gm[e];
+    bv[e] = bt[e] - meanf * av[e];
     if (emb_mode == 1) {
-      const float sc = 1.f + emb[(size_t)n * emb_stride + ce];
-      const float sh = emb[(size_t)n * emb_stride + C + ce];
-      av[e] *= sc;
-      bv[e] = bv[e] * sc + sh;
+      av[e] *= sc[e];
+      bv[e] = bv[e] * sc[e] + sh[e];
     }
   }
   if (tid < Q) {

@@ -51,6 +51,8 @@ MAT_CMAX = 128
 # 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
 DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
 MAT_MIN_HW = 128 * 128
+# ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); FMD_POINT_1X1=0 for A/B runs
+POINT_1X1 = os.environ.get("FMD_POINT_1X1", "1") == "1"
 
 
 class Act:
@@ -122,6 +124,8 @@ class WeightCache:
                 self._dpack(e["src"], e["mode"], e["buf"])
             elif e["kind"] == "e1d":
                 self._embed1d(e["src"], e["buf"])
+            elif e["kind"] == "ctr":
+                e["buf"].copy_(e["src"].detach()[:, :, 1:2, 1:2])
             elif e["kind"] == "fused":
                 o = 0
                 for w in e["src"]:
@@ -188,6 +192,18 @@ class WeightCache:
             buf = e["buf"] if e is not None else torch.empty((*w.shape[:2], k, k), device=w.device, dtype=F32)
             self._embed1d(w, buf)
             self._c[key] = dict(kind="e1d", src=w, buf=buf, ver=self._ver(w))
+            self._force.discard(key)
+        return self._c[key]["buf"]
+
+    def center(self, w: torch.Tensor) -> torch.Tensor:
+        """fp32 [K][C][1][1] centre tap of a 3x3 weight: on a 1x1 image (zero padding all round) the 3x3 conv is
+        exactly the 1x1 conv with this weight, a ninth of the weight bytes and K-steps."""
+        key = (id(w), "ctr")
+        if not self._fresh(key, self._ver(w)):
+            e = self._c.get(key)
+            buf = e["buf"] if e is not None else torch.empty((*w.shape[:2], 1, 1), device=w.device, dtype=F32)
+            buf.copy_(w.detach()[:, :, 1:2, 1:2])
+            self._c[key] = dict(kind="ctr", src=w, buf=buf, ver=self._ver(w))
             self._force.discard(key)
         return self._c[key]["buf"]
 
@@ -563,7 +579,10 @@ class UNetEngine:
         mat1 = _materialise(halo1, x1, Cin, HW)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
             halo1 = self._halo_ok(N, sp, Cout, Cin)
-        w1, w1t = self._wts(c1.weight, 0, halo1)
+        # a 1x1 level (the bottom of a small latent UNet): the 3x3 convs are their centre taps (exact)
+        point = POINT_1X1 and sp == (1, 1) and c1.weight.dim() == 4 and not halo1
+        pk = dict(ks=1, pad=0) if point else {}
+        w1, w1t = (self.wc.get(self.wc.center(c1.weight), 0), None) if point else self._wts(c1.weight, 0, halo1)
         if mat1 and ops.gn_fused_eligible(HW, Cin, C0, g1.num_groups):
             # small level: statistics, affine and the materialised prologue in one launch from x0|x1
             a1, b1, mr1, t1 = ops.gn_fused_apply(x0.t, x1.t if x1 else None, g1.num_groups, g1.eps, g1.weight,
@@ -579,7 +598,7 @@ class UNetEngine:
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=add or not fuse2,
-                          wgt_tiled=w1t)
+                          wgt_tiled=w1t, **pk)
         t2 = None
         if fuse2:
             a2, b2, mr2, t2 = ops.gn_fused_apply(h, None, g2.num_groups, g2.eps, g2.weight, g2.bias,
@@ -603,7 +622,10 @@ class UNetEngine:
         if not isinstance(sk, Identity):
             s2, s2t = self._wts(sk.conv.weight, 0, halo2)
             kw.update(src2=x0.t, src3=x1.t if x1 else None, wgt2=s2, wgt2_tiled=s2t, bias2=sk.conv.bias)
-        w2, w2t = self._wts(c2.weight, 0, halo2)
+        point2 = POINT_1X1 and sp == (1, 1) and c2.weight.dim() == 4 and not halo2
+        w2, w2t = (self.wc.get(self.wc.center(c2.weight), 0), None) if point2 else self._wts(c2.weight, 0, halo2)
+        if point2:
+            kw.update(ks=1, pad=0)
         if mat2 and t2 is None:
             t2 = ops.gn_apply_fwd(h, None, a2, b2)
         if drop:
