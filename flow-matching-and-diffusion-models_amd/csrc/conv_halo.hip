@@ -1212,6 +1212,15 @@ __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, i
 
 // Called by fmd_conv when the problem qualifies (3x3, stride 1, pad 1, forward gather,
 // output tile 16x16 inside one image, >= 128 tiles).  Returns 1 if not applicable.
+// fewest workgroups (tiles x splits) the halo conv takes; smaller grids go to the implicit GEMM
+static int g_halo_min_wg = 128;
+
+extern "C" int fmd_halo_set_min_workgroups(int32_t n) {
+  if (n < 1) return -1;
+  g_halo_min_wg = n;
+  return 0;
+}
+
 extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->ks != 3 || d->stride != 1 || d->pad != 1 || d->transposed) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;
@@ -1245,7 +1254,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt2 = (const bf16r*)d->wgt2_tiled;
   A.dbg = g_dbg;
   const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
-  if (nwg * A.splits < 128) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
+  if (nwg * A.splits < g_halo_min_wg) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);

@@ -85,6 +85,7 @@ SIGNATURES = {
     "fmd_gn_gb_fold": [p, i32, p],
     "fmd_lincomb": [C.POINTER(LincombDesc), p],
     "fmd_halo_set_workgroup": [i32],
+    "fmd_halo_set_min_workgroups": [i32],
     "fmd_halo_set_variant": [i32],
     "fmd_halo_set_persist": [i32, i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
@@ -155,6 +156,8 @@ def lib():
             fn.restype = _RESTYPE.get(name, i32)
         if os.environ.get("FMD_HALO_NT"):
             check(L.fmd_halo_set_workgroup(int(os.environ["FMD_HALO_NT"])), "fmd_halo_set_workgroup")
+        if os.environ.get("FMD_HALO_MIN_WG"):
+            check(L.fmd_halo_set_min_workgroups(int(os.environ["FMD_HALO_MIN_WG"])), "fmd_halo_set_min_workgroups")
         if os.environ.get("FMD_HALO_STAGGER"):
             check(L.fmd_halo_set_persist(512, int(os.environ["FMD_HALO_STAGGER"])), "fmd_halo_set_persist")
         if os.environ.get("FMD_HALO_V"):

@@ -212,20 +212,27 @@ HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
 SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
 
 
+# fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (FMD_HALO_MIN_WG, _lib load)
+HALO_MIN_WG = int(os.environ.get("FMD_HALO_MIN_WG", "128") or 128)
+
+
 def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
     """Split-K factor the halo kernel uses: 1 when the 16x16 tiles x cout tiles already give >= 128
-    workgroups, else enough chunk-range splits (>= 2 chunks each) to reach ~256; 0 = not eligible."""
+    workgroups, else enough chunk-range splits (>= 2 chunks each) to reach ~256; 0 = not eligible
+    (fewer than HALO_MIN_WG workgroups)."""
     nwg = N * (Ho // 16) * (Wo // 16) * -(-K // 128)
     if nwg >= 128:
         return 1
     nch = -(-max(Cin, 1) // HALO_BK) * ztaps
     sp = min(-(-256 // max(nwg, 1)), nch // 2, 16)
-    if sp < 2 or nwg * sp < 128:
+    if sp < 2 and nwg >= HALO_MIN_WG:
+        return 1
+    if sp < 2 or nwg * sp < HALO_MIN_WG:
         return 0
     cps = -(-nch // sp)
     while sp > 1 and (sp - 1) * cps >= nch:   # every split owns at least one chunk (mirrors the kernel)
         sp -= 1
-    return sp if nwg * sp >= 128 else 0
+    return sp if nwg * sp >= HALO_MIN_WG else 0
 
 
 def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False, Cin=0,

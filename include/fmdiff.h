@@ -110,6 +110,10 @@ int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_st
 /* Halo conv workgroup size: 512 (8 waves x 64 pixels each, default) or 256 (4 waves x 128 pixels,
  * 256 VGPRs per wave).  Returns -1 for other values.  Also settable with FMD_HALO_NT at load time. */
 int fmd_halo_set_workgroup(int32_t nt);
+/* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv
+ * (default 128; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
+ * halo_splits mirror reads the same variable. */
+int fmd_halo_set_min_workgroups(int32_t n);
 /* 2-D halo conv main loop: 1 (default) = v_mfma_f32_16x16x32_bf16 (v1) everywhere; 2 = v2
  * (v_mfma_f32_32x32x16_bf16) for GroupNorm-prologue problems, v1 otherwise; 3 = v2 everywhere (testing). */
 int fmd_halo_set_variant(int32_t v);
