@@ -525,8 +525,15 @@ __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
     const int p = (int)(idx / K);
     const int c = (int)(idx - (size_t)p * K);
     const int n = p / HWo;
-    float v = 0.f;
-    for (int s = 0; s < d.splits; ++s) v += d.ws[(size_t)s * total + idx];
+    // the tiny levels split K 16-72 ways: 8 independent loads in flight per thread, not one chain
+    float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 8 <= d.splits; s += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a8[u] += d.ws[(size_t)(s + u) * total + idx];
+    }
+    for (; s < d.splits; ++s) a8[0] += d.ws[(size_t)s * total + idx];
+    float v = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
     if (d.bias) v += d.bias[c];
     if (d.bias2) v += d.bias2[c];
     if (d.bias_nc) v += d.bias_nc[(size_t)n * K + c];
@@ -569,9 +576,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d,
       const int p = row * RP + pl;
       const int n = p / HWo;
       const size_t idx = (size_t)p * K + c;
-      f32x4 v = *(const f32x4*)(d.ws + idx);
-#pragma unroll 4
-      for (int s = 1; s < d.splits; ++s) v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+      // four independent chains over the splits (loads of four slabs in flight), fixed summation order
+      f32x4 v = *(const f32x4*)(d.ws + idx), v1 = {0.f, 0.f, 0.f, 0.f}, v2 = v1, v3 = v1;
+      int s = 1;
+      for (; s + 4 <= d.splits; s += 4) {
+        v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+        v1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * total + idx);
+        v2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * total + idx);
+        v3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * total + idx);
+      }
+      for (; s < d.splits; ++s) v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+      v = (v + v1) + (v2 + v3);
       if (d.bias) v += *(const f32x4*)(d.bias + c);
       if (d.bias2) v += *(const f32x4*)(d.bias2 + c);
       if (d.bias_nc) {   // may be a row view of a wider table: no 16-byte alignment assumed
