@@ -90,17 +90,31 @@ __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const f
                             : st1 + (size_t)n * E1 * C1 * 2 + (size_t)(c_begin - C0) * 2;
     const int E = in0 ? E0 : E1;
     const int stride = (in0 ? C0 : C1) * 2;
-    float f1 = 0.f, f2 = 0.f;
-    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    // four slab entries per thread in flight (independent partial sums), not one load round trip each
+    float f1[4] = {0.f, 0.f, 0.f, 0.f}, f2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int step = blockDim.x;
+    int e = threadIdx.x;
+    for (; e + 3 * step < E; e += 4 * step) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = base + (size_t)(e + u * step) * stride;
+        for (int q = 0; q < Cg / 2; ++q) {
+          const f32x4 v = *(const f32x4*)(p + 4 * q);
+          f1[u] += v[0] + v[2];
+          f2[u] += v[1] + v[3];
+        }
+      }
+    }
+    for (; e < E; e += step) {
       const float* p = base + (size_t)e * stride;
       for (int q = 0; q < Cg / 2; ++q) {
         const f32x4 v = *(const f32x4*)(p + 4 * q);
-        f1 += v[0] + v[2];
-        f2 += v[1] + v[3];
+        f1[0] += v[0] + v[2];
+        f2[0] += v[1] + v[3];
       }
     }
-    s1 = f1;
-    s2 = f2;
+    s1 = (double)((f1[0] + f1[1]) + (f1[2] + f1[3]));
+    s2 = (double)((f2[0] + f2[1]) + (f2[2] + f2[3]));
   } else {
     for (int idx = threadIdx.x;; idx += blockDim.x) {
       // enumerate (channel in group, entry)
@@ -182,12 +196,25 @@ __global__ __launch_bounds__(256) void gn_bwd_prep_kernel(
   double a = 0.0, q = 0.0, sx = 0.0;
   if (cl < Cg) {
     const int c = g * Cg + cl;
-    for (int e = sub; e < E; e += T) {
-      const float* p = s12 + (((size_t)n * E + e) * C + c) * 2;
-      a += p[0];
-      q += p[1];
+    // four slab entries in flight per thread (independent partial sums)
+    double a4[4] = {0.0, 0.0, 0.0, 0.0}, q4[4] = {0.0, 0.0, 0.0, 0.0};
+    int e = sub;
+    for (; e + 3 * T < E; e += 4 * T) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float2 v = *(const float2*)(s12 + (((size_t)n * E + e + u * T) * C + c) * 2);
+        a4[u] += v.x;
+        q4[u] += v.y;
+      }
     }
-    for (int e = sub; e < FE; e += T) sx += fst[(((size_t)n * FE + e) * C + c) * 2];
+    for (; e < E; e += T) {
+      const float2 v = *(const float2*)(s12 + (((size_t)n * E + e) * C + c) * 2);
+      a4[0] += v.x;
+      q4[0] += v.y;
+    }
+    a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    q = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+    for (int e2 = sub; e2 < FE; e2 += T) sx += fst[(((size_t)n * FE + e2) * C + c) * 2];
   }
   sS1[tid] = a; sS2[tid] = q; sSx[tid] = sx;
   __syncthreads();
