@@ -195,9 +195,9 @@ def out_hw(Hs, ks, stride, pad, upsample):
 
 # split-K of the generic implicit GEMM on small grids: >= SPLIT_MIN_STEPS k-steps per split, about
 # SPLIT_CU_MULT workgroups per CU, at most SPLIT_CAP splits (env overrides for A/B measurements)
-SPLIT_MIN_STEPS = int(os.environ.get("FMD_SPLIT_MIN_STEPS", "4"))
+SPLIT_MIN_STEPS = int(os.environ.get("FMD_SPLIT_MIN_STEPS", "2"))
 SPLIT_CU_MULT = int(os.environ.get("FMD_SPLIT_CU_MULT", "2"))
-SPLIT_CAP = int(os.environ.get("FMD_SPLIT_CAP", "32"))
+SPLIT_CAP = int(os.environ.get("FMD_SPLIT_CAP", "64"))
 
 
 def _choose_splits(M, K, nk, bpx=128, bco=128):
