@@ -212,6 +212,11 @@ HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
 SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
 
 
+# halo split-K on the small levels: ~HALO_SPLIT_WG workgroups, >= HALO_MIN_CHUNKS 32-channel chunks per split,
+# <= HALO_SPLIT_CAP splits (env overrides for A/B runs)
+HALO_SPLIT_WG = int(os.environ.get("FMD_HALO_SPLIT_WG", "256"))
+HALO_MIN_CHUNKS = int(os.environ.get("FMD_HALO_MIN_CHUNKS", "2"))
+HALO_SPLIT_CAP = int(os.environ.get("FMD_HALO_SPLIT_CAP", "16"))
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (FMD_HALO_MIN_WG, _lib load)
 HALO_MIN_WG = int(os.environ.get("FMD_HALO_MIN_WG", "128") or 128)
 
@@ -224,7 +229,7 @@ def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
     if nwg >= 128:
         return 1
     nch = -(-max(Cin, 1) // HALO_BK) * ztaps
-    sp = min(-(-256 // max(nwg, 1)), nch // 2, 16)
+    sp = min(-(-HALO_SPLIT_WG // max(nwg, 1)), nch // HALO_MIN_CHUNKS, HALO_SPLIT_CAP)
     if sp < 2 and nwg >= HALO_MIN_WG:
         return 1
     if sp < 2 or nwg * sp < HALO_MIN_WG:
@@ -412,6 +417,9 @@ def head_wgrad(dpred, K, h, pro, dw, db):
               stream())
 
 
+# generic weight-gradient split-K: >= WGRAD_MIN_STEPS 32-pixel steps per split, ~WGRAD_CU_MULT workgroups per CU
+WGRAD_MIN_STEPS = int(os.environ.get("FMD_WGRAD_MIN_STEPS", "8"))
+WGRAD_CU_MULT = int(os.environ.get("FMD_WGRAD_CU_MULT", "4"))
 # workgroups the halo weight gradient aims for (one per CU); fewer means fewer pixel splits, i.e. smaller
 # split-K slabs (their write + reduce read) at the small levels (FMD_WGRAD_HALO_WG: A/B override)
 WGRAD_HALO_WG = int(os.environ.get("FMD_WGRAD_HALO_WG", "0") or 0) or NUM_CU
@@ -476,9 +484,10 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             T = ks * ks * (ks if d3 else 1)
             tiles = -(-K // 128) * (1 if T > 1 and Ct * T <= 128 else -(-Ct // 128) * T)
             steps = -(-M // 32)
-            # up to 4 workgroups per CU (the kernel is latency-bound at one), partial slabs <= 48 MB
+            # up to WGRAD_CU_MULT workgroups per CU (the kernel is latency-bound at one), >= WGRAD_MIN_STEPS
+            # 32-pixel steps per split, partial slabs <= 48 MB
             cap = max(256, min(1024, (48 << 20) // (K * Ct * T * 4)))
-            splits = max(1, min(steps // 8, -(-4 * NUM_CU // tiles), cap))
+            splits = max(1, min(steps // WGRAD_MIN_STEPS, -(-WGRAD_CU_MULT * NUM_CU // tiles), cap))
     d.splits = splits
     ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
     d.ws = _p(ws)
