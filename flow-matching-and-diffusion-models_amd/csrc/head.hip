@@ -9,7 +9,8 @@
 // VALU kernels around a once-per-element transform:
 //   head_fwd   : 16x16-pixel tile per workgroup, thread = pixel; per 32-channel chunk the
 //                transformed (18x18) halo is staged once in LDS (chunk-major planes, as in
-//                conv_halo.hip) and every tap reads it; weights of the chunk in LDS (broadcast).
+//                conv_halo.hip) and every tap reads it; weights of the chunk in LDS as bf16 pairs
+//                (broadcast); taps are v_dot2c_f32_bf16 on the packed halo (fp32 accumulate).
 //   head_dgrad : thread = 8 channels x one tile row; dpred's 18x18 halo (Kp = 8 bf16 = 16 B per
 //                pixel) in LDS; epilogue = SiLU' of the forward pre-activation, bf16 store and the
 //                GroupNorm-backward sums (sum dz, sum dz*x) per 64-pixel slab row.
@@ -74,35 +75,45 @@ struct HeadArgs {
 template <int KT>
 __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
   __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
-  __shared__ __attribute__((aligned(16))) float wl[KT][9][CK];   // chunk weights [k][tap][c]
+  __shared__ __attribute__((aligned(16))) unsigned int wl[KT][9][CK / 2];   // chunk weights [k][tap][c pair], bf16x2
   const int tid = threadIdx.x;
   const int tile = blockIdx.x, per = A.tiles_x * A.tiles_y;
   const int n = tile / per, tr = tile - n * per;
   const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
   const int py = tid >> 4, px = tid & 15;
-  float acc[KT];
+  // two accumulators per output channel (the 8-channel pieces alternate), fp32 throughout
+  float acc[KT][2];
 #pragma unroll
-  for (int k = 0; k < KT; ++k) acc[k] = 0.f;
+  for (int k = 0; k < KT; ++k) acc[k][0] = acc[k][1] = 0.f;
   for (int c0 = 0; c0 < A.C; c0 += CK) {
     stage_halo(halo, A.h, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
-    for (int i = tid; i < KT * 9 * CK; i += NTH) {
-      const int k = i / (9 * CK), r = i - k * 9 * CK, tap = r / CK, c = r - tap * CK;
-      wl[k][tap][c] = k < A.K ? A.w[((size_t)k * A.C + c0 + c) * 9 + tap] : 0.f;
+    for (int i = tid; i < KT * 9 * (CK / 2); i += NTH) {
+      const int k = i / (9 * (CK / 2)), r = i - k * 9 * (CK / 2), tap = r / (CK / 2), cp = r - tap * (CK / 2);
+      const size_t w0 = ((size_t)k * A.C + c0 + 2 * cp) * 9 + tap;
+      wl[k][tap][cp] = k < A.K ? pack2(A.w[w0], A.w[w0 + 9]) : 0u;
     }
     __syncthreads();
+    // bf16 operands straight from LDS into v_dot2c_f32_bf16 (two products per op, fp32 accumulate):
+    // no per-tap unpacking of the halo, a quarter of the fp32-FMA form's VALU ops
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int pos = (py + tap / 3) * HR + px + tap % 3;
 #pragma unroll
       for (int kc = 0; kc < KCP; ++kc) {
         const u32x4 v = halo[kc * HPADP + pos];
-        const float t[8] = {bf_lo(v[0]), bf_hi(v[0]), bf_lo(v[1]), bf_hi(v[1]),
-                            bf_lo(v[2]), bf_hi(v[2]), bf_lo(v[3]), bf_hi(v[3])};
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-          const f32x4 w0 = *(const f32x4*)&wl[k][tap][kc * 8], w1 = *(const f32x4*)&wl[k][tap][kc * 8 + 4];
-          acc[k] += t[0] * w0[0] + t[1] * w0[1] + t[2] * w0[2] + t[3] * w0[3] +
-                    t[4] * w1[0] + t[5] * w1[1] + t[6] * w1[2] + t[7] * w1[3];
+          const u32x4 w = *(const u32x4*)&wl[k][tap][kc * 4];
+          float a = acc[k][kc & 1];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // copy the vector lanes to scalars first: __builtin_bit_cast of an ext_vector element lvalue
+            // reads lane 0 (hipcc 7.2), which silently dotted the first channel pair four times
+            const unsigned int ve = v[e], we = w[e];
+            a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_, ve), __builtin_bit_cast(bf16x2_, we), a,
+                                                false);
+          }
+          acc[k][kc & 1] = a;
         }
       }
     }
@@ -118,7 +129,7 @@ __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
       float r = 0.f;
 #pragma unroll
       for (int j = 0; j < KT; ++j)
-        if (j == kk) r = acc[j];
+        if (j == kk) r = acc[j][0] + acc[j][1];
       v[e] = kk < A.K ? r + (A.bias ? A.bias[kk] : 0.f) : 0.f;
     }
     *(f32x4*)(o + k) = v;
