@@ -332,10 +332,8 @@ __global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restric
   };
   // 16-byte accesses over the (16-byte aligned) flat buffers; the n % 4 tail element-wise
   const long long n4 = vec ? n >> 2 : 0;
-  // every byte is touched once per step: nontemporal loads / stores keep the 3.2 GB stream out of L2
   GRID_STRIDE(i, n4) {
-    f32x4 pv = __builtin_nontemporal_load((const f32x4*)p + i), gv = __builtin_nontemporal_load((const f32x4*)g + i);
-    f32x4 mv = __builtin_nontemporal_load((const f32x4*)m + i), vv = __builtin_nontemporal_load((const f32x4*)v + i);
+    f32x4 pv = ((const f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float pe = pv[e], me = mv[e], ve = vv[e];
@@ -344,9 +342,9 @@ __global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restric
       mv[e] = me;
       vv[e] = ve;
     }
-    __builtin_nontemporal_store(pv, (f32x4*)p + i);
-    __builtin_nontemporal_store(mv, (f32x4*)m + i);
-    __builtin_nontemporal_store(vv, (f32x4*)v + i);
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
   }
   for (long long i = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float pv = p[i], mv = m[i], vv = v[i];
