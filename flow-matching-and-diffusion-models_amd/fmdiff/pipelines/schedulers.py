@@ -202,6 +202,13 @@ class DDPMScheduler:
         ts = ts.contiguous()
         if ts.numel() != N or nz.shape != x0.shape:
             raise ValueError("add_noise: one timestep per sample and noise of the samples' shape")
+        # the kernel gathers sa[t] / sb[t] unchecked: validate the range here, as torch indexing does in the
+        # reference (IndexError); a stream capture cannot read the device tensor, so captures skip the check
+        T = int(sa.numel())
+        if N and not torch.cuda.is_current_stream_capturing():
+            lo, hi = int(ts.min()), int(ts.max())
+            if lo < 0 or hi >= T:
+                raise IndexError(f"add_noise: timesteps must lie in [0, {T}), got [{lo}, {hi}]")
         out = torch.empty_like(x0)
         from .. import _lib
         _lib.call("fmd_add_noise", x0.data_ptr(), nz.data_ptr(), sa.data_ptr(), sb.data_ptr(), ts.data_ptr(), N,

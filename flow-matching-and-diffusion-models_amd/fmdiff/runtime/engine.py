@@ -111,6 +111,9 @@ class WeightCache:
         self._jobs_key = None
         self._jobs = None
         self._nblk = 0
+        # job tables replaced by a rebuild: a captured graph (train step, sampler) holds the raw pointer of
+        # the table it recorded and replays fmd_prep_weights_batch on it, so a table lives as long as the cache
+        self._retired: List[torch.Tensor] = []
 
     @staticmethod
     def _ver(t):
@@ -166,6 +169,8 @@ class WeightCache:
                     rows.append(row + [0] * (16 - len(row)))
                     blk += kt * ct
             dev = jobs[0][1]["buf"].device
+            if self._jobs is not None:
+                self._retired.append(self._jobs)
             self._jobs = torch.tensor(rows, dtype=torch.int64).to(dev)
             self._njobs = len(rows)
             self._nblk = blk
@@ -704,7 +709,15 @@ class UNetEngine:
         forward's value to regenerate its masks."""
         st = getattr(self, "_drop_state", None)
         if st is None:
-            st = self._drop_state = (torch.zeros(1, device=dev, dtype=torch.int32), {})
+            # the counter starts from torch's (host) generator, so training.seed / set_seed selects the mask
+            # sequence, and is offset by the data-parallel rank so ranks draw different masks for the same local
+            # sample position (the reference draws every mask from torch's RNG). Not saved in checkpoints: a
+            # resumed run restarts the sequence from the seeded generator.
+            import torch.distributed as dist
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+            base = int(torch.randint(0, 1 << 30, (1,)).item())
+            start = (base + rank * 1000003) % (1 << 31)
+            st = self._drop_state = (torch.full((1,), start, device=dev, dtype=torch.int32), {})
         seed, salts = st
         if not ctx.drop_seeded:
             ops.counter_add(seed, 1)

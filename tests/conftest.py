@@ -64,3 +64,15 @@ def golden_attn():
     tensors = torch.load(os.path.join(d, "golden_attn.pt"), weights_only=True)
     meta = json.load(open(os.path.join(d, "golden_attn.json")))
     return tensors, meta
+
+
+@pytest.fixture(scope="session")
+def golden_ddpm():
+    """Reference DDPM train steps on configs C (256^2) and A (MNIST diffusers): make_golden_ddpm.py."""
+    import json
+
+    import torch
+    d = os.path.join(REPO, "tests", "golden")
+    tensors = torch.load(os.path.join(d, "golden_ddpm.pt"), weights_only=True)
+    meta = json.load(open(os.path.join(d, "golden_ddpm.json")))
+    return tensors, meta

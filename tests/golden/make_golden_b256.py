@@ -15,7 +15,9 @@ the parameters with ``oracle.unet.seeded_state_dict`` and records, at 256x256 an
   (lr 1e-4, wd 0) stepped under ``transformers.get_cosine_schedule_with_warmup`` (the formula
   diffusers' helper implements; warmup 0 so this first step moves the weights, total 1000)):
   the loss, per-parameter gradient sums / sums of squares, the full gradients of every
-  parameter with <= 4096 elements, and per-parameter sums before and after the AdamW update.
+  parameter with <= 4096 elements, and per-parameter sums before and after the AdamW update;
+  plus order-sensitive fingerprints (tests/golden/projections.py) of every gradient and every AdamW
+  parameter delta: 8 seeded Rademacher projections per tensor and every 397th element of the concatenation.
 
 Output: ``tests/golden/golden_b256.pt`` (tensors only; ``weights_only=True``) + ``golden_b256.json``.
 """
@@ -39,6 +41,9 @@ from transformers.optimization import get_cosine_schedule_with_warmup  # noqa: E
 
 from oracle import spec as S  # noqa: E402
 from oracle import unet as U  # noqa: E402
+
+sys.path.insert(0, HERE)
+import projections as P  # noqa: E402
 
 torch.set_num_threads(8)
 CFG = "configs/flow_matching/ldct_flow_matching.json"
@@ -79,6 +84,7 @@ def main():
     sched = get_cosine_schedule_with_warmup(opt, num_warmup_steps=WARMUP, num_training_steps=TOTAL)
     names = [k for k, _ in model.named_parameters()]
     before = torch.stack([p.detach().double().sum() for _, p in model.named_parameters()])
+    p_before = [p.detach().clone() for _, p in model.named_parameters()]
     opt.zero_grad(set_to_none=True)
     pred = model(torch.cat([x_t, ldct], 1), timesteps)
     loss = F.mse_loss(pred, noise - clean)
@@ -87,6 +93,11 @@ def main():
     opt.step()
     sched.step()
     after = torch.stack([p.detach().double().sum() for _, p in model.named_parameters()])
+    deltas = [p.detach().double() - b.double() for (_, p), b in zip(model.named_parameters(), p_before)]
+    glist = [grads[k] for k in names]
+    out.update({"step/proj_grad": P.projections(glist, SEED), "step/sample_grad": P.strided_sample(glist).float(),
+                "step/proj_delta": P.projections(deltas, SEED + 1),
+                "step/sample_delta": P.strided_sample(deltas).float()})
     out.update({"step/clean": clean, "step/ldct": ldct, "step/noise": noise, "step/t": tt,
                 "step/loss": loss.detach(), "step/param_sum_before": before, "step/param_sum_after": after,
                 "step/grad_sum": torch.stack([grads[k].double().sum() for k in names]),

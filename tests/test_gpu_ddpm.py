@@ -173,3 +173,38 @@ def test_sample_with_scheduler_vs_oracle(golden, kind):
     print(f"{kind}: sample_with_scheduler rel L2 {err:.3e}, model calls {timing.get('model_calls')}")
     assert timing["model_calls"] == n_calls
     assert err < 2e-2
+
+
+@pytest.mark.parametrize("case", ["c256", "mnist"])
+def test_ddpm_fused_train_step_vs_reference_golden(golden_ddpm, case):
+    """FusedTrainStep(objective="ddpm"), graph-captured, on the configurations that train with DDPM, vs the
+    reference's own step (tests/golden/make_golden_ddpm.py; diffusion_lib.py:153-185):
+
+    * ``c256``: config C's 113 M EfficientUNetND (configs/diffusion/ldct_ddpm.json) at 256x256, batch 2;
+    * ``mnist``: config A's UNetDiffusersND (configs/MNIST/mnist_ddpm_diffusers_nd.json) at 32x32, batch 2.
+
+    Injected eps and integer timesteps; the config's betas; AdamW at the config's lr under the cosine
+    schedule (warmup 0).  Checks: loss, per-tensor gradient statistics, full small gradients, Rademacher
+    projections and strided samples of every large gradient and AdamW delta (test_gpu_unet.py)."""
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.pipelines.schedulers import DDPMScheduler
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    from oracle import spec as S
+    from oracle import unet as U
+    from test_gpu_unet import _check_step_vs_golden
+    T, M = golden_ddpm
+    m = M[case]
+    tr_cfg = m["training"]
+    model = DiffusionUNetFactory().build(m["unet"], tr_cfg["conditioning"], tr_cfg["channels"]).to(DEV)
+    spec = S.derive_spec(m["unet"], tr_cfg["conditioning"], tr_cfg["channels"])
+    sd = U.seeded_state_dict(spec, m["seed"])
+    model.load_state_dict(sd)
+    sch = DDPMScheduler(m["num_train_timesteps"], **m["scheduler"].get("params", {}))
+    tr = FusedTrainStep(model, objective="ddpm", ddpm_scheduler=sch, lr=m["lr"], weight_decay=m["weight_decay"],
+                        warmup=m["warmup"], total_steps=m["total"], num_train_timesteps=m["num_train_timesteps"])
+    clean, ldct, noise, ts = (T[f"{case}/{k}"].to(DEV) for k in ("clean", "ldct", "noise", "t"))
+    tr.capture(clean, ldct, warmup_iters=2, noise=noise, t=ts)
+    loss = tr.replay()
+    torch.cuda.synchronize()
+    assert int(tr.step_ctr.item()) == 1
+    _check_step_vs_golden(model, T, m, case, loss.item(), m["lr"], small=m["small_grads"], sd_before=sd)

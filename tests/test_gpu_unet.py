@@ -92,19 +92,32 @@ def test_train_step_gradients_vs_oracle(golden):
     assert worst[0] > 0.99, worst
 
 
-def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), tol_sum=5e-2, tol_sq=5e-2,
-                          flip_frac=0.05, negligible=1e-5, dead_bound=1e-3):
-    """Loss, per-parameter gradient sums / sums of squares, full small gradients and post-AdamW parameter
-    sums of a finished FusedTrainStep vs a reference-generated fixture.
+def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_before=None, tol_sum=5e-2,
+                          tol_sq=5e-2, flip_frac=0.05, negligible=1e-5, dead_bound=1e-3, cos_grad=0.99,
+                          cos_delta=0.99):
+    """Loss, per-parameter gradient statistics, element-order-sensitive gradient / AdamW-delta fingerprints
+    and post-AdamW parameter sums of a finished FusedTrainStep vs a reference-generated fixture.
 
     Tensors whose reference gradient norm is below ``negligible`` x the whole-model gradient norm are
     mathematically ~0 (e.g. the bias of a conv feeding a GroupNorm with one channel per group): their
     reference values are fp32 round-off, so they are only required to stay below ``dead_bound`` x the
-    whole-model norm on the GPU (bf16 round-off of an exact cancellation).
-    Gradient sums are compared relative to sqrt(numel) * ||g_ref|| (the Cauchy-Schwarz bound of a sum of
-    differences), so a tensor whose sum cancels to ~0 is not held to a relative bar it cannot meet.  The
-    first AdamW step moves every element by ~lr * sign(g): the per-tensor change of the parameter sum may
-    differ from the reference's by at most ``flip_frac`` of the elements flipping sign (2 lr each)."""
+    whole-model norm on the GPU (bf16 round-off of an exact cancellation).  For every other ("live") tensor:
+
+    * gradient sum: |sum(g) - sum(g_ref)| <= tol_sum * ||g_ref|| (the sum of an error vector e of random
+      signs is ~||e||; bf16 round-off gives ||e|| ~ 1e-2 ||g||);
+    * gradient norm within tol_sq relative;
+    * fingerprints (tests/golden/projections.py), for tensors of more than 4096 elements (smaller ones are
+      compared in full): cosine >= cos_grad between the 8 seeded Rademacher projections of g and of g_ref,
+      and between g and g_ref on the fixture's strided sample (every 397th element of the concatenation;
+      tensors with >= 8 sampled elements).  Sums and norms are permutation-invariant, these are not: a tap-
+      or channel-permuted weight gradient has cosine ~0;
+    * AdamW parameter delta (p_after - p_before): the same two cosines against the reference's delta
+      (>= cos_delta), and the per-tensor change of the parameter sum may differ from the reference's by at
+      most ``flip_frac`` of the elements flipping sign (the first AdamW step moves each element by
+      ~lr * sign(g), 2 lr per flip)."""
+    import sys
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "golden"))
+    import projections as P
     names = m["param_names"]
     params = dict(model.named_parameters())
     numel = {k: params[k].numel() for k in names}
@@ -114,17 +127,18 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), tol_su
     total = math.sqrt(T[f"{prefix}/grad_sq"].sum().item())
     live = set()
     worst_sum = worst_sq = worst_dead = 0.0
+    grads = [params[k].grad.detach().double().cpu() for k in names]
     for i, k in enumerate(names):
-        g = params[k].grad.double().cpu()
+        g = grads[i]
         rs, rq = T[f"{prefix}/grad_sum"][i].item(), T[f"{prefix}/grad_sq"][i].item()
         gn = math.sqrt(g.pow(2).sum().item())
         if math.sqrt(rq) < negligible * total:
             worst_dead = max(worst_dead, gn / total)
             continue
         live.add(k)
-        worst_sum = max(worst_sum, abs(g.sum().item() - rs) / math.sqrt(numel[k] * rq))
+        worst_sum = max(worst_sum, abs(g.sum().item() - rs) / math.sqrt(rq))
         worst_sq = max(worst_sq, abs(gn - math.sqrt(rq)) / math.sqrt(rq))
-    print(f"grad sums over {len(live)} tensors: worst |d sum| / (sqrt(n) ||g||) {worst_sum:.3e}, worst relative "
+    print(f"grad sums over {len(live)} tensors: worst |d sum| / ||g|| {worst_sum:.3e}, worst relative "
           f"norm error {worst_sq:.3e}; {len(names) - len(live)} ~0-gradient tensors, worst norm {worst_dead:.2e} x total")
     assert worst_sum < tol_sum and worst_sq < tol_sq and worst_dead < dead_bound
     worst_cos = 1.0
@@ -137,7 +151,34 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), tol_su
     if small:
         print(f"small-tensor gradients: worst cosine {worst_cos:.5f} over {len(small)} tensors")
         assert worst_cos > 0.99
+
+    seed_g = m.get("proj_seed_grad", m["seed"])
+    seed_d = m.get("proj_seed_delta", m["seed"] + 1)
+    segs = P.sample_segments([numel[k] for k in names])
+    large = [i for i, k in enumerate(names) if k in live and numel[k] > 4096]
+
+    def fingerprint(vals, proj_ref, sample_ref, seed, what, bound):
+        pj = P.projections(vals, seed)
+        sm = P.strided_sample(vals)
+        wp = ws = (1.0, "")
+        for i in large:
+            wp = min(wp, (P.cosine(pj[i], proj_ref[i]), names[i]))
+            sg = segs[i]
+            if sg.stop - sg.start >= 8:
+                ws = min(ws, (P.cosine(sm[sg], sample_ref[sg]), names[i]))
+        print(f"{what}: worst projection cosine {wp[0]:.5f} ({wp[1]}), worst strided-sample cosine {ws[0]:.5f} "
+              f"({ws[1]}) over {len(large)} tensors > 4096 elements")
+        assert wp[0] >= bound and ws[0] >= bound, (what, wp, ws)
+
+    if f"{prefix}/proj_grad" in T:
+        fingerprint(grads, T[f"{prefix}/proj_grad"], T[f"{prefix}/sample_grad"], seed_g, "gradients", cos_grad)
+    del grads
     before = T[f"{prefix}/param_sum_before"]
+    if f"{prefix}/proj_delta" in T and sd_before is not None:
+        deltas = [params[k].detach().double().cpu() - sd_before[k].double() for k in names]
+        fingerprint(deltas, T[f"{prefix}/proj_delta"], T[f"{prefix}/sample_delta"], seed_d, "AdamW deltas",
+                    cos_delta)
+        del deltas
     worst_flip = 0.0
     for i, k in enumerate(names):
         if k not in live:   # lr * sign(round-off) on both sides
@@ -172,7 +213,7 @@ def test_b256_fused_train_step_vs_reference_golden(golden_b256):
     from fmdiff.pipelines.train.fused import FusedTrainStep
     T, m = golden_b256
     model = _build(m).to(DEV)
-    _load_seeded(model, m)
+    _, sd = _load_seeded(model, m)
     tr = FusedTrainStep(model, lr=m["lr"], warmup=m["warmup"], total_steps=m["total"],
                         num_train_timesteps=m["num_train_timesteps"], weight_decay=m["weight_decay"])
     clean, ldct, noise, t = (T[f"step/{k}"].to(DEV) for k in ("clean", "ldct", "noise", "t"))
@@ -181,7 +222,7 @@ def test_b256_fused_train_step_vs_reference_golden(golden_b256):
     loss = tr.replay()
     torch.cuda.synchronize()
     assert int(tr.step_ctr.item()) == 1
-    _check_step_vs_golden(model, T, m, "step", loss.item(), m["lr"], small=m["small_grads"])
+    _check_step_vs_golden(model, T, m, "step", loss.item(), m["lr"], small=m["small_grads"], sd_before=sd)
 
 
 def test_fused_train_step_tiny_post_adamw_vs_golden(golden):

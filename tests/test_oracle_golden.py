@@ -88,6 +88,60 @@ def test_b256_fm_train_step(golden_b256):
     torch.testing.assert_close(ps, T["step/param_sum_after"], rtol=1e-7, atol=1e-6)
 
 
+def _fingerprints_match(T, prefix, vals, seed, what):
+    """The fixture's order-sensitive fingerprints (tests/golden/projections.py) regenerate from the oracle's
+    tensors: pins both the oracle and the fingerprint code the GPU tests use."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import projections as P
+    pj = P.projections(vals, seed)
+    ref = T[f"{prefix}/proj_{what}"]
+    assert torch.allclose(pj, ref, rtol=1e-6, atol=1e-9 * ref.abs().max().item()), (pj - ref).abs().max()
+    sm = P.strided_sample(vals).float()
+    assert torch.allclose(sm, T[f"{prefix}/sample_{what}"], rtol=1e-6, atol=1e-12)
+
+
+def test_b256_fingerprints(golden_b256):
+    """Config B 256^2 FM step: the oracle's gradients reproduce the fixture's projections / strided sample."""
+    T, m = golden_b256
+    spec = _spec(m)
+    sd = _params(spec, m["seed"])
+    loss, scaled = OT.fm_loss(sd, spec, T["step/clean"], T["step/ldct"], T["step/noise"], T["step/t"],
+                              m["num_train_timesteps"])
+    scaled.backward()
+    _fingerprints_match(T, "step", [sd[k].grad for k in m["param_names"]], m["seed"], "grad")
+
+
+@pytest.mark.parametrize("case", ["c256", "mnist"])
+def test_ddpm_train_step_vs_reference(golden_ddpm, case):
+    """Configs C (256^2, 113 M EfficientUNetND) and A (MNIST UNetDiffusersND): the oracle's DDPM step
+    (add_noise, loss, gradients, AdamW under the cosine schedule) vs the reference's
+    (tests/golden/make_golden_ddpm.py; diffusion_lib.py:153-185)."""
+    T, M = golden_ddpm
+    m = M[case]
+    spec = _spec(m)
+    sd = _params(spec, m["seed"])
+    before = {k: v.detach().clone() for k, v in sd.items()}
+    sch = OS.DDPM(m["num_train_timesteps"], **m["scheduler"].get("params", {}))
+    assert torch.equal(sch.add_noise(T[f"{case}/clean"], T[f"{case}/noise"], T[f"{case}/t"]), T[f"{case}/noisy"])
+    loss, scaled = OT.ddpm_loss(sd, spec, sch, T[f"{case}/clean"], T[f"{case}/ldct"], T[f"{case}/noise"],
+                                T[f"{case}/t"])
+    scaled.backward()
+    assert torch.equal(loss.detach(), T[f"{case}/loss"])
+    names = m["param_names"]
+    torch.testing.assert_close(torch.stack([sd[k].grad.double().sum() for k in names]), T[f"{case}/grad_sum"],
+                               rtol=1e-9, atol=1e-12)
+    for k in m["small_grads"]:
+        assert torch.equal(sd[k].grad, T[f"{case}/grad/{k}"]), k
+    _fingerprints_match(T, case, [sd[k].grad for k in names], m["proj_seed_grad"], "grad")
+    lr = m["lr"] * OS.cosine_with_warmup(0, m["warmup"], m["total"])
+    OT.adamw_step(sd, lr, 1, {}, weight_decay=m["weight_decay"])
+    ps = torch.stack([sd[k].detach().double().sum() for k in names])
+    torch.testing.assert_close(ps, T[f"{case}/param_sum_after"], rtol=1e-7, atol=1e-6)
+    _fingerprints_match(T, case, [sd[k].detach().double() - before[k].double() for k in names],
+                        m["proj_seed_delta"], "delta")
+
+
 def test_self_attention_raw_reshape(golden):
     T, M = golden
     m = M["attn"]
