@@ -433,14 +433,64 @@ __global__ void lincomb_kernel(const fmd_lincomb_desc D) {
   if (vec) {
     GRID_STRIDE(i, n4) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < D.nin; ++k) acc += D.c[k] * ((const f32x4*)D.in[k])[i];
+      for (int k = 0; k < D.nin; ++k) {
+        const f32x4 v = ((const f32x4*)D.in[k])[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(D.c[k], v[e], acc[e]);
+      }
       ((f32x4*)D.out)[i] = acc;
     }
   } else {
     GRID_STRIDE(i, D.n) {
       float acc = 0.f;
-      for (int k = 0; k < D.nin; ++k) acc += D.c[k] * D.in[k][i];
+      for (int k = 0; k < D.nin; ++k) acc = __builtin_fmaf(D.c[k], D.in[k][i], acc);
       D.out[i] = acc;
+    }
+  }
+}
+
+// fmd_sched_step (include/fmdiff.h): one DPM-Solver / UniPC step, coefficients from the device-indexed table
+__global__ void sched_step_kernel(const fmd_sched_step_desc D) {
+  const int i = D.index[0];
+  const float* c = D.coef + (size_t)i * FMD_SCHED_NCOEF;
+  float* const rw = D.ring[i & 3];
+  const float* const r1 = D.ring[(i - 1) & 3];
+  const float* const r2 = D.ring[(i - 2) & 3];
+  const float* const r3 = D.ring[(i - 3) & 3];
+  const bool corr = c[2] != 0.f;
+  const long long total = (long long)D.N * D.HW;
+  GRID_STRIDE(p, total) {
+    const int n = (int)(p / D.HW), hw = (int)(p % D.HW);
+    for (int ch = 0; ch < D.Cx; ++ch) {
+      const size_t xi = ((size_t)n * D.Cx + ch) * D.HW + hw;
+      const float xv = D.x[xi];
+      float m = 0.f;
+      m = __builtin_fmaf(c[0], xv, m);
+      m = __builtin_fmaf(c[1], D.eps[p * D.Kpad + ch], m);
+      rw[xi] = m;
+      float xc = xv;
+      if (corr) {
+        float a = 0.f;
+        a = __builtin_fmaf(c[3], D.last[xi], a);
+        a = __builtin_fmaf(c[4], r1[xi], a);
+        a = __builtin_fmaf(c[5], r2[xi], a);
+        a = __builtin_fmaf(c[6], r3[xi], a);
+        a = __builtin_fmaf(c[7], m, a);
+        xc = a;
+      }
+      if (D.last) D.last[xi] = xc;
+      float pv = 0.f;
+      pv = __builtin_fmaf(c[8], xc, pv);
+      pv = __builtin_fmaf(c[9], m, pv);
+      pv = __builtin_fmaf(c[10], r1[xi], pv);
+      pv = __builtin_fmaf(c[11], r2[xi], pv);
+      D.x[xi] = pv;
+      if (D.next) ((bf16r*)D.next)[p * D.Cpad + ch] = (bf16r)f2bf(pv);
+    }
+    if (D.next) {
+      bf16r* nx = (bf16r*)D.next;
+      for (int ch = 0; ch < D.Cc; ++ch) nx[p * D.Cpad + D.Cx + ch] = (bf16r)f2bf(D.cond[((size_t)n * D.Cc + ch) * D.HW + hw]);
+      for (int ch = D.Cx + D.Cc; ch < D.Cpad; ++ch) nx[p * D.Cpad + ch] = 0;
     }
   }
 }
@@ -950,6 +1000,15 @@ int fmd_lincomb(const fmd_lincomb_desc* d, fmd_stream_t s) {
   }
   if (d->n == 0) return 0;
   LAUNCH(lincomb_kernel, grid_for((d->n & 3) == 0 ? d->n / 4 : d->n), *d);
+}
+
+int fmd_sched_step(const fmd_sched_step_desc* d, fmd_stream_t s) {
+  if (!d || !d->x || !d->eps || !d->coef || !d->index || d->N < 1 || d->Cx < 1 || d->HW < 1 || d->Kpad < d->Cx)
+    return -1;
+  for (int k = 0; k < 4; ++k)
+    if (!d->ring[k]) return -2;
+  if (d->next && (d->Cpad < d->Cx + d->Cc || (d->Cc > 0 && !d->cond))) return -3;
+  LAUNCH(sched_step_kernel, grid_for((long long)d->N * d->HW), *d);
 }
 
 int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s) {

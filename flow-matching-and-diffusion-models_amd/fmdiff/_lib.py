@@ -58,6 +58,15 @@ class LincombDesc(C.Structure):
     _fields_ = [("out", p), ("in_", p * LINCOMB_MAX), ("c", C.c_float * LINCOMB_MAX), ("nin", i32), ("n", i64)]
 
 
+SCHED_NCOEF = 12  # FMD_SCHED_NCOEF
+
+
+class SchedStepDesc(C.Structure):
+    """Mirror of ``fmd_sched_step_desc``."""
+    _fields_ = [("x", p), ("eps", p), ("ring", p * 4), ("last", p), ("coef", p), ("index", p), ("N", i32), ("Cx", i32),
+                ("HW", i32), ("Kpad", i32), ("cond", p), ("Cc", i32), ("Cpad", i32), ("next", p)]
+
+
 class GbJob(C.Structure):
     """Mirror of ``fmd_gb_job``."""
     _fields_ = [("ws", p), ("dgamma", p), ("dbeta", p), ("N", i32), ("C", i32)]
@@ -84,6 +93,7 @@ SIGNATURES = {
     "fmd_dropout_apply": [p, i32, i64, i32, f32, p, u32, p, p, p, p, p],
     "fmd_gn_gb_fold": [p, i32, p],
     "fmd_lincomb": [C.POINTER(LincombDesc), p],
+    "fmd_sched_step": [C.POINTER(SchedStepDesc), p],
     "fmd_halo_set_workgroup": [i32],
     "fmd_halo_set_min_workgroups": [i32],
     "fmd_halo_set_variant": [i32],

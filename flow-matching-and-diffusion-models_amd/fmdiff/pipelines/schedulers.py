@@ -20,6 +20,8 @@ import torch
 
 from ..runtime import ops
 
+SCHED_NCOEF = 12   # FMD_SCHED_NCOEF: coefficient row of the table-driven multistep step (fmd_sched_step)
+
 
 @dataclass
 class SchedulerOutput:
@@ -396,6 +398,43 @@ class DPMSolverMultistepScheduler(_MultistepBase):
         d2 = [y / (r0 + r1) for y in diff]
         return cx, [c0 + cd1 * d1[0] + cd2 * d2[0], cd1 * d1[1] + cd2 * d2[1], cd1 * d1[2] + cd2 * d2[2]]
 
+    def plan(self, start: int = 0) -> torch.Tensor:
+        """Coefficient rows of fmd_sched_step for steps ``start`` .. end of the schedule set by set_timesteps, in
+        the order ``step`` takes them from a fresh state (the same order decisions and coefficient folding, so
+        the table-driven graph step equals this class's eager steps): [n - start][12] fp32."""
+        n = len(self.timesteps)
+        saved = self._step_index
+        pp = self.config.algorithm_type == "dpmsolver++"
+        rows, lon = [], 0
+        try:
+            for i in range(start, n):
+                self._step_index = i
+                lof = i == n - 1 and (self.config.euler_at_final or (self.config.lower_order_final and n < 15)
+                                      or self.config.final_sigmas_type == "zero")
+                los = i == n - 2 and self.config.lower_order_final and n < 15
+                if self.config.solver_order == 1 or lon < 1 or lof:
+                    order = 1
+                elif self.config.solver_order == 2 or lon < 2 or los:
+                    order = 2
+                else:
+                    order = 3
+                cx, cm = self._coefs(order)
+                row = [0.0] * SCHED_NCOEF
+                if pp:
+                    a, s = self._alpha_sigma(self.sigmas[i])
+                    row[0], row[1] = float(1.0 / a), float(-(s / a))
+                else:
+                    row[1] = 1.0
+                row[8] = float(cx)
+                for k, c in enumerate(cm):
+                    row[9 + k] = float(c)
+                rows.append(row)
+                if lon < self.config.solver_order:
+                    lon += 1
+        finally:
+            self._step_index = saved
+        return torch.tensor(rows, dtype=torch.float32)
+
     def step(self, model_output, timestep, sample, generator=None, variance_noise=None, return_dict: bool = True,
              **_kw):
         eps, x = self._prep(model_output, sample)
@@ -495,6 +534,37 @@ class UniPCMultistepScheduler(_MultistepBase):
             cmt = -(g * rhos[-1])
             cm[0] = cm[0] + g * rhos[-1]
         return cx, cm, cmt
+
+    def plan(self, start: int = 0) -> torch.Tensor:
+        """Coefficient rows of fmd_sched_step (corrector + predictor) for steps ``start`` .. end of the schedule,
+        in the order ``step`` takes them from a fresh state: [n - start][12] fp32."""
+        n = len(self.timesteps)
+        saved = (self._step_index, self.this_order)
+        rows, lon, this_order = [], 0, None
+        try:
+            for i in range(start, n):
+                self._step_index = i
+                row = [0.0] * SCHED_NCOEF
+                a, s = self._alpha_sigma(self.sigmas[i])
+                row[0], row[1] = float(1.0 / a), float(-(s / a))
+                if i > start and (i - 1) not in self.config.disable_corrector:
+                    cx, cm, cmt = self._update(True, this_order)
+                    row[2], row[3], row[7] = 1.0, float(cx), float(cmt)
+                    for k, c in enumerate(cm):
+                        row[4 + k] = float(c)
+                order = min(self.config.solver_order, n - i) if self.config.lower_order_final \
+                    else self.config.solver_order
+                this_order = min(order, lon + 1)
+                cx, cm, _ = self._update(False, this_order)
+                row[8] = float(cx)
+                for k, c in enumerate(cm):
+                    row[9 + k] = float(c)
+                rows.append(row)
+                if lon < self.config.solver_order:
+                    lon += 1
+        finally:
+            self._step_index, self.this_order = saved
+        return torch.tensor(rows, dtype=torch.float32)
 
     def step(self, model_output, timestep, sample, return_dict: bool = True, generator=None, **_kw):
         eps, x = self._prep(model_output, sample)

@@ -20,6 +20,7 @@ buckets.
 from __future__ import annotations
 
 import math
+import time
 from typing import Optional
 
 import torch
@@ -27,6 +28,7 @@ import torch
 from ...runtime import ops
 from ...runtime.dp import bucketed_allreduce, bucketed_allreduce_async, world_size
 from ...runtime.engine import get_engine
+from ..schedulers import SCHED_NCOEF
 
 
 class FlatParams:
@@ -361,15 +363,42 @@ class FusedTrainStep:
         return self._graph_loss
 
 
-class FusedFlowSampler:
-    """FlowMatchEuler sampling loop (``src/pipelines/utils.py:163-220``) with one replayable step."""
+class FusedSampler:
+    """The sampling loop of ``src/pipelines/utils.py:163-220`` (``cat([x, cond])`` -> UNet ->
+    ``scheduler.step``) with one replayable step for every scheduler that has a HIP step:
 
-    def __init__(self, model, num_inference_steps: int = 50, num_train_timesteps: int = 1000):
-        from ..schedulers import FlowMatchEulerDiscreteScheduler
+    * FlowMatchEuler: ``fmd_flow_euler`` (sigmas on the device);
+    * DDPM / DDIM (eta 0): ``fmd_ddpm_step`` with a per-step coefficient table (``scheduler.coefficients``)
+      and, for DDPM, the variance noise of every step drawn up front into one [S][N,C,*S] buffer (or injected);
+    * DPM-Solver(++) / UniPC: ``fmd_sched_step`` over ``scheduler.plan()`` (the host bookkeeping of the
+      eager ``step``: order warm-up, lower-order final steps, corrector) and a 4-slot data-prediction ring.
+
+    Every table is indexed by a device step counter, so the step (time embedding row, UNet forward, scheduler
+    update, next packed model input) is captured once and replayed S times; a later call with the same shapes
+    only re-arms the static buffers.  ``start``: first step index of the schedule (the reference's tail
+    selection, ``select_timesteps``); the eager scheduler would begin there from a fresh state, and so does
+    the table."""
+
+    def __init__(self, model, scheduler, num_inference_steps: int, start: int = 0):
+        from ..schedulers import (DDIMScheduler, DDPMScheduler, DPMSolverMultistepScheduler,
+                                  FlowMatchEulerDiscreteScheduler, UniPCMultistepScheduler)
         self.eng = get_engine(model)
-        self.sched = FlowMatchEulerDiscreteScheduler(num_train_timesteps)
+        self.sched = scheduler
         self.sched.set_timesteps(num_inference_steps)
-        self.S = num_inference_steps
+        if isinstance(scheduler, FlowMatchEulerDiscreteScheduler):
+            self.kind = "fm"
+        elif isinstance(scheduler, DDIMScheduler):
+            self.kind = "ddim"
+        elif isinstance(scheduler, DDPMScheduler):
+            self.kind = "ddpm"
+        elif isinstance(scheduler, (DPMSolverMultistepScheduler, UniPCMultistepScheduler)):
+            self.kind = "ms"
+        else:
+            raise NotImplementedError(f"no fused step for {type(scheduler).__name__}")
+        self.S0 = int(start)
+        self.S = len(self.sched.timesteps) - self.S0
+        if self.S < 1:
+            raise ValueError("No timesteps selected after applying start_step/last_n_steps.")
         self._graph = None
         self._gkey = None
         self.cca = None
@@ -378,32 +407,63 @@ class FusedFlowSampler:
         return (tuple(init.shape), init.device, None if cond is None else tuple(cond.shape),
                 None if context_ca is None else tuple(context_ca.shape))
 
+    def _tables(self, dev):
+        sch = self.sched
+        self.ts = sch.timesteps.to(dev).float().contiguous()         # model timestep of every step
+        self.sig = self.coef = None
+        if self.kind == "fm":
+            self.sig = sch.sigmas.to(dev)
+        elif self.kind in ("ddpm", "ddim"):
+            self.coef = torch.stack([sch.coefficients(int(t)) for t in sch.timesteps]).to(dev).contiguous()
+        else:
+            self.coef = torch.zeros(len(sch.timesteps), SCHED_NCOEF, dtype=torch.float32)
+            self.coef[self.S0:] = sch.plan(self.S0)
+            self.coef = self.coef.to(dev)
+
     def _prepare(self, init, cond):
         dev = init.device
-        self.ts = self.sched.timesteps.to(dev)
-        self.sig = self.sched.sigmas.to(dev)
-        self.idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._tables(dev)
+        self.idx = torch.full((1,), self.S0, dtype=torch.int32, device=dev)
         self.x = init.float().clone()
         self.cond = cond.float().contiguous() if cond is not None else None
         Cx = init.shape[1]
         Cc = cond.shape[1] if cond is not None else 0
         self.inp = ops.noise_prepare(None, self.x, None, None, self.cond, max(8, -(-(Cx + Cc) // 8) * 8))
         self.tbuf = torch.empty(init.shape[0], device=dev, dtype=torch.float32)
+        self.noise = None
+        if self.kind == "ddpm":   # row i = step i's variance noise (NCHW), all steps of the schedule
+            self.noise = torch.empty((len(self.sched.timesteps), *init.shape), device=dev, dtype=torch.float32)
+        self.ring = self.last = None
+        if self.kind == "ms":
+            self.ring = [torch.zeros_like(self.x) for _ in range(4)]
+            self.last = torch.zeros_like(self.x)
         # the schedule is fixed: every step's time embedding is computed once, the step copies its row
         self.eng.set_time_table(self.ts, init.shape[0], self.idx)
         self._tt = self.eng._tt   # the captured step reads these tables: keep them alive with the graph
 
+    def _draw(self, noise, generator):
+        if self.noise is None:
+            return
+        if noise is not None:
+            self.noise[self.S0:].copy_(noise.reshape(self.S, *self.noise.shape[1:]))
+        else:
+            self.noise[self.S0:].normal_(generator=generator)
+
     def _refresh(self, init, cond, context_ca):
         """Re-arm the cached graph's static buffers for a new call (same shapes): sample, conditioning, the
-        packed model input, the step counter, and the time-embedding tables (the time MLP's weights may have
-        changed since the capture)."""
+        packed model input, the step counter, the solver history, and the time-embedding tables (the time
+        MLP's weights may have changed since the capture)."""
         self.eng.invalidate_weights()   # bf16 kernel weights re-derived in place from the fp32 masters
         self.x.copy_(init)
         if self.cond is not None:
             self.cond.copy_(cond)
         if self.cca is not None:
             self.cca.copy_(context_ca)
-        self.idx.zero_()
+        self.idx.fill_(self.S0)
+        if self.ring is not None:
+            for r in self.ring:
+                r.zero_()
+            self.last.zero_()
         Cx = init.shape[1]
         Cc = cond.shape[1] if cond is not None else 0
         ops.noise_prepare(None, self.x, None, None, self.cond, max(8, -(-(Cx + Cc) // 8) * 8), out=self.inp)
@@ -418,40 +478,76 @@ class FusedFlowSampler:
         if self.eng._tt is None:   # no precomputed embedding table: the MLP runs on t = ts[idx]
             ops.fill_from_table(self.ts, self.idx, self.tbuf)
         out, _ = self.eng.forward(self.inp, self.tbuf, save=False, context_ca=self.cca)
-        ops.flow_euler(self.x, out, self.sig, self.idx, self.cond, self.inp)
+        if self.kind == "fm":
+            ops.flow_euler(self.x, out, self.sig, self.idx, self.cond, self.inp)
+        elif self.kind in ("ddpm", "ddim"):
+            ops.ddpm_step(self.x, out, self.coef, self.idx, self.noise, self.cond, self.inp)
+        else:
+            ops.sched_step(self.x, out, self.ring, self.last if self._unipc() else None, self.coef, self.idx,
+                           self.cond, self.inp)
         ops.counter_add(self.idx)
+
+    def _unipc(self):
+        from ..schedulers import UniPCMultistepScheduler
+        return isinstance(self.sched, UniPCMultistepScheduler)
 
     @torch.no_grad()
     def sample(self, init: torch.Tensor, cond: Optional[torch.Tensor] = None, use_graph: bool = True,
-               context_ca: Optional[torch.Tensor] = None):
-        """``cond``: concatenated conditioning; ``context_ca``: cross-attention conditioning.
+               context_ca: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None, generator=None,
+               timing: Optional[dict] = None):
+        """``cond``: concatenated conditioning; ``context_ca``: cross-attention conditioning; ``noise``: DDPM
+        variance noise of the S steps ([S, *init.shape]; drawn with ``generator`` when None).  ``timing``: the
+        reference's ``model_seconds`` / ``model_calls`` accumulators (pipelines/utils.py:196-200), here the
+        whole replayed loop (UNet + scheduler update) between two device synchronisations.
 
         With ``use_graph`` the step is captured once per input shape and the graph is kept: a later call
         with the same shapes only re-arms the static buffers (``_refresh``) and replays it S times.  The
-        returned tensor is that static sample buffer (overwritten by the next call)."""
+        returned tensor is a copy of the sample buffer."""
         key = self._key(init, cond, context_ca)
+        t0 = None
         if use_graph and self._graph is not None and self._gkey == key:
             self._refresh(init, cond, context_ca)
+            self._draw(noise, generator)
+            if timing is not None:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
             for _ in range(self.S):
                 self._graph.replay()
-            self.eng.set_time_table(None)
-            return self.x.clone()
+            return self._finish(timing, t0)
         self._graph = None
         self._prepare(init, cond)
+        self._draw(noise, generator)
         self.cca = context_ca.float().contiguous() if context_ca is not None else None
+        if timing is not None:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
         if not use_graph:
             for _ in range(self.S):
                 self._one()
-            self.eng.set_time_table(None)
-            return self.x
+            return self._finish(timing, t0)
         self.eng.invalidate_weights()
-        self._one()   # step 0 eagerly: re-derives the bf16 weights and warms the allocator
+        self._one()   # the first step eagerly: re-derives the bf16 weights and warms the allocator
         g = torch.cuda.CUDAGraph()
         mode = "thread_local" if torch.distributed.is_available() and torch.distributed.is_initialized() else "global"
-        with torch.cuda.graph(g, capture_error_mode=mode):   # records, does not execute: the counter stays at 1
+        with torch.cuda.graph(g, capture_error_mode=mode):   # records, does not execute: the counter stays
             self._one()
         for _ in range(self.S - 1):
             g.replay()
         self._graph, self._gkey = g, key
+        return self._finish(timing, t0)
+
+    def _finish(self, timing, t0):
         self.eng.set_time_table(None)
+        if timing is not None:
+            torch.cuda.synchronize()
+            timing["model_seconds"] = timing.get("model_seconds", 0.0) + (time.perf_counter() - t0)
+            timing["model_calls"] = timing.get("model_calls", 0) + self.S
         return self.x.clone()
+
+
+class FusedFlowSampler(FusedSampler):
+    """FlowMatchEuler sampling loop (``src/pipelines/utils.py:163-220``) with one replayable step."""
+
+    def __init__(self, model, num_inference_steps: int = 50, num_train_timesteps: int = 1000):
+        from ..schedulers import FlowMatchEulerDiscreteScheduler
+        super().__init__(model, FlowMatchEulerDiscreteScheduler(num_train_timesteps), num_inference_steps)

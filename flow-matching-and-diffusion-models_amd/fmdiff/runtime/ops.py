@@ -903,6 +903,20 @@ def ddpm_step(x, eps_nhwc, coef, index, noise, cond, next_inp):
               _p(cond), Cc, next_inp.shape[-1] if next_inp is not None else 0, _p(next_inp), stream())
 
 
+def sched_step(x, eps_nhwc, ring, last, coef, index, cond, next_inp):
+    """One table-driven DPM-Solver / UniPC step (fmd_sched_step): x [N,Cx,*S] fp32 updated in place, ring = 4
+    fp32 history buffers of x's shape, last (UniPC corrector state) or None, coef [steps][12] fp32."""
+    N, Cx = x.shape[:2]
+    d = _lib.SchedStepDesc()
+    d.x, d.eps, d.last, d.coef, d.index = _p(x), _p(eps_nhwc), _p(last), _p(coef), _p(index)
+    for k in range(4):
+        d.ring[k] = _p(ring[k])
+    d.N, d.Cx, d.HW, d.Kpad = N, Cx, x[0, 0].numel(), eps_nhwc.shape[-1]
+    d.cond, d.Cc = _p(cond), cond.shape[1] if cond is not None else 0
+    d.Cpad, d.next = (next_inp.shape[-1], _p(next_inp)) if next_inp is not None else (0, None)
+    _lib.call("fmd_sched_step", C.byref(d), stream())
+
+
 def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step):
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step

@@ -7,9 +7,10 @@
   plain load fails.  Checkpoints are read with ``weights_only=True`` only.
 * ``decode_diffusion_batch`` (``:165-245``): scheduler from the config (+ ``run_model --scheduler``
   override), tail selection, optional noised-reference init, then ``sample_with_scheduler`` on the HIP
-  engine.  When the scheduler is FlowMatchEuler, the whole schedule is run, the init is random and the
-  model is an fmdiff UNet, the loop is the graph-replayed ``FusedFlowSampler`` (same arithmetic: the
-  bit-exact Euler kernel after the same UNet forward), unless ``use_fused=False``.
+  engine.  On an fmdiff UNet with any scheduler that has a HIP step (FlowMatchEuler, DDPM, DDIM,
+  DPM-Solver(++), UniPC) the loop -- whole schedule or its selected tail -- is the graph-replayed
+  ``FusedSampler`` (the generic loop's arithmetic, one host launch per step; DDPM's variance noise drawn
+  up front), unless ``use_fused=False``.
 * ``encode_diffusion_batch`` (``:147-162``), ``prepare_diffusion_visual_batch`` (``:273-300``),
   ``select_visual_indices`` (``src/utils/indexing_utils.py:6-28``), ``warn_attention_conditioning_shape``.
 """
@@ -23,7 +24,7 @@ import torch
 
 from ...models.generators import DiffusionUNetFactory
 from ...pipelines.utils import (build_scheduler, resolve_conditioning_mode, resolve_scheduler_override,
-                                sample_with_scheduler)
+                                sample_with_scheduler, select_timesteps)
 
 # diffusers / legacy UNet parameter names -> this model tree's names (reference diffusion_utils.py:15-43)
 _LEGACY_RENAMES = (
@@ -113,12 +114,14 @@ def encode_diffusion_batch(scheduler, targets: torch.Tensor, timesteps: torch.Te
     return scheduler.add_noise(targets, torch.randn_like(targets), timesteps)
 
 
-def _fused_flow_ok(model, scheduler, init_sample, start_step, last_n_steps, timing, use_fused) -> bool:
+def _fused_ok(model, scheduler, use_fused) -> bool:
+    """The graph-replayed sampler (FusedSampler) serves every scheduler with a HIP step on an fmdiff UNet."""
     from ...models.unet.base import BaseUNetND
-    from ...pipelines.schedulers import FlowMatchEulerDiscreteScheduler
-    return (use_fused and isinstance(scheduler, FlowMatchEulerDiscreteScheduler) and isinstance(model, BaseUNetND)
-            and float(getattr(scheduler.config, "shift", 1.0)) == 1.0 and init_sample is None
-            and start_step is None and last_n_steps is None and timing is None)
+    from ...pipelines.schedulers import (DDIMScheduler, DDPMScheduler, DPMSolverMultistepScheduler,
+                                         FlowMatchEulerDiscreteScheduler, UniPCMultistepScheduler)
+    return use_fused and isinstance(model, BaseUNetND) and isinstance(scheduler, (
+        FlowMatchEulerDiscreteScheduler, DDPMScheduler, DDIMScheduler, DPMSolverMultistepScheduler,
+        UniPCMultistepScheduler))
 
 
 def decode_diffusion_batch(model, training_cfg: dict, model_cfg: dict, device, batch_shape,
@@ -154,28 +157,30 @@ def decode_diffusion_batch(model, training_cfg: dict, model_cfg: dict, device, b
                             "random init.", scheduler.__class__.__name__)
     mode = resolve_conditioning_mode(training_cfg.get("conditioning") or model_cfg.get("conditioning"))
     latent_norm = training_cfg.get("latent_norm")
-    if _fused_flow_ok(model, scheduler, init, start_step, last_n_steps, timing, use_fused) and mode in (
-            None, "concatenate", "attention"):
-        return _fused_flow_decode(model, scheduler, n_inf, batch_shape, device, mode, conditioning_batch, latent_norm)
+    if _fused_ok(model, scheduler, use_fused) and mode in (None, "concatenate", "attention"):
+        start = len(scheduler.timesteps) - len(select_timesteps(scheduler.timesteps, start_step, last_n_steps))
+        return _fused_decode(model, scheduler, n_inf, batch_shape, device, mode, conditioning_batch, latent_norm,
+                             init, start, timing)
     return sample_with_scheduler(model, scheduler, n_inf, batch_shape, device, conditioning_mode=mode,
                                  conditioning_batch=conditioning_batch, latent_norm=latent_norm, timing=timing,
                                  start_step=start_step, last_n_steps=last_n_steps, init_sample=init)
 
 
-def _fused_flow_decode(model, scheduler, n_inf, batch_shape, device, mode, cond, latent_norm):
-    """The FlowMatchEuler schedule as one graph-replayed step (FusedFlowSampler): identical arithmetic to the
-    generic loop (conditioning aligned / normalised the same way), one host launch per step."""
-    from ...pipelines.train.fused import FusedFlowSampler
+def _fused_decode(model, scheduler, n_inf, batch_shape, device, mode, cond, latent_norm, init, start, timing):
+    """The schedule (or its selected tail, from step ``start``) as one graph-replayed step (FusedSampler): the
+    generic loop's arithmetic with the conditioning aligned / normalised the same way, one host launch per
+    step; ``timing`` gets the loop's model_seconds / model_calls."""
+    from ...pipelines.train.fused import FusedSampler
     from ...pipelines.utils import _align_conditioning, normalize_latent_conditioning
-    init = torch.randn(batch_shape, device=device)
+    init = init.to(device) if init is not None else torch.randn(batch_shape, device=device)
     cond = _align_conditioning(cond, init.size(0))
     cat = cca = None
     if mode == "concatenate" and cond is not None:
         cat = cond.to(device)
     elif mode == "attention" and cond is not None:
         cca = normalize_latent_conditioning(cond.to(device), latent_norm)
-    sampler = FusedFlowSampler(model, n_inf, scheduler.config.num_train_timesteps)
-    return sampler.sample(init, cat, use_graph=True, context_ca=cca).clone()
+    sampler = FusedSampler(model, scheduler, n_inf, start=start)
+    return sampler.sample(init, cat, use_graph=True, context_ca=cca, timing=timing)
 
 
 def warn_attention_conditioning_shape(conditioning_batch: Optional[torch.Tensor], model_cfg: dict) -> bool:

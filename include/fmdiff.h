@@ -380,6 +380,33 @@ typedef struct {
   int64_t n;
 } fmd_lincomb_desc;
 int fmd_lincomb(const fmd_lincomb_desc* d, fmd_stream_t s);
+/* One multistep-solver step with every scalar taken from row index[0] of a per-step coefficient table, so a
+ * whole DPM-Solver / UniPC sampling loop replays from one captured step (the graph-replayed form of the
+ * DPMSolverMultistepScheduler.step / UniPCMultistepScheduler.step arithmetic, reference call site
+ * src/pipelines/utils.py:218).  Per element of the sample (step i = index[0], r(j) = ring[j & 3]):
+ *   m      = c[0]*x + c[1]*eps                                   (data prediction; dpmsolver: eps itself)
+ *   r(i)   = m
+ *   xc     = c[2] != 0 ? c[3]*last + c[4]*r(i-1) + c[5]*r(i-2) + c[6]*r(i-3) + c[7]*m : x   (UniPC corrector)
+ *   last   = xc                                                  (if last != NULL)
+ *   x      = c[8]*xc + c[9]*r(i) + c[10]*r(i-1) + c[11]*r(i-2)   (predictor / solver update)
+ * each sum accumulated left to right from 0 with fused multiply-adds, as fmd_lincomb does, so the step equals
+ * the eager scheduler's fmd_lincomb calls on the same coefficients.  x: [N][Cx][HW] fp32; eps: the UNet
+ * output [N*HW][Kpad] fp32; ring / last: [N][Cx][HW] fp32; next (optional): the next model input
+ * (NHWC bf16 [N*HW][Cpad], x then cond channels, zero padded) as fmd_flow_euler writes it. */
+#define FMD_SCHED_NCOEF 12
+typedef struct {
+  float* x;
+  const float* eps;
+  float* ring[4];
+  float* last;
+  const float* coef;        /* [steps][FMD_SCHED_NCOEF] */
+  const int32_t* index;
+  int32_t N, Cx, HW, Kpad;
+  const float* cond;
+  int32_t Cc, Cpad;
+  void* next;
+} fmd_sched_step_desc;
+int fmd_sched_step(const fmd_sched_step_desc* d, fmd_stream_t s);
 /* out[0:n] = table[index[0]*n : (index[0]+1)*n] -- a per-step row (e.g. precomputed time embeddings of a
  * sampling schedule) selected by a device-side step counter, so the step stays graph-replayable. */
 int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s);

@@ -1,0 +1,91 @@
+"""Child process of tests/test_gpu_dp.py (not collected by pytest): one data-parallel rank of FusedTrainStep.
+
+    python tests/dp_worker.py --world W --rank R --out FILE [--steps S]
+
+Env: MASTER_ADDR / MASTER_PORT (world > 1).  Every rank uses cuda:0 (the test box has one GPU) and the
+gloo backend, so the split capture, the per-bucket backward graphs, the overlapped async bucket all-reduces
+and the 1/world AdamW scaling all run exactly as on the 8-GPU node, only the transport differs.
+
+The model is the tiny LDCT config of tests/golden/golden.json (``ldct_fm_test``) with the oracle's seeded
+weights; the global batch (GLOBAL images) and every step's injected eps / t are drawn from a fixed seed,
+and rank R trains on images [R*GLOBAL/W, (R+1)*GLOBAL/W) of each step's batch.  Writes the flat fp32
+parameters after every step, the last step's (all-reduced, summed) gradient and the world size.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "flow-matching-and-diffusion-models_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GLOBAL = 4
+IMG = 32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    from oracle import spec as S
+    from oracle import unet as U
+
+    torch.cuda.set_device(0)
+    if a.world > 1:
+        dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
+    meta = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["ldct_fm_test"]
+    tr_cfg = meta["training"]
+    ch = tr_cfg["channels"] or 1
+    model = DiffusionUNetFactory().build(meta["unet"], tr_cfg["conditioning"], ch).to("cuda")
+    model.load_state_dict(U.seeded_state_dict(S.derive_spec(meta["unet"], tr_cfg["conditioning"], ch), meta["seed"]))
+    step = FusedTrainStep(model, lr=1e-3, warmup=0, total_steps=100,
+                          process_group=dist.group.WORLD if a.world > 1 else None)
+
+    g = torch.Generator().manual_seed(77)
+    batches = []
+    for _ in range(a.steps):
+        clean = torch.rand(GLOBAL, 1, IMG, IMG, generator=g)
+        ldct = (clean + 0.05 * torch.randn(GLOBAL, 1, IMG, IMG, generator=g)).clamp(0, 1)
+        noise = torch.randn(GLOBAL, 1, IMG, IMG, generator=g)
+        t = torch.rand(GLOBAL, generator=g)
+        batches.append((clean, ldct, noise, t))
+    per = GLOBAL // a.world
+    sl = slice(a.rank * per, (a.rank + 1) * per)
+
+    def local(i):
+        return tuple(v[sl].contiguous().to("cuda") for v in batches[i])
+
+    c0, l0, n0, t0 = local(0)
+    step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0)
+    params, losses = [], []
+    for i in range(a.steps):
+        c, l, n, t = local(i)
+        loss = step.replay(clean=c, ldct=l, noise=n, t=t)
+        torch.cuda.synchronize()
+        params.append(torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu())
+        losses.append(float(loss.item()))
+    grad = torch.cat([p.grad.detach().reshape(-1) for p in model.parameters()]).cpu()
+    torch.save({"params": torch.stack(params), "grad": grad, "losses": torch.tensor(losses),
+                "world": a.world, "overlap": bool(step.overlap), "split": bool(step._split),
+                "buckets": len(step.seg_buckets) if step.seg_buckets else 0,
+                "numels": torch.tensor([p.numel() for p in model.parameters()])}, a.out)
+    if a.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

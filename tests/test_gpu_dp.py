@@ -1,0 +1,109 @@
+"""The N-rank train step numerically (N-GPU step == one process on the concatenated batch).
+
+Two fresh child processes (tests/dp_worker.py; gloo, both ranks on cuda:0 -- the box has one GPU) run
+``FusedTrainStep`` exactly as the 8-GPU node does: split capture in thread-local mode, the backward cut into
+per-bucket graphs, each bucket's all-reduce issued async while the next bucket's segments replay, AdamW
+with the 1/world scaling.  A third child runs world 1 on the concatenated batch (the same global images,
+eps and t every step).  Reference: ``flow_matching_lib.py:81`` (DistributedSampler sharding); the gradient
+exchange itself is this build's addition (dp.py header).
+
+Checks, over 2 replayed steps:
+* the two ranks hold bit-identical parameters after every step (they applied the same summed gradient);
+* the summed gradient / world vs the world-1 gradient: relative L2 < 2e-2 and per-tensor cosine > 0.999
+  (the ranks run batch 2 where world 1 runs batch 4, so split-K / tiling choices -- and with them the bf16
+  rounding of activations -- may differ; a missing, stale or double-counted bucket would be O(1) off);
+* parameter updates (p_step - p_0) vs world 1: cosine > 0.99 per step (the first AdamW step is ~lr*sign(g),
+  so elements whose gradient is at round-off level may flip);
+* the mean of the ranks' local losses vs the world-1 loss within 1e-2 relative.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(REPO, "tests", "dp_worker.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, out_dir, timeout=240):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    procs, outs = [], []
+    for r in range(world):
+        out = os.path.join(out_dir, f"w{world}_r{r}.pt")
+        log = open(os.path.join(out_dir, f"w{world}_r{r}.log"), "w")
+        procs.append((subprocess.Popen([sys.executable, WORKER, "--world", str(world), "--rank", str(r),
+                                        "--out", out], env=env, stdout=log, stderr=subprocess.STDOUT), log))
+        outs.append(out)
+    try:
+        for p, _ in procs:
+            p.wait(timeout=timeout)
+    finally:
+        for p, log in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            log.close()
+    for r, (p, _) in enumerate(procs):
+        if p.returncode != 0:
+            print(open(os.path.join(out_dir, f"w{world}_r{r}.log")).read()[-4000:])
+        assert p.returncode == 0, (world, r, p.returncode)
+    return [torch.load(o, weights_only=True) for o in outs]
+
+
+def _cos(a, b):
+    a, b = a.double(), b.double()
+    return float((a @ b) / (a.norm() * b.norm() + 1e-300))
+
+
+def test_two_rank_overlapped_step_equals_concatenated_batch(tmp_path):
+    (one,) = _run(1, str(tmp_path))
+    r0, r1 = _run(2, str(tmp_path))
+    assert r0["world"] == 2 and r0["split"] and r0["overlap"] and r0["buckets"] >= 2
+    assert torch.equal(r0["params"], r1["params"]), "ranks diverged: the all-reduced gradient differs"
+    assert torch.equal(r0["grad"], r1["grad"])
+    g2 = r0["grad"].double() / 2
+    g1 = one["grad"].double()
+    rel = float((g2 - g1).norm() / g1.norm())
+    worst = 1.0
+    off = 0
+    total = g1.norm()
+    for n in r0["numels"].tolist():
+        a, b = g2[off:off + n], g1[off:off + n]
+        if b.norm() > 1e-4 * total:
+            worst = min(worst, _cos(a, b))
+        off += n
+    print(f"summed gradient / world vs world 1: rel L2 {rel:.3e}, worst per-tensor cosine {worst:.6f}")
+    assert rel < 2e-2 and worst > 0.999
+    p0 = _initial_params()
+    for s in range(one["params"].shape[0]):
+        c = _cos(r0["params"][s].double() - p0, one["params"][s].double() - p0)
+        print(f"step {s + 1}: update cosine world 2 vs world 1 {c:.5f}")
+        assert c > 0.99
+    lw2 = (r0["losses"] + r1["losses"]) / 2
+    print(f"losses world 1 {one['losses'].tolist()} vs mean of ranks {lw2.tolist()}")
+    assert torch.allclose(lw2, one["losses"], rtol=1e-2)
+
+
+def _initial_params():
+    import json
+    sys.path.insert(0, REPO)
+    from oracle import spec as S
+    from oracle import unet as U
+    from fmdiff.models.generators import DiffusionUNetFactory
+    meta = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["ldct_fm_test"]
+    tr = meta["training"]
+    ch = tr["channels"] or 1
+    model = DiffusionUNetFactory().build(meta["unet"], tr["conditioning"], ch)
+    model.load_state_dict(U.seeded_state_dict(S.derive_spec(meta["unet"], tr["conditioning"], ch), meta["seed"]))
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()]).double()

@@ -214,7 +214,7 @@ def _dp_worker(rank, world, port, meta, tensors, q):
             w.wait()
         flat /= world                                                     # grad_scale folded into AdamW on GPU
         if rank == 0:
-            q.put(flat)
+            q.put(flat.numpy().copy())   # plain bytes: a shared-memory tensor dies with this process
     finally:
         dist.destroy_process_group()
 
@@ -232,7 +232,7 @@ def test_dp_allreduce_equals_global_batch(golden):
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, meta, tensors, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    got = torch.from_numpy(q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
