@@ -185,6 +185,9 @@ def main():
         dist.init_process_group(os.environ.get("FMD_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", dev_idx)
     torch.cuda.set_device(dev)
+    # all work on a created stream: collectives after graph replays on the legacy null stream were measured to
+    # corrupt gradient buckets on this stack (fused.py _own_stream)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     from fmdiff.models.generators import DiffusionUNetFactory
     from fmdiff.pipelines.train.fused import FusedFlowSampler, FusedTrainStep

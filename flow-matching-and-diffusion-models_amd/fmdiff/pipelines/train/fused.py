@@ -19,6 +19,7 @@ buckets.
 """
 from __future__ import annotations
 
+import functools
 import math
 import time
 from typing import Optional
@@ -29,6 +30,35 @@ from ...runtime import ops
 from ...runtime.dp import bucketed_allreduce, bucketed_allreduce_async, world_size
 from ...runtime.engine import get_engine
 from ..schedulers import SCHED_NCOEF
+
+
+
+def _own_stream(fn):
+    """Run a public entry point on the object's private HIP stream when the caller is on the device's default
+    (legacy null) stream, handing off with stream waits at entry and exit.
+
+    Measured on MI355X / ROCm 7.x (tests/test_gpu_dp.py, tools/dp_debug.py): with the train step replayed on the
+    null stream, a collective issued afterwards (ProcessGroupGloo's CUDA all-reduce: event on the current stream
+    -> copy on its own stream -> event back) intermittently returned corrupted gradient buckets (norms of 1e16 /
+    inf at step 2), even with a host synchronisation between the replay and the all-reduce; the same steps on a
+    created stream were bit-identical to the eager reference in every run.  Every path of this module
+    therefore issues its graphs, collectives and kernels on a created stream."""
+    @functools.wraps(fn)
+    def wrapped(self, *a, **kw):
+        cur = torch.cuda.current_stream()
+        if cur != torch.cuda.default_stream(cur.device):
+            return fn(self, *a, **kw)
+        st = self.__dict__.get("_work_stream")
+        if st is None or st.device != cur.device:
+            st = self._work_stream = torch.cuda.Stream(device=cur.device)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            out = fn(self, *a, **kw)
+        cur.wait_stream(st)
+        if torch.is_tensor(out):
+            out.record_stream(cur)   # produced on st, consumed on the caller's stream
+        return out
+    return wrapped
 
 
 class FlatParams:
@@ -174,6 +204,7 @@ class FusedTrainStep:
     def _allreduce(self):
         bucketed_allreduce(self.flat.grad, self.buckets, self.pg)
 
+    @_own_stream
     def step(self, clean, ldct, noise=None, t=None, context_ca=None):
         """One optimizer step on (clean, ldct) [N,C,H,W] fp32 device tensors; returns the last chunk's loss.
         ``context_ca``: cross-attention conditioning (conditioning "attention", e.g. VAE latents)."""
@@ -299,6 +330,7 @@ class FusedTrainStep:
         self.step_ctr.fill_(steps)
 
     # ---------------------------------------------------------- hipGraph
+    @_own_stream
     def capture(self, clean, ldct, warmup_iters: int = 2, split_collectives: Optional[bool] = None,
                 context_ca=None, noise=None, t=None):
         """Capture one step into a hipGraph.  Single process: the whole step (RNG, forward, loss, backward,
@@ -346,6 +378,7 @@ class FusedTrainStep:
                     self._bwd_bucket(b)
                 self._graphs.append(gb)
 
+    @_own_stream
     def replay(self, clean=None, ldct=None, context_ca=None, noise=None, t=None):
         for i, new in ((0, clean), (1, ldct), (2, noise), (3, t), (4, context_ca)):
             if new is None:
@@ -491,6 +524,7 @@ class FusedSampler:
         from ..schedulers import UniPCMultistepScheduler
         return isinstance(self.sched, UniPCMultistepScheduler)
 
+    @_own_stream
     @torch.no_grad()
     def sample(self, init: torch.Tensor, cond: Optional[torch.Tensor] = None, use_graph: bool = True,
                context_ca: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None, generator=None,

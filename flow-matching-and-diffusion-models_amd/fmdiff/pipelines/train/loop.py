@@ -77,7 +77,7 @@ def _save_grid(t: torch.Tensor, path: Path) -> None:
 def run_training(dataset, json_path, val_dataset=None, resume: Optional[str] = None, *, objective: str,
                  step_factory: Optional[Callable] = None, use_graph: Optional[bool] = None):
     """Train on ``dataset`` (items: dicts with ``target`` [C,*S] and ``image`` (conditioning or = target))."""
-    model_type, prefix, default_out, log_name = _KIND[objective]
+    model_type = _KIND[objective][0]
     logging.basicConfig(level=logging.INFO, format="%(asctime)s | %(levelname)s | %(message)s", force=True)
     cfg = U.load_json_config(json_path)
     if "model" not in cfg:
@@ -91,6 +91,20 @@ def run_training(dataset, json_path, val_dataset=None, resume: Optional[str] = N
     U.setup_distributed(tr.get("dist_backend"))
     U.set_seed(tr.get("seed"))
     device = U.resolve_device(tr.get("manual_device"), torch.device("cuda" if torch.cuda.is_available() else "cpu"))
+    if device.type == "cuda" and torch.cuda.current_stream(device) == torch.cuda.default_stream(device):
+        # the whole loop (prefetch hand-off, graph replays, epoch reductions) on a created stream: collectives
+        # next to graph replays on the legacy null stream were measured to corrupt data (fused.py _own_stream)
+        work = torch.cuda.Stream(device)
+        work.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(work):
+            out = _train_loop(dataset, val_dataset, resume, cfg, tr, mblock, objective, step_factory, use_graph, device)
+        torch.cuda.current_stream(device).wait_stream(work)
+        return out
+    return _train_loop(dataset, val_dataset, resume, cfg, tr, mblock, objective, step_factory, use_graph, device)
+
+
+def _train_loop(dataset, val_dataset, resume, cfg, tr, mblock, objective, step_factory, use_graph, device):
+    model_type, prefix, default_out, log_name = _KIND[objective]
     batch_size = U.resolve_batch_size(tr, "train_batch_size", tr.get("batch_size", 4))
     num_workers = int(tr.get("num_workers", 4))
     epochs = int(tr.get("num_epochs", tr.get("epochs", 1)))

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--rank", type=int, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--mode", default="graph", choices=["graph", "graph_plain", "eager", "eager_plain"],
+                    help="graph: capture + replay (the trainer's path); eager: step() with the overlapped exchange; "
+                         "eager_plain: step() with one blocking all-reduce after the backward")
     a = ap.parse_args()
 
     import torch
@@ -52,7 +55,8 @@ def main():
     model = DiffusionUNetFactory().build(meta["unet"], tr_cfg["conditioning"], ch).to("cuda")
     model.load_state_dict(U.seeded_state_dict(S.derive_spec(meta["unet"], tr_cfg["conditioning"], ch), meta["seed"]))
     step = FusedTrainStep(model, lr=1e-3, warmup=0, total_steps=100,
-                          process_group=dist.group.WORLD if a.world > 1 else None)
+                          process_group=dist.group.WORLD if a.world > 1 else None,
+                          overlap_allreduce=False if a.mode.endswith("_plain") else None)
 
     g = torch.Generator().manual_seed(77)
     batches = []
@@ -68,18 +72,27 @@ def main():
     def local(i):
         return tuple(v[sl].contiguous().to("cuda") for v in batches[i])
 
+    side = torch.cuda.Stream() if os.environ.get("FMD_DP_SIDE", "0") == "1" else None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(side)
     c0, l0, n0, t0 = local(0)
-    step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0)
-    params, losses = [], []
+    if a.mode.startswith("graph"):
+        step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0)
+    params, losses, gnorms = [], [], []
     for i in range(a.steps):
         c, l, n, t = local(i)
-        loss = step.replay(clean=c, ldct=l, noise=n, t=t)
+        if a.mode.startswith("graph"):
+            loss = step.replay(clean=c, ldct=l, noise=n, t=t)
+        else:
+            loss = step.step(c, l, noise=n, t=t)
         torch.cuda.synchronize()
         params.append(torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu())
+        gnorms.append(float(torch.cat([p.grad.detach().reshape(-1) for p in model.parameters()]).norm()))
         losses.append(float(loss.item()))
     grad = torch.cat([p.grad.detach().reshape(-1) for p in model.parameters()]).cpu()
-    torch.save({"params": torch.stack(params), "grad": grad, "losses": torch.tensor(losses),
-                "world": a.world, "overlap": bool(step.overlap), "split": bool(step._split),
+    torch.save({"params": torch.stack(params), "grad": grad, "losses": torch.tensor(losses), "gnorms": torch.tensor(gnorms),
+                "world": a.world, "overlap": bool(step.overlap), "split": bool(step._split), "mode": a.mode,
                 "buckets": len(step.seg_buckets) if step.seg_buckets else 0,
                 "numels": torch.tensor([p.numel() for p in model.parameters()])}, a.out)
     if a.world > 1:

@@ -101,7 +101,8 @@ def main():
     out.update({"step/clean": clean, "step/ldct": ldct, "step/noise": noise, "step/t": tt,
                 "step/loss": loss.detach(), "step/param_sum_before": before, "step/param_sum_after": after,
                 "step/grad_sum": torch.stack([grads[k].double().sum() for k in names]),
-                "step/grad_sq": torch.stack([grads[k].double().pow(2).sum() for k in names])})
+                "step/grad_sq": torch.stack([grads[k].double().pow(2).sum() for k in names]),
+                "step/grad_l1": torch.stack([grads[k].double().abs().sum() for k in names])})
     small = [k for k in names if grads[k].numel() <= SMALL]
     for k in small:
         out[f"step/grad/{k}"] = grads[k]

@@ -100,6 +100,7 @@ def run_case(name, path, img, B, seed, ts_list):
         param_sum_before=before, param_sum_after=after,
         grad_sum=torch.stack([gg.double().sum() for gg in grads]),
         grad_sq=torch.stack([gg.double().pow(2).sum() for gg in grads]),
+        grad_l1=torch.stack([gg.double().abs().sum() for gg in grads]),
         proj_grad=P.projections(grads, seed), sample_grad=P.strided_sample(grads).float(),
         proj_delta=P.projections(deltas, seed + 1), sample_delta=P.strided_sample(deltas).float()).items()}
     small = [k for k, gg in zip(names, grads) if gg.numel() <= SMALL]

@@ -35,15 +35,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, out_dir, timeout=240):
+def _run(world, out_dir, timeout=240, mode="graph"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
     procs, outs = [], []
     for r in range(world):
-        out = os.path.join(out_dir, f"w{world}_r{r}.pt")
+        out = os.path.join(out_dir, f"w{world}_r{r}_{mode}.pt")
         log = open(os.path.join(out_dir, f"w{world}_r{r}.log"), "w")
         procs.append((subprocess.Popen([sys.executable, WORKER, "--world", str(world), "--rank", str(r),
-                                        "--out", out], env=env, stdout=log, stderr=subprocess.STDOUT), log))
+                                        "--out", out, "--mode", mode, "--steps", os.environ.get("FMD_DP_STEPS", "2")], env=env, stdout=log, stderr=subprocess.STDOUT), log))
         outs.append(out)
     try:
         for p, _ in procs:
@@ -69,6 +69,9 @@ def _cos(a, b):
 def test_two_rank_overlapped_step_equals_concatenated_batch(tmp_path):
     (one,) = _run(1, str(tmp_path))
     r0, r1 = _run(2, str(tmp_path))
+    for name, r in (("world 1", one), ("rank 0", r0), ("rank 1", r1)):
+        print(f"{name}: losses {r['losses'].tolist()} grad norms after each step {r['gnorms'].tolist()} "
+              f"final grad norm {float(r['grad'].norm()):.6f}")
     assert r0["world"] == 2 and r0["split"] and r0["overlap"] and r0["buckets"] >= 2
     assert torch.equal(r0["params"], r1["params"]), "ranks diverged: the all-reduced gradient differs"
     assert torch.equal(r0["grad"], r1["grad"])

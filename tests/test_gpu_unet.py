@@ -103,8 +103,9 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_bef
     reference values are fp32 round-off, so they are only required to stay below ``dead_bound`` x the
     whole-model norm on the GPU (bf16 round-off of an exact cancellation).  For every other ("live") tensor:
 
-    * gradient sum: |sum(g) - sum(g_ref)| <= tol_sum * ||g_ref|| (the sum of an error vector e of random
-      signs is ~||e||; bf16 round-off gives ||e|| ~ 1e-2 ||g||);
+    * gradient sum: |sum(g) - sum(g_ref)| <= tol_sum * ||g_ref||_1 (|sum e| <= ||e||_1, and the bf16 path's
+      L1 error is ~1e-2 of ||g||_1 like its L2 error; an L2-scaled bound does not hold: a rounding bias of
+      1e-3 per element that is common to a tensor adds up to ~1e-3 sqrt(n) ||g||_2 in the sum);
     * gradient norm within tol_sq relative;
     * fingerprints (tests/golden/projections.py), for tensors of more than 4096 elements (smaller ones are
       compared in full): cosine >= cos_grad between the 8 seeded Rademacher projections of g and of g_ref,
@@ -136,9 +137,10 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_bef
             worst_dead = max(worst_dead, gn / total)
             continue
         live.add(k)
-        worst_sum = max(worst_sum, abs(g.sum().item() - rs) / math.sqrt(rq))
+        l1 = T[f"{prefix}/grad_l1"][i].item() if f"{prefix}/grad_l1" in T else math.sqrt(numel[k] * rq)
+        worst_sum = max(worst_sum, abs(g.sum().item() - rs) / l1)
         worst_sq = max(worst_sq, abs(gn - math.sqrt(rq)) / math.sqrt(rq))
-    print(f"grad sums over {len(live)} tensors: worst |d sum| / ||g|| {worst_sum:.3e}, worst relative "
+    print(f"grad sums over {len(live)} tensors: worst |d sum| / ||g||_1 {worst_sum:.3e}, worst relative "
           f"norm error {worst_sq:.3e}; {len(names) - len(live)} ~0-gradient tensors, worst norm {worst_dead:.2e} x total")
     assert worst_sum < tol_sum and worst_sq < tol_sq and worst_dead < dead_bound
     worst_cos = 1.0
