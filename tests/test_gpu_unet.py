@@ -94,7 +94,7 @@ def test_train_step_gradients_vs_oracle(golden):
 
 def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_before=None, tol_sum=5e-2,
                           tol_sq=5e-2, flip_frac=0.05, negligible=1e-5, dead_bound=1e-3, cos_grad=0.99,
-                          cos_delta=0.99):
+                          cos_delta=0.85):
     """Loss, per-parameter gradient statistics, element-order-sensitive gradient / AdamW-delta fingerprints
     and post-AdamW parameter sums of a finished FusedTrainStep vs a reference-generated fixture.
 
@@ -112,10 +112,15 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_bef
       and between g and g_ref on the fixture's strided sample (every 397th element of the concatenation;
       tensors with >= 8 sampled elements).  Sums and norms are permutation-invariant, these are not: a tap-
       or channel-permuted weight gradient has cosine ~0;
-    * AdamW parameter delta (p_after - p_before): the same two cosines against the reference's delta
-      (>= cos_delta), and the per-tensor change of the parameter sum may differ from the reference's by at
-      most ``flip_frac`` of the elements flipping sign (the first AdamW step moves each element by
-      ~lr * sign(g), 2 lr per flip)."""
+    * AdamW parameter delta (p_after - p_before), two ways.  (1) Against the reference's delta: the two
+      fingerprint cosines >= cos_delta.  The first AdamW step moves every element by lr * g / (|g| + eps) ~
+      lr * sign(g), so this cosine is 1 - 2 x (fraction of elements whose gradient sign differs): elements
+      whose gradient is at bf16 round-off level flip (measured worst 0.90 - 0.97 per tensor on configs A-C,
+      i.e. 1.5 - 5 % flips) while a misplaced or permuted update gives ~0.  (2) Against AdamW applied in fp64
+      to the GPU's own gradient (which the gradient fingerprints pin to the reference at cosine >= cos_grad):
+      every element within 2 fp32 ulps of |p| plus 1e-3 lr -- the optimizer itself is exact, so the chain
+      g_ref ~ g -> delta is closed.  The per-tensor change of the parameter sum may differ from the
+      reference's by at most ``flip_frac`` of the elements flipping sign (2 lr per flip)."""
     import sys
     sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "golden"))
     import projections as P
@@ -180,6 +185,17 @@ def _check_step_vs_golden(model, T, m, prefix, loss, lr_eff, *, small=(), sd_bef
         deltas = [params[k].detach().double().cpu() - sd_before[k].double() for k in names]
         fingerprint(deltas, T[f"{prefix}/proj_delta"], T[f"{prefix}/sample_delta"], seed_d, "AdamW deltas",
                     cos_delta)
+        # (2) the update is AdamW step 1 of the GPU's own gradient: p - lr*wd*p - lr * g / (|g| + eps)
+        wd, eps = float(m.get("weight_decay", 0.0)), 1e-8
+        worst = 0.0
+        for k, dl in zip(names, deltas):
+            p0 = sd_before[k].double()
+            g = params[k].grad.detach().double().cpu()
+            want = -lr_eff * wd * p0 - lr_eff * g / (g.abs() + eps)
+            tol = 2.0 * p0.abs().clamp_min(1e-30) * 2.0 ** -23 + 1e-3 * lr_eff
+            worst = max(worst, ((dl - want).abs() / tol).max().item())
+        print(f"AdamW delta vs fp64 AdamW of the GPU gradient: worst |error| / (2 ulp(p) + 1e-3 lr) {worst:.3f}")
+        assert worst <= 1.0
         del deltas
     worst_flip = 0.0
     for i, k in enumerate(names):
