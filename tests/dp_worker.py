@@ -47,6 +47,9 @@ def main():
     from oracle import unet as U
 
     torch.cuda.set_device(0)
+    # as bench.py and the trainer loop do: all work on a created stream (graph replays and collectives on the
+    # legacy null stream corrupted gradient buckets on this stack)
+    torch.cuda.set_stream(torch.cuda.Stream())
     if a.world > 1:
         dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
     meta = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["ldct_fm_test"]
@@ -72,10 +75,6 @@ def main():
     def local(i):
         return tuple(v[sl].contiguous().to("cuda") for v in batches[i])
 
-    side = torch.cuda.Stream() if os.environ.get("FMD_DP_SIDE", "0") == "1" else None
-    if side is not None:
-        side.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(side)
     c0, l0, n0, t0 = local(0)
     if a.mode.startswith("graph"):
         step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0)

@@ -7,7 +7,9 @@ mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 if [ -z "$SKIP_TESTS" ]; then
-  step tests timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -rA > gpurun_out/gpu_tests.log 2>&1
+  # no -x: every GPU test reports (a failing test does not stop the smoke / bench / profile steps)
+  timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rA > gpurun_out/gpu_tests.log 2>&1
+  rc=$?; echo "tests rc=$rc"; [ $rc -le 1 ] || exit $rc
   step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 fi
 step bench timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_out/bench.json 2> gpurun_out/bench.err
