@@ -39,8 +39,6 @@ constexpr int TH = 16, TW = 16;           // output tile
 constexpr int BCO = 128;                  // output channels per tile
 constexpr int BK = FMD_HALO_BK;           // input channels per chunk (32)
 constexpr int KC = BK / 8;                // 16-byte chunks per position (4)
-// Workgroup: NT = 512 (8 waves of 64 couts x 4 rows, 128 VGPRs, 4 waves/SIMD) or NT = 256 (4 waves of
-// 64 couts x 8 rows: twice the MFMAs per fragment read and 256 VGPRs for addresses / prefetch, 2 waves/SIMD).
 constexpr int HALO = (TH + 2) * (TW + 2); // 324 positions
 constexpr int HPAD = 336;                 // plane stride (rows): == 0 mod 16 bank slots
 constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer (21 KiB)
@@ -61,8 +59,6 @@ struct HArgs {
                           // kz, 32-channel block cb) = kz*ncb + cb, reading logical input slice z + kz - 1
                           // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
-  int ntiles;                  // workgroups of the first dispatch round (those that take part in the stagger)
-  int stagger;                 // s_sleep(127) rounds the second first-round workgroup of a CU waits
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
 };
@@ -74,7 +70,6 @@ struct HArgs {
 #endif
 
 static int g_dbg = 0;
-static int g_nt = 512;   // workgroup size of the halo conv (fmd_halo_set_workgroup; FMD_HALO_NT at load)
 
 // staged piece h (16 bytes) of a chunk: blocks of 32 = 8 consecutive positions x KC channel groups
 FMD_DEV int piece_pos(int h) { return (h >> 5) * 8 + (h & 7); }
@@ -102,41 +97,15 @@ FMD_DEV void step_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Workgroup: 8 waves = 2 cout halves (64 couts) x 4 pixel-row groups (4 tile rows), 128 VGPRs, 4 waves/SIMD
+constexpr int NT = 512;
+constexpr int WR = 4;    // output rows per wave
+constexpr int NWH = 4;   // waves per cout half
+
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
-template <int NT>
-struct HaloCfg {
-  static constexpr int NW = NT / 64;           // waves
-  static constexpr int WR = 16 / (NW / 2);     // output rows per wave (4 | 8)
-  static constexpr int EPW = NT == 512 ? 4 : 2;
-};
-
-// per-CU arrival counters of the first-round stagger (monotonic; parity only)
-__device__ unsigned g_cu_ticket[2048];
-
-// First-round stagger: the second workgroup of each CU in the first dispatch round (blockIdx < first_round,
-// the odd ticket of a per-CU arrival counter) starts `stagger` s_sleep(127) rounds late.  Every later workgroup
-// takes the CU slot its predecessor frees, so the two slots of a CU stay out of phase and one slot's
-// prologue / epilogue (exposed loads, HBM-bound store and side-load bursts) overlaps the other's MFMAs.
-FMD_DEV void first_round_stagger(int first_round, int stagger, int* flag) {
-  if (stagger <= 0 || (int)blockIdx.x >= first_round || blockIdx.y != 0) return;
-  if (threadIdx.x == 0) {
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: cu 11:8, sh 12, se 15:13
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // XCC_ID 3:0
-    const unsigned key = ((((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15));
-    *flag = (int)(atomicAdd(&g_cu_ticket[key], 1u) & 1u);
-  }
-  __syncthreads();
-  const int late = *(volatile int*)flag;
-  __syncthreads();
-  if (late)
-    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
-}
-
-template <bool UP, int PRO, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(HaloCfg<NT>::EPW, HaloCfg<NT>::EPW)))
+template <bool UP, int PRO>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void conv3x3_halo(const HArgs A) {
-  constexpr int WR = HaloCfg<NT>::WR;
-  constexpr int NWH = HaloCfg<NT>::NW / 2;                 // waves per cout half
   constexpr int WDMA = WBUF / (NT * 8);                    // 16-byte weight DMAs per thread per tap
   static_assert(WDMA * NT * 8 == WBUF, "weight tile DMA split");
   constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
@@ -158,7 +127,6 @@ void conv3x3_halo(const HArgs A) {
   const fmd_conv_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wco = wid / NWH, wpx = wid % NWH;   // 2 x NWH waves: 64 couts x WR pixel rows each
-  first_round_stagger(A.ntiles, A.stagger, (int*)(smem + SM_EPI));
   const int l16 = lane & 15, lq = lane >> 4;
   const int kc = piece_kc(tid);              // staged pieces start at multiples of 32: the channel group is fixed
 
@@ -323,24 +291,11 @@ void conv3x3_halo(const HArgs A) {
       }
       return *(const bf16x8*)(hb + (lq * HPAD + pos) * 8);
     };
-    if constexpr (NT == 256) {
-      // all WR row fragments read up front (256-VGPR variant): their LDS latency overlaps the MFMAs
-      bf16x8 bv[WR];
 #pragma unroll
-      for (int j = 0; j < WR; ++j) bv[j] = bfrag(j);
-      __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them)
+    for (int j = 0; j < WR; ++j) {
+      const bf16x8 bv = bfrag(j);
 #pragma unroll
-      for (int j = 0; j < WR; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv[j], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);   // and keep later waits (halo consume) out of the MFMA block
-    } else {
-#pragma unroll
-      for (int j = 0; j < WR; ++j) {
-        const bf16x8 bv = bfrag(j);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
-      }
+      for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(af[i], bv, acc[i][j]);
     }
   };
 
@@ -670,526 +625,6 @@ void conv3x3_halo(const HArgs A) {
   }
 }
 
-// ============================================================================================================
-// v2: the same tile / chunk / staging pipeline on v_mfma_f32_32x32x16_bf16 (2-D problems).
-//
-// Why: the 16x16x32 MFMA holds its SIMD's vector issue for 8 of its 16 cycles, the 32x32x16 one for 8 of 32
-// (MI355X_MICROARCH.md cycle constants), so at equal FLOPs the 32x32 form leaves 1.5x the VALU issue slots
-// for the GN+SiLU staging transform that this kernel carries beside its MFMAs (PMC: the v1 loop is
-// VALU-issue-bound).  The loop is also re-cut so every tap is a compile-time constant: fragment addresses
-// are one per-lane base register + immediate offsets, and the per-thread halo staging offsets are computed
-// once per workgroup, not per chunk.
-//
-// Wave w (8 waves): cout half wco = w >> 2 (64 couts), pixel group g = w & 3.  Per tap a wave runs
-// 2 (32-cout blocks c) x 2 (32-pixel blocks b) x 2 (16-channel k-steps) MFMAs.  Pixel block b of wave g is
-// tile rows {g + 8b, g + 8b + 4}; MFMA column n (= lane & 31) is row g + 8b + 4(n >> 4), column
-// (n & 15) ^ 8(n >> 4): the second row's columns are rotated by 8 so that, with the 18-position halo row
-// pitch (4 rows = 72 positions = 8 mod 16 bank slots), every ds_read_b128 lane group of gfx950 hits 16
-// distinct 16-byte bank slots for every tap.  Accumulator register i of block (c, b) is cout
-// 32c + (i & 3) + 8(i >> 2) + 4h (h = lane >> 5) of the wave's half, the column's pixel.
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-FMD_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// Sum over each 32-lane half with DPP: lanes 31 and 63 receive the totals of lanes 0-31 / 32-63.
-FMD_DEV float half32_sum_to_last(float v) {
-  v = row16_sum_to_last(v);
-  // row_bcast:15 (gfx9 DPP 0x142): rows 1 and 3 (row_mask 0xa) add lane 15 of the row before them
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xa, 0xf, false));
-  return v;
-}
-
-
-template <bool UP, int PRO>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
-void conv3x3_halo_v2(const HArgs A) {
-  constexpr int NT = 512;
-  constexpr int WDMA = WBUF / (NT * 8);                    // 16-byte weight DMAs per thread per tap (1)
-  constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;          // halo row width (10 | 18)
-  constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : HALO;   // positions of a main chunk (100 | 324)
-  constexpr int TOT1 = ((HPOS + 7) / 8) * 8 * KC;          // staged pieces of a main chunk
-  constexpr int PC1 = ((TOT1 + 3) / 4 + 31) & ~31;         // pieces staged per step (4 staging steps per chunk)
-  constexpr int LPRO = (TOT1 + NT - 1) / NT;               // pieces per thread for a whole chunk (prologue)
-  constexpr int SEG2 = TH * TW * KC;                       // pieces of a 1x1 chunk (1024)
-  static_assert(PC1 <= NT && WDMA == 1, "one staged piece and one weight DMA per thread and step");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  bf16r* const lds = (bf16r*)smem;
-  bf16r* const hbuf = (bf16r*)(smem + SM_H);
-  bf16r* const wbuf = (bf16r*)(smem + SM_W);
-  float* const coef = (float*)(smem + SM_COEF);
-  float* const epi = (float*)(smem + SM_EPI);
-  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
-
-  const fmd_conv_desc& d = A.d;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wco = wid >> 2, wpx = wid & 3;
-  const int cn = lane & 31, hh = lane >> 5, q = cn >> 4;
-  const int kc = piece_kc(tid);
-
-  // ---- stagger: the second workgroup of each CU in the first dispatch round (blockIdx < A.stagger_wgs, the
-  //      odd ticket of a per-CU arrival counter) starts A.stagger s_sleep(127) rounds late.  Every later
-  //      workgroup takes the CU slot its predecessor frees, so the two slots of a CU stay half a tile apart
-  //      and reach their epilogues (HBM-bound store / side-load bursts) while the other slot runs MFMAs.
-  first_round_stagger(A.ntiles, A.stagger, (int*)(smem + SM_EPI));
-  const int per_img = A.tiles_x * A.tiles_y;
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int tco = b % A.ntc;
-  const int tile = b / A.ntc;
-  const int n = tile / per_img;
-  const int tin = tile - n * per_img;
-  const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
-  const int co0 = tco * BCO;
-  const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;
-  const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
-  const int HWs = d.Hs * d.Ws;
-
-  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
-  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
-  const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
-  const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
-
-  if (PRO != 0) {
-    for (int i = tid; i < 2 * A.C; i += NT)
-      coef[i] = i < A.C ? d.pro_a[(size_t)n * A.C + i] : d.pro_b[(size_t)n * A.C + (i - A.C)];
-  }
-  if (tid < BCO) {
-    const int co = co0 + tid;
-    const bool ok = co < d.K;
-    float bsum = 0.f;
-    if (ok && d.bias) bsum += d.bias[co];
-    if (ok && d.bias2) bsum += d.bias2[co];
-    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)n * d.K + co];
-    epi[tid] = bsum;
-    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)n * d.K + co] : 0.f;
-    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)n * d.K + co] : 0.f;
-  }
-
-  // ---- weights: one 8 KiB tile per tap slot (9 per 3x3 chunk, then 1 per 1x1 chunk), DMA'd global -> LDS
-  const bf16r* const wsrc1 = A.wt + (size_t)tco * A.nchunk1 * 9 * WBUF + tid * 8;
-  const bf16r* const wsrc2 = A.wt2 + (size_t)tco * A.nchunk2 * WBUF + tid * 8;
-  const int T1 = A.nchunk1 * 9;
-  auto load_w = [&](int slot, int wtile) {
-    const bf16r* src = slot < T1 ? wsrc1 + (size_t)slot * WBUF : wsrc2 + (size_t)(slot - T1) * WBUF;
-    glds16(src, __builtin_amdgcn_readfirstlane(lds_base + SM_W + (unsigned)(wtile * WBUF + wid * 64 * 8) * 2));
-  };
-
-  // ---- per-thread staging geometry of a main chunk, fixed for the workgroup: staged piece of step ps
-  //      (0..3) is halo position ppos0 + ps * PC1 / 4 of channel group kc; spix[ps] = its image-relative
-  //      pixel, -1 = zero padding, -2 = nothing to store
-  const int ppos0 = piece_pos(tid);
-  int spix[4];
-#pragma unroll
-  for (int ps = 0; ps < 4; ++ps) {
-    const int pos = ppos0 + ps * (PC1 / 4);
-    const bool on = tid < PC1 && pos < HPOS && ps * PC1 + tid < TOT1;
-    const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-    const int y = hy0 + py, x = hx0 + px;
-    const bool valid = y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
-    spix[ps] = !on ? -2 : (valid ? y * d.Ws + x : -1);
-  }
-  const int loff0 = (kc * HPAD + ppos0) * 8;
-
-  // channel source of the chunk being staged (this thread's 8-channel group)
-  const bf16r* cptr = s0;
-  int cs = 0, cch = 0;
-  bool cok = false;
-  auto setup = [&](int chunk) {
-    if (chunk < A.nchunk1) {
-      const int c = chunk * BK + kc * 8;
-      cok = c < A.C;
-      cptr = !cok ? s0 : (c < d.C0) ? s0 + (size_t)n * HWs * d.C0 + c : s1 + (size_t)n * HWs * d.C1 + (c - d.C0);
-      cs = (c < d.C0) ? d.C0 : d.C1;
-      cch = cok ? c : 0;
-    } else {
-      const int c = (chunk - A.nchunk1) * BK + kc * 8;
-      const int HWo = d.Ho * d.Wo;
-      cok = c < A.C23;
-      cptr = !cok ? s2 : (c < d.C2) ? s2 + (size_t)n * HWo * d.C2 + c : s3 + (size_t)n * HWo * d.C3 + (c - d.C2);
-      cs = (c < d.C2) ? d.C2 : d.C3;
-      cch = 0;
-    }
-  };
-  auto transform = [&](u32x4 v, int c) -> u32x4 {
-    if (PRO != 0 && !HDBG(2)) {
-      const f32x4 a0 = *(const f32x4*)(coef + c), a1 = *(const f32x4*)(coef + c + 4);
-      const f32x4 b0 = *(const f32x4*)(coef + A.C + c), b1 = *(const f32x4*)(coef + A.C + c + 4);
-      const float ca[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const float cb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float lo = bf_lo(v[e]) * ca[2 * e] + cb[2 * e];
-        float hi = bf_hi(v[e]) * ca[2 * e + 1] + cb[2 * e + 1];
-        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-        v[e] = pack2(lo, hi);
-      }
-    }
-    return v;
-  };
-  u32x4 rh = u32x4{0u, 0u, 0u, 0u};
-  int rsp = -2;   // spix of the piece held in rh
-  auto load_piece = [&](int ps) {   // always one load (an in-bounds dummy when nothing is staged)
-    rsp = spix[ps];
-    const bool ld = rsp >= 0 && cok;
-    rh = *(const u32x4*)(cptr + (ld ? (size_t)rsp * cs : 0));
-  };
-  auto store_piece = [&](int buf, int ps, int c) {
-    asm volatile("" ::"v"(rh));
-    u32x4 v = transform(rh, c);
-    if (rsp == -1 || !cok) v = u32x4{0u, 0u, 0u, 0u};
-    if (rsp != -2) *(u32x4*)(hbuf + buf * HBUF + loff0 + ps * (PC1 / 4) * 8) = v;
-  };
-
-  // ---- fragment bases: weights [kc][co][8] (A, rows = couts), halo [kc plane][position][8] (B, cols = pixels)
-  const int abase = (hh * BCO + wco * 64 + cn) * 8;
-  const int px_r = wpx + 4 * q, px_x = (cn & 15) ^ (q << 3);   // pixel of column cn in block 0 (block 1: +8 rows)
-  const int bbase = (hh * HPAD + px_r * (TW + 2) + px_x) * 8;  // non-UP / 1x1 halo image (row pitch 18)
-  int ubase[3] = {0, 0, 0};                                      // UP: lane part of the 10-wide image, per kx
-  int uy[3] = {0, 0, 0};                                         // UP: wave part, per ky
-  if (UP) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      ubase[k] = (hh * HPAD + 2 * q * HROW + ((px_x + k - 1) >> 1) + 1) * 8;
-      uy[k] = ((((wpx + k - 1) >> 1) + 1) * HROW) * 8;
-    }
-  }
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[c][bb][i] = 0.f;
-
-  auto compute = [&](const bf16r* hb, const bf16r* wb, int tap, bool seg2) {
-    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-    bf16x8 af[2][2], bv[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) af[c][s] = *(const bf16x8*)(wb + abase + (2 * s * BCO + 32 * c) * 8);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const bf16r* p;
-        if (UP && !seg2) p = hb + ubase[kx] + uy[ky] + (4 * bb * HROW + 2 * s * HPAD) * 8;
-        else p = hb + bbase + ((8 * bb + ky) * (TW + 2) + kx + 2 * s * HPAD) * 8;
-        bv[bb][s] = *(const bf16x8*)p;
-      }
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) acc[c][bb] = mfma32(af[c][s], bv[bb][s], acc[c][bb]);
-  };
-
-  // ---- reduction range of this workgroup (split-K over 3x3 chunks; the 1x1 segment goes to the last split)
-  const int split = blockIdx.y;
-  const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
-  const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
-  const int slot_end = n_seg2 ? T1 + n_seg2 : c_hi * 9;
-
-  // ---- prologue: the full halo of the first chunk + the weights of its first step
-  __syncthreads();
-  setup(c_lo);
-  load_w(c_lo * 9, 0);
-  if (c_lo * 9 + 1 < slot_end) load_w(c_lo * 9 + 1, 1);
-  {
-    u32x4 pr[LPRO];
-    int po[LPRO];
-#pragma unroll
-    for (int k = 0; k < LPRO; ++k) {
-      const int h = tid + NT * k;
-      const int pos = piece_pos(h);
-      const bool on = h < TOT1 && pos < HPOS;
-      const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-      const int y = hy0 + py, x = hx0 + px;
-      const bool valid = on && cok && y >= 0 && y < d.Hs && x >= 0 && x < d.Ws;
-      pr[k] = *(const u32x4*)(cptr + (valid ? (size_t)(y * d.Ws + x) * cs : 0));
-      po[k] = !on ? -1 : ((piece_kc(h) * HPAD + pos) * 8) | (valid ? 0 : (1 << 30));
-    }
-#pragma unroll
-    for (int k = 0; k < LPRO; ++k) {
-      u32x4 v = transform(pr[k], cch);
-      if (po[k] & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
-      if (po[k] >= 0) *(u32x4*)(hbuf + (c_lo & 1) * HBUF + (po[k] & ~(1 << 30))) = v;
-    }
-  }
-  step_barrier<0>();
-
-  // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8); piece ps of the next chunk is loaded in step
-  //      ps and stored in step ps+1.  The wco 0 waves stage before their first tap, the wco 1 waves after it.
-  int wb = 0;
-  for (int chunk = c_lo; chunk < c_hi; ++chunk) {
-    const int nx = chunk + 1 < c_hi ? chunk + 1 : (chunk + 1 == c_hi && n_seg2 ? A.nchunk1 : -1);
-    const bool more = nx >= 0, nseg2 = nx >= A.nchunk1;
-    const bf16r* hb = hbuf + (chunk & 1) * HBUF;
-    int pc = 0;
-#pragma unroll
-    for (int ps = 0; ps < 5; ++ps) {
-      const int slot = chunk * 9 + 2 * ps;
-      const bf16r* w0 = wbuf + (2 * wb) * WBUF;
-      auto stage = [&]() {
-        if (more && ps > 0 && !nseg2) store_piece(nx & 1, ps - 1, pc);
-        const int nslot = ps < 4 ? slot + 2 : (nx < 0 ? slot_end : nx < A.nchunk1 ? nx * 9 : T1 + (nx - A.nchunk1));
-        if (nslot < slot_end && !HDBG(8)) {
-          load_w(nslot, 2 * (wb ^ 1));
-          if (nslot < T1 && (nslot - (nslot / 9) * 9) < 8) load_w(nslot + 1, 2 * (wb ^ 1) + 1);
-        }
-        if (ps == 0 && more) {
-          setup(nx);
-          pc = cch;
-        }
-        if (more && ps < 4 && !nseg2) load_piece(ps);
-      };
-      if (wco == 0) stage();
-      compute(hb, w0, 2 * ps, false);
-      if (wco != 0) stage();
-      if (ps < 4) compute(hb, w0 + WBUF, 2 * ps + 1, false);
-      if (more && ps < 4 && !nseg2) step_barrier<1>();
-      else step_barrier<0>();
-      wb ^= 1;
-    }
-  }
-  // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, the next chunk staged whole
-  for (int chunk = A.nchunk1; chunk < A.nchunk1 + n_seg2; ++chunk) {
-    const bool more = chunk + 1 < A.nchunk1 + n_seg2;
-    const int slot = T1 + (chunk - A.nchunk1);
-    if (chunk == A.nchunk1) {   // the first 1x1 chunk is staged whole here (the 3x3 steps stage 3x3 halos only)
-      setup(chunk);
-#pragma unroll
-      for (int k = 0; k < SEG2 / NT; ++k) {
-        const int h = tid + NT * k, pos = piece_pos(h), py = pos >> 4, px = pos & 15;
-        u32x4 v = *(const u32x4*)(cptr + (cok ? (size_t)((ty0 + py) * d.Wo + tx0 + px) * cs : 0));
-        if (!cok) v = u32x4{0u, 0u, 0u, 0u};
-        *(u32x4*)(hbuf + (chunk & 1) * HBUF + (piece_kc(h) * HPAD + (py + 1) * (TW + 2) + px + 1) * 8) = v;
-      }
-      step_barrier<0>();
-    }
-    if (slot + 1 < slot_end) load_w(slot + 1, 2 * (wb ^ 1));
-    u32x4 sv[SEG2 / NT];
-    if (more) {
-      setup(chunk + 1);
-#pragma unroll
-      for (int k = 0; k < SEG2 / NT; ++k) {
-        const int h = tid + NT * k, pos = piece_pos(h), py = pos >> 4, px = pos & 15;
-        sv[k] = *(const u32x4*)(cptr + (cok ? (size_t)((ty0 + py) * d.Wo + tx0 + px) * cs : 0));
-      }
-    }
-    compute(hbuf + (chunk & 1) * HBUF, wbuf + (2 * wb) * WBUF, 4, true);
-    if (more) {
-#pragma unroll
-      for (int k = 0; k < SEG2 / NT; ++k) {
-        const int h = tid + NT * k, pos = piece_pos(h), py = pos >> 4, px = pos & 15;
-        u32x4 v = sv[k];
-        if (!cok) v = u32x4{0u, 0u, 0u, 0u};
-        *(u32x4*)(hbuf + ((chunk + 1) & 1) * HBUF + (piece_kc(h) * HPAD + (py + 1) * (TW + 2) + px + 1) * 8) = v;
-      }
-    }
-    step_barrier<0>();
-    wb ^= 1;
-  }
-
-  if (HDBG(4)) return;
-  // ------------------------------------------------------------ epilogue
-  const int K = d.K;
-  const int Ho = d.Ho, Wo = d.Wo;
-  auto pix_of = [&](int bb) { return (px_r + 8 * bb) * 16 + px_x; };   // pixel index in the tile
-  if (A.splits > 1) {   // fp32 partials of this split; splitk_reduce applies the epilogue
-    float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const int pi = pix_of(bb);
-        const size_t p = ((size_t)n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int co = co0 + wco * 64 + 32 * c + 8 * g + 4 * hh;
-          const f32x4 v4 = {acc[c][bb][4 * g], acc[c][bb][4 * g + 1], acc[c][bb][4 * g + 2], acc[c][bb][4 * g + 3]};
-          if (co + 3 < K) {
-            *(f32x4*)(ws + p * K + co) = v4;
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (co + r < K) ws[p * K + co + r] = v4[r];
-          }
-        }
-      }
-    return;
-  }
-  const bool stats = d.stats != nullptr;
-  const bool dep = d.ep_a != nullptr;
-  const bool hasx = d.ep_x0 != nullptr;
-  const int srow = tile * 4 + wpx;   // slab row: the wave's 64 pixels (tile rows wpx, +4, +8, +12) of image n
-  auto flush_stats = [&](int c, const float (&s1)[16], const float (&s2)[16]) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float a = half32_sum_to_last(s1[i]), qv = half32_sum_to_last(s2[i]);
-      const int co = co0 + wco * 64 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (cn == 31 && co < K) {
-        float* sp = d.stats + ((size_t)srow * K + co) * 2;
-        sp[0] = a;
-        sp[1] = qv;
-      }
-    }
-  };
-
-  if (co0 + BCO <= K && !d.out_f32 && !d.accumulate && !(d.resid && hasx)) {
-    // the 256-pixel x 128-channel tile through LDS ([pixel][16-byte chunk ^ (pixel & 15)]): coalesced stores
-    bf16r* tileb = lds;
-    const bool side = d.resid != nullptr || hasx;
-    if (side) {
-      constexpr int SK = TH * TW * BCO / 8 / NT;
-      u32x4 sv[SK];
-#pragma unroll
-      for (int k = 0; k < SK; ++k) {
-        const int qq = tid + NT * k, pi = qq >> 4, c16 = qq & 15;
-        const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-        const int c = co0 + c16 * 8;
-        const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
-                           : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
-                                           : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-        sv[k] = *(const u32x4*)src;
-      }
-#pragma unroll
-      for (int k = 0; k < SK; ++k) {
-        const int qq = tid + NT * k, pi = qq >> 4, c16 = qq & 15;
-        *(u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8)) = sv[k];
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      float st1[16], st2[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { st1[i] = 0.f; st2[i] = 0.f; }
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const int pi = pix_of(bb);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int cl = wco * 64 + 32 * c + 8 * g + 4 * hh;
-          const f32x4 bias = *(const f32x4*)(epi + cl);
-          const f32x4 ea = *(const f32x4*)(epi + BCO + cl), eb = *(const f32x4*)(epi + 2 * BCO + cl);
-          bf16r* tp8 = tileb + pi * BCO + (((cl >> 3) ^ (pi & 15)) * 8) + (cl & 7);
-          float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[c][bb][4 * g + r] + bias[r];
-          if (side) {
-            const u32x2 sr = *(const u32x2*)tp8;
-            const float f[4] = {bf_lo(sr[0]), bf_hi(sr[0]), bf_lo(sr[1]), bf_hi(sr[1])};
-            if (d.resid) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] += f[r];
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                xv[r] = f[r];
-                if (dep) v[r] *= silu_grad(ea[r] * f[r] + eb[r]);
-              }
-            }
-          }
-          u32x2 o;
-          o[0] = pack2(v[0], v[1]);
-          o[1] = pack2(v[2], v[3]);
-          *(u32x2*)tp8 = o;
-          if (stats) {
-            const float w[4] = {bf_lo(o[0]), bf_hi(o[0]), bf_lo(o[1]), bf_hi(o[1])};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              st1[4 * g + r] += w[r];
-              st2[4 * g + r] += hasx ? w[r] * xv[r] : w[r] * w[r];
-            }
-          }
-        }
-      }
-      if (stats && !HDBG(32)) flush_stats(c, st1, st2);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TH * TW * BCO / 8 / NT; ++k) {
-      const int qq = tid + NT * k, pi = qq >> 4, c16 = qq & 15;
-      const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-      *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) =
-          *(const u32x4*)(tileb + pi * BCO + ((c16 ^ (pi & 15)) * 8));
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      float st1[16], st2[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { st1[i] = 0.f; st2[i] = 0.f; }
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const int pi = pix_of(bb);
-        const size_t p = ((size_t)n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int co = co0 + wco * 64 + 32 * c + 8 * g + 4 * hh;
-          if (co >= K) continue;
-          const bool full = co + 3 < K;
-          float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int r = 0; r < 4; ++r) {
-            float bsum = 0.f;
-            if (co + r < K) {
-              if (d.bias) bsum += d.bias[co + r];
-              if (d.bias2) bsum += d.bias2[co + r];
-              if (d.bias_nc) bsum += d.bias_nc[(size_t)n * K + co + r];
-            }
-            v[r] = acc[c][bb][4 * g + r] + bsum;
-          }
-          if (d.resid) {
-            for (int r = 0; r < 4; ++r)
-              if (co + r < K) v[r] += bf2f(((const bf16r*)d.resid)[p * K + co + r]);
-          }
-          if (hasx) {
-            const int C0e = d.ep_C0;
-            for (int r = 0; r < 4; ++r) {
-              const int cc = co + r;
-              if (cc >= K) continue;
-              const bf16r* xp = (cc < C0e) ? (const bf16r*)d.ep_x0 + p * C0e + cc
-                                           : (const bf16r*)d.ep_x1 + p * (K - C0e) + (cc - C0e);
-              xv[r] = bf2f(*xp);
-              if (dep) v[r] *= silu_grad(d.ep_a[(size_t)n * K + cc] * xv[r] + d.ep_b[(size_t)n * K + cc]);
-            }
-          }
-          if (d.out_f32) {
-            float* op = (float*)d.out + p * K + co;
-            for (int r = 0; r < 4; ++r)
-              if (co + r < K) op[r] = d.accumulate ? op[r] + v[r] : v[r];
-          } else {
-            bf16r* op = (bf16r*)d.out + p * K + co;
-            for (int r = 0; r < 4; ++r)
-              if (co + r < K) {
-                const float w = d.accumulate ? bf2f(op[r]) + v[r] : v[r];
-                op[r] = (bf16r)f2bf(w);
-                v[r] = bf2f(op[r]);
-              }
-          }
-          (void)full;
-          if (stats) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              st1[4 * g + r] += v[r];
-              st2[4 * g + r] += hasx ? v[r] * xv[r] : v[r] * v[r];
-            }
-          }
-        }
-      }
-      if (stats) flush_stats(c, st1, st2);
-    }
-  }
-}
-
-static int g_halo_variant = 1;   // fmd_halo_set_variant: 1 = v1 (16x16x32, default), 2 = v2 (32x32x16) for GN-prologue 2-D problems
-static int g_persist = 512;      // v2: workgroups resident in the first dispatch round (2 per CU)
-static int g_stagger = 0;        // stagger of a CU's second workgroup (s_sleep(127) rounds); measured: no gain
-static int g_v2_all = 0;         // variant 3: v2 for every 2-D problem (testing)
-
 // [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
 __global__ void tile_weights_kernel(const bf16r* __restrict__ w, int K, int T, int C, int ntc, int nchunk,
                                     bf16r* __restrict__ out) {
@@ -1258,48 +693,15 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);
-  A.ntiles = g_persist;   // first dispatch round: 2 workgroups per CU (81 KB LDS each)
-  A.stagger = (A.splits == 1 && nwg > 2 * g_persist) ? g_stagger : 0;   // >= 2 full rounds: a phase to keep
-  // v2 (32x32x16) wins where the staging carries the GroupNorm(+SiLU) transform (VALU-bound v1 loop); without a
-  // prologue the v1 loop is not VALU-bound and its cheaper epilogue wins (tools/conv_micro.py)
-  if (g_halo_variant == 2 && !d3 && (pro != 0 || g_v2_all)) {
-    const dim3 blk(512);
-    const dim3 g2(nwg, A.splits);
-#define g g2
-    if (d->upsample) {
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo_v2<true, 2>), g, blk, 0, st, A);
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo_v2<true, 1>), g, blk, 0, st, A);
-      else hipLaunchKernelGGL((conv3x3_halo_v2<true, 0>), g, blk, 0, st, A);
-    } else {
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo_v2<false, 2>), g, blk, 0, st, A);
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo_v2<false, 1>), g, blk, 0, st, A);
-      else hipLaunchKernelGGL((conv3x3_halo_v2<false, 0>), g, blk, 0, st, A);
-    }
-#undef g
-    return (int)hipGetLastError();
-  }
-  if (g_nt == 256) {
-    const dim3 blk(256);
-    if (d->upsample) {
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2, 256>), g, blk, 0, st, A);
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1, 256>), g, blk, 0, st, A);
-      else hipLaunchKernelGGL((conv3x3_halo<true, 0, 256>), g, blk, 0, st, A);
-    } else {
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2, 256>), g, blk, 0, st, A);
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1, 256>), g, blk, 0, st, A);
-      else hipLaunchKernelGGL((conv3x3_halo<false, 0, 256>), g, blk, 0, st, A);
-    }
-    return (int)hipGetLastError();
-  }
-  const dim3 blk(512);
+  const dim3 blk(NT);
   if (d->upsample) {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2, 512>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1, 512>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo<true, 0, 512>), g, blk, 0, st, A);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<true, 0>), g, blk, 0, st, A);
   } else {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2, 512>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1, 512>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo<false, 0, 512>), g, blk, 0, st, A);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<false, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo<false, 0>), g, blk, 0, st, A);
   }
   return (int)hipGetLastError();
 }
@@ -1307,26 +709,6 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
 // Debug hook (not part of the public ABI): ablation flags of the next launches (see HArgs::dbg).
 extern "C" int fmd_debug_halo_flags(int flags) {
   g_dbg = flags;
-  return 0;
-}
-
-extern "C" int fmd_halo_set_variant(int32_t v) {
-  if (v < 1 || v > 3) return -1;
-  g_halo_variant = v == 3 ? 2 : v;
-  g_v2_all = v == 3;
-  return 0;
-}
-
-extern "C" int fmd_halo_set_persist(int32_t wgs, int32_t stagger) {
-  if (wgs < 0 || stagger < 0 || stagger > 64) return -1;
-  g_persist = wgs;
-  g_stagger = stagger;
-  return 0;
-}
-
-extern "C" int fmd_halo_set_workgroup(int32_t nt) {
-  if (nt != 256 && nt != 512) return -1;
-  g_nt = nt;
   return 0;
 }
 

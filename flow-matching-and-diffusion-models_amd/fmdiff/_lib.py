@@ -94,10 +94,7 @@ SIGNATURES = {
     "fmd_gn_gb_fold": [p, i32, p],
     "fmd_lincomb": [C.POINTER(LincombDesc), p],
     "fmd_sched_step": [C.POINTER(SchedStepDesc), p],
-    "fmd_halo_set_workgroup": [i32],
     "fmd_halo_set_min_workgroups": [i32],
-    "fmd_halo_set_variant": [i32],
-    "fmd_halo_set_persist": [i32, i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_t": [p, i32, i32, i32, i32, i32, i32, p, p],
@@ -116,8 +113,6 @@ SIGNATURES = {
     "fmd_grouped_linear": [p, i32, i32, p, p, i32, i32, p, i32, p],
     "fmd_grouped_linear_bwd_workspace": [i32, i32, i32],
     "fmd_grouped_linear_bwd": [p, i32, i32, p, p, i32, i32, p, i32, p, i32, p, p],
-    "fmd_attention_fwd": [p, i32, i32, i32, i32, i32, p, p, p],
-    "fmd_attention_bwd": [p, p, p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_conv_combine": [C.POINTER(ConvDesc), p],
     "fmd_attn_head_pad": [i32],
     "fmd_attn_pack": [p, p, i32, i32, i32, i32, i32, i32, i32, i32, i32, p, p, p, p],
@@ -164,14 +159,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, i32)
-        if os.environ.get("FMD_HALO_NT"):
-            check(L.fmd_halo_set_workgroup(int(os.environ["FMD_HALO_NT"])), "fmd_halo_set_workgroup")
         if os.environ.get("FMD_HALO_MIN_WG"):
             check(L.fmd_halo_set_min_workgroups(int(os.environ["FMD_HALO_MIN_WG"])), "fmd_halo_set_min_workgroups")
-        if os.environ.get("FMD_HALO_STAGGER"):
-            check(L.fmd_halo_set_persist(512, int(os.environ["FMD_HALO_STAGGER"])), "fmd_halo_set_persist")
-        if os.environ.get("FMD_HALO_V"):
-            check(L.fmd_halo_set_variant(int(os.environ["FMD_HALO_V"])), "fmd_halo_set_variant")
         _lib = L
     return _lib
 

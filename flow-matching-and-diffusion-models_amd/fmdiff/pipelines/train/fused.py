@@ -37,17 +37,24 @@ def _own_stream(fn):
     """Run a public entry point on the object's private HIP stream when the caller is on the device's default
     (legacy null) stream, handing off with stream waits at entry and exit.
 
-    Measured on MI355X / ROCm 7.x (tests/test_gpu_dp.py, tools/dp_debug.py): with the train step replayed on the
-    null stream, a collective issued afterwards (ProcessGroupGloo's CUDA all-reduce: event on the current stream
-    -> copy on its own stream -> event back) intermittently returned corrupted gradient buckets (norms of 1e16 /
-    inf at step 2), even with a host synchronisation between the replay and the all-reduce; the same steps on a
-    created stream were bit-identical to the eager reference in every run.  Every path of this module
-    therefore issues its graphs, collectives and kernels on a created stream."""
+    Measured on MI355X / ROCm 7.x (tests/test_gpu_dp.py, tools/dp_debug.py): with the process on the legacy
+    null stream, the 2-rank step's gradient buckets came back corrupted after the second replay (norms of 1e16 /
+    inf) -- with the graphs replayed on the null stream, with a host synchronisation between the replay and the
+    all-reduce, and also with this hand-off to a private stream; with the whole process on a created stream
+    (``torch.cuda.set_stream`` before any work, as bench.py and the trainer loop do) every run was bit-identical
+    to the eager reference.  Multi-rank callers on the null stream therefore get a warning."""
     @functools.wraps(fn)
     def wrapped(self, *a, **kw):
         cur = torch.cuda.current_stream()
         if cur != torch.cuda.default_stream(cur.device):
             return fn(self, *a, **kw)
+        if getattr(self, "world", 1) > 1 and not getattr(self, "_warned_stream", False):
+            import warnings
+            warnings.warn("FusedTrainStep with several ranks on the default (null) HIP stream: collectives next to "
+                          "graph replays on that stream corrupted gradients on this stack; call "
+                          "torch.cuda.set_stream(torch.cuda.Stream()) before building the model (as bench.py and "
+                          "the trainer loop do)", RuntimeWarning)
+            self._warned_stream = True
         st = self.__dict__.get("_work_stream")
         if st is None or st.device != cur.device:
             st = self._work_stream = torch.cuda.Stream(device=cur.device)

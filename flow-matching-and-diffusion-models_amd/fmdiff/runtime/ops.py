@@ -638,9 +638,7 @@ def silu_bwd(x, dy):
     return dx
 
 
-# softmax attention: MFMA kernels over canonical [B*heads][rows][head_pad] planes (csrc/attention_mfma.hip);
-# FMD_ATTN=valu selects the older VALU kernels of csrc/attention.hip (A/B measurements only)
-_ATTN_VALU = os.environ.get("FMD_ATTN", "") == "valu"
+# softmax attention: MFMA kernels over canonical [B*heads][rows][head_pad] planes (csrc/attention_mfma.hip)
 
 
 def _attn_planes(B, heads, rows, dh, dev):
@@ -701,13 +699,7 @@ def _attn_softmax_bwd(src_q, src_kv, o, dout, saved, B, Tq, Tk, heads, dh, raw, 
 
 def attention_fwd(qkv, T, heads, dh, raw):
     """Softmax self-attention over the fused qkv projection [B][T][3*inner] -> (o [B][T][inner], lse)."""
-    B = qkv.shape[0]
-    if not _ATTN_VALU:
-        return _attn_softmax_fwd(qkv, qkv, B, T, T, heads, dh, raw, 0)
-    o = torch.empty((B, T, heads * dh), device=qkv.device, dtype=BF16)
-    lse = torch.empty((B, heads, T), device=qkv.device, dtype=F32)
-    _lib.call("fmd_attention_fwd", _p(qkv), B, T, heads, dh, int(raw), _p(o), _p(lse), stream())
-    return o, lse
+    return _attn_softmax_fwd(qkv, qkv, qkv.shape[0], T, T, heads, dh, raw, 0)
 
 
 def _la_workspace(B, heads, dev):
@@ -736,31 +728,24 @@ def cross_attention_fwd(q, kv, Tq, Tk, heads, dh, linear_eps=None, raw=1):
     """SpatialCrossAttention core (csrc/attention.hip): q [B][Tq][inner], kv [B][Tk][2*inner] -> (o, saved),
     softmax (saved = lse) or LinearQKVAttention when ``linear_eps`` is given (saved = state)."""
     B = q.shape[0]
+    if linear_eps is None:
+        return _attn_softmax_fwd(q, kv, B, Tq, Tk, heads, dh, raw, 1)
     o = torch.empty((B, Tq, heads * dh), device=q.device, dtype=BF16)
-    lin = linear_eps is not None
-    if lin:
-        saved = torch.empty((int(_lib.lib().fmd_linear_attention_state(B, heads)),), device=q.device, dtype=F32)
-        ws = _la_workspace(B, heads, q.device)
-    else:
-        if not _ATTN_VALU:
-            return _attn_softmax_fwd(q, kv, B, Tq, Tk, heads, dh, raw, 1)
-        saved = torch.empty((B, heads, Tq), device=q.device, dtype=F32)
-        ws = None
-    _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, int(raw), int(lin),
-              float(linear_eps or 0.0), _p(o), _p(saved), _p(ws), stream())
+    saved = torch.empty((int(_lib.lib().fmd_linear_attention_state(B, heads)),), device=q.device, dtype=F32)
+    ws = _la_workspace(B, heads, q.device)
+    _lib.call("fmd_cross_attention_fwd", _p(q), _p(kv), B, Tq, Tk, heads, dh, int(raw), 1, float(linear_eps),
+              _p(o), _p(saved), _p(ws), stream())
     return o, saved
 
 
 def cross_attention_bwd(q, kv, o, dout, saved, Tq, Tk, heads, dh, linear_eps=None, raw=1):
     B = q.shape[0]
-    lin = linear_eps is not None
     dq, dkv = torch.empty_like(q), torch.empty_like(kv)
-    if not lin and not _ATTN_VALU:
+    if linear_eps is None:
         _attn_softmax_bwd(q, kv, o, dout, saved, B, Tq, Tk, heads, dh, raw, 1, dq, dkv)
         return dq, dkv
-    ws = _la_workspace(B, heads, q.device) if lin else torch.empty((B, heads, Tq), device=q.device, dtype=F32)
-    _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(ws), B, Tq, Tk, heads, dh,
-              int(raw), int(lin), float(linear_eps or 0.0), _p(dq), _p(dkv), stream())
+    _lib.call("fmd_cross_attention_bwd", _p(q), _p(kv), _p(o), _p(dout), _p(saved), _p(_la_workspace(B, heads, q.device)),
+              B, Tq, Tk, heads, dh, int(raw), 1, float(linear_eps), _p(dq), _p(dkv), stream())
     return dq, dkv
 
 
@@ -785,14 +770,8 @@ def context_norm_bwd(ctx, tok_major, groups, mr, dout, dgamma, dbeta):
 
 
 def attention_bwd(qkv, o, dout, lse, T, heads, dh, raw):
-    B = qkv.shape[0]
     dqkv = torch.empty_like(qkv)
-    if not _ATTN_VALU:
-        _attn_softmax_bwd(qkv, qkv, o, dout, lse, B, T, T, heads, dh, raw, 0, dqkv, dqkv)
-        return dqkv
-    delta = torch.empty_like(lse)
-    _lib.call("fmd_attention_bwd", _p(qkv), _p(o), _p(dout), _p(lse), _p(delta), B, T, heads, dh, int(raw),
-              _p(dqkv), stream())
+    _attn_softmax_bwd(qkv, qkv, o, dout, lse, qkv.shape[0], T, T, heads, dh, raw, 0, dqkv, dqkv)
     return dqkv
 
 

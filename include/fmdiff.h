@@ -107,19 +107,10 @@ int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_st
 
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
-/* Halo conv workgroup size: 512 (8 waves x 64 pixels each, default) or 256 (4 waves x 128 pixels,
- * 256 VGPRs per wave).  Returns -1 for other values.  Also settable with FMD_HALO_NT at load time. */
-int fmd_halo_set_workgroup(int32_t nt);
 /* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv
  * (default 128; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
  * halo_splits mirror reads the same variable. */
 int fmd_halo_set_min_workgroups(int32_t n);
-/* 2-D halo conv main loop: 1 (default) = v_mfma_f32_16x16x32_bf16 (v1) everywhere; 2 = v2
- * (v_mfma_f32_32x32x16_bf16) for GroupNorm-prologue problems, v1 otherwise; 3 = v2 everywhere (testing). */
-int fmd_halo_set_variant(int32_t v);
-/* v2 dispatch: wgs = workgroups resident in the first round (2 per CU), stagger = s_sleep(127) rounds by
- * which the second first-round workgroup of each CU starts late (0 = off).  Also FMD_HALO_STAGGER at load. */
-int fmd_halo_set_persist(int32_t wgs, int32_t stagger);
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);
@@ -278,21 +269,17 @@ int fmd_grouped_linear_bwd(const float* x, int32_t B, int32_t I, const void* gro
 int fmd_silu_bwd_f32(const float* x, const float* dy, float* dx, int64_t n, fmd_stream_t s);
 
 /* ----------------------------------------------------------- attention
- * F.scaled_dot_product_attention inside SpatialSelfAttention (raw=1, raw
- * reshape head split, src/nn/blocks/attention.py:111-115) and
- * DiffusersAttentionND (raw=0, attention.py:262-268). qkv: bf16 [B][T][3*inner]. */
-int fmd_attention_fwd(const void* qkv, int32_t B, int32_t T, int32_t heads, int32_t dh, int32_t raw, void* o,
-                      float* lse, fmd_stream_t s);
-int fmd_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, float* delta, int32_t B,
-                      int32_t T, int32_t heads, int32_t dh, int32_t raw, void* dqkv, fmd_stream_t s);
+ * Softmax attention (F.scaled_dot_product_attention inside SpatialSelfAttention / DiffusersAttentionND /
+ * SpatialCrossAttention) runs on the MFMA kernels declared further down (fmd_attn_pack / fmd_attn_mfma_fwd /
+ * fmd_attn_mfma_bwd / fmd_attn_unpack). */
 /* LinearQKVAttention (src/nn/blocks/attention.py:53-70) inside SpatialSelfAttention(use_linear=True)
  * (attention.py:104-117; same raw head split): out = softmax_d(q) (softmax_tokens(k)^T v / (sum ks + eps)).
  * ``state`` (fmd_linear_attention_state floats) is written by the forward and read by the backward;
  * ``ws`` holds fmd_linear_attention_workspace floats. dh <= 64. */
 /* SpatialCrossAttention (attention.py:120-189): q [B][Tq][inner] (q_proj output), kv [B][Tk][2*inner]
  * (kv_proj output), raw head split q.reshape(b, heads, Tq, dh), kv.reshape(b, heads, Tk, 2dh).chunk(2).
- * linear = 1: LinearQKVAttention (lse_or_state = fmd_linear_attention_state floats, ws = workspace);
- * linear = 0: softmax (lse_or_state = lse [B][heads][Tq]; backward: ws_or_delta = delta [B][heads][Tq]). */
+ * linear must be 1: LinearQKVAttention (lse_or_state = fmd_linear_attention_state floats, ws = workspace);
+ * linear = 0 returns -2 (softmax cross-attention is fmd_attn_mfma_fwd / fmd_attn_mfma_bwd). */
 int fmd_cross_attention_fwd(const void* q, const void* kv, int32_t B, int32_t Tq, int32_t Tk, int32_t heads,
                             int32_t dh, int32_t raw, int32_t linear, float eps, void* o, float* lse_or_state,
                             float* ws, fmd_stream_t s);

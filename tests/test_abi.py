@@ -21,7 +21,7 @@ def _declared():
 def test_header_declares_entry_points():
     names = _declared()
     assert len(names) >= 25
-    for must in ("fmd_conv", "fmd_wgrad", "fmd_gn_prep", "fmd_attention_fwd", "fmd_flow_euler", "fmd_adamw_sched"):
+    for must in ("fmd_conv", "fmd_wgrad", "fmd_gn_prep", "fmd_attn_mfma_fwd", "fmd_flow_euler", "fmd_adamw_sched"):
         assert must in names
 
 

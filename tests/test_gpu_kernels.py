@@ -717,21 +717,26 @@ def test_halo_conv_split_k_matches_generic(case):
         torch.testing.assert_close(ta, tb, rtol=2e-3, atol=2e-2)
 
 
-@pytest.mark.parametrize("case", ["pro_stats", "skip_seg2", "dgrad_ep", "upsample", "split"])
-def test_halo_workgroup_256_matches_512(case):
-    """fmd_halo_set_workgroup(256) (4 waves x 8 rows, 256 VGPRs) computes exactly what the default
-    512-thread kernel computes: same per-element reduction order, so outputs and statistics are equal."""
-    import ctypes
-    from fmdiff import _lib
+@pytest.mark.parametrize("case", ["pro_stats", "skip_seg2", "dgrad_ep", "upsample", "split", "concat_pro"])
+def test_halo_conv_matches_generic_implicit_gemm(case):
+    """The halo-tiled 3x3 conv (csrc/conv_halo.hip: unrolled 9-tap chunk pipeline, chunk-invariant staging
+    geometry) against the generic implicit GEMM (csrc/conv.hip, force_generic) on every epilogue / prologue
+    variant the UNet uses: GN+SiLU prologue with statistics, the ResBlock skip 1x1 segment, the dgrad
+    SiLU' epilogue with GN-backward sums, nearest-x2 upsample gather, split-K, two-source concat.  Two
+    independent kernels, fp32 accumulation in different orders: outputs within bf16 rounding (relative L2
+    < 4e-3), statistics within 1e-2 relative."""
     O = ops()
     N, H, W, C, K = 4, 128, 128, 128, 128
     if case == "split":
         N, H, W, C, K = 4, 32, 32, 512, 256
     x = _rand_nhwc(N, H // 2 if case == "upsample" else H, W // 2 if case == "upsample" else W, C, 51).to(DEV)
-    w = O.prep_weights(_w(K, C, 3, 52).to(DEV), 0)
+    w = O.prep_weights(_w(K, C if case != "concat_pro" else 2 * C, 3, 52).to(DEV), 0)
     kw = dict(bias=(torch.randn(K) * 0.1).to(DEV), want_stats=case != "split")
-    if case in ("pro_stats", "upsample", "split"):
-        kw["pro"] = ((torch.rand(N, C) + 0.5).to(DEV), (torch.randn(N, C) * 0.2).to(DEV), True)
+    Ct = 2 * C if case == "concat_pro" else C
+    if case in ("pro_stats", "upsample", "split", "concat_pro"):
+        kw["pro"] = ((torch.rand(N, Ct) + 0.5).to(DEV), (torch.randn(N, Ct) * 0.2).to(DEV), True)
+    if case == "concat_pro":
+        kw["src1"] = _rand_nhwc(N, H, W, C, 56).to(DEV)
     if case == "upsample":
         kw["upsample"] = True
     if case == "skip_seg2":
@@ -739,21 +744,20 @@ def test_halo_workgroup_256_matches_512(case):
     if case == "dgrad_ep":
         kw["ep"] = (_rand_nhwc(N, H, W, K, 55).to(DEV), None, (torch.rand(N, K) + 0.5).to(DEV),
                     (torch.randn(N, K) * 0.2).to(DEV))
-    assert O.halo_eligible(N, x.shape[1], H, W, K, upsample=case == "upsample", Cin=C, pro="pro" in kw)
-    L = _lib.lib()
-    outs = []
-    try:
-        for nt in (512, 256):
-            assert L.fmd_halo_set_workgroup(ctypes.c_int32(nt)) == 0
-            wt = O.tile_weights(w)
-            w2t = O.tile_weights(kw["wgt2"]) if "wgt2" in kw else None
-            o, st = O.conv(x, K, w, wgt_tiled=wt, wgt2_tiled=w2t, **kw)
-            outs.append((o, st))
-    finally:
-        L.fmd_halo_set_workgroup(ctypes.c_int32(512))
-    assert torch.equal(outs[0][0], outs[1][0])
-    if outs[0][1] is not None:
-        assert torch.equal(outs[0][1].slab, outs[1][1].slab)
+    assert O.halo_eligible(N, x.shape[1], H, W, K, upsample=case == "upsample", Cin=Ct, pro="pro" in kw)
+    wt = O.tile_weights(w)
+    w2t = O.tile_weights(kw["wgt2"]) if "wgt2" in kw else None
+    oh, sh = O.conv(x, K, w, wgt_tiled=wt, wgt2_tiled=w2t, **kw)
+    og, sg = O.conv(x, K, w, force_generic=True, **kw)
+    err = ((oh.float() - og.float()).norm() / og.float().norm()).item()
+    print(f"{case}: halo vs generic rel L2 {err:.3e}")
+    assert err < 4e-3
+    if sh is not None:
+        a = sh.slab.view(N, -1, K, 2).sum(1)
+        b = sg.slab.view(N, -1, K, 2).sum(1)
+        serr = ((a - b).norm() / b.norm()).item()
+        print(f"{case}: statistics rel L2 {serr:.3e}")
+        assert serr < 1e-2
 
 
 @pytest.mark.parametrize("kind,order,variant,betas", [

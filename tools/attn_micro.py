@@ -1,6 +1,6 @@
 """Micro-benchmark of the softmax attention cores (GPU box; also run under rocprofv3 --kernel-trace --stats).
 
-usage: python tools/attn_micro.py [--iters 20] [--impl mfma,valu]
+usage: python tools/attn_micro.py [--iters 20] 
 Problems (batch 8):
   vae_mid   : SpatialSelfAttention of the VAE mid block, 32x32 latent grid -> T=1024, 4 heads x 64 (raw split)
   unet_mid  : EfficientUNetND config-B mid block, 8x8 -> T=64, 4 heads x 64 (raw split)
@@ -23,7 +23,7 @@ from fmdiff.runtime import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--impl", default="mfma,valu")
+    ap.add_argument("--impl", default="mfma")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -44,7 +44,7 @@ def main():
             fwd = lambda: ops.attention_fwd(qkv, Tq, heads, dh, raw)  # noqa: E731
         dout = (torch.randn(B, Tq, inner, device=dev, generator=g) * 0.5).to(torch.bfloat16)
         for impl in a.impl.split(","):
-            ops._ATTN_VALU = impl == "valu"
+            assert impl == "mfma", "the VALU softmax kernels were removed in round 3"
             o, lse = fwd()
             if cross:
                 bwd = lambda: ops.cross_attention_bwd(q, kv, o, dout, lse, Tq, Tk, heads, dh, None, raw)  # noqa: E731
@@ -63,7 +63,7 @@ def main():
                 ms = e0.elapsed_time(e1) / a.iters
                 flops = 2.0 * nprod * B * heads * Tq * Tk * dh
                 print(f"{name:9s} {impl:4s} {label} {ms * 1e3:9.1f} us/call {flops / ms / 1e9:7.2f} TFLOP/s", flush=True)
-    ops._ATTN_VALU = False
+
 
 
 if __name__ == "__main__":

@@ -92,9 +92,6 @@ def main():
             for sg in stg]
     warmed = False
     for name, fl, var, sg in todo:
-        L.fmd_halo_set_variant(ctypes.c_int(var))
-        if sg is not None:
-            L.fmd_halo_set_persist(512, sg)
         fn, flops = probs[name]
         if a.only and name not in a.only.split(","):
             continue
