@@ -190,7 +190,7 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     from fmdiff.models.generators import DiffusionUNetFactory
-    from fmdiff.pipelines.train.fused import FusedFlowSampler, FusedTrainStep
+    from fmdiff.pipelines.train.fused import FusedFlowSampler, FusedSampler, FusedTrainStep
 
     torch.manual_seed(1234 + rank)
     model = DiffusionUNetFactory().build(LDCT_FM_UNET, "concatenate", 1).to(dev)
@@ -240,26 +240,44 @@ def main():
 
     samp = {}
     if not args.no_sampler:
-        sampler = FusedFlowSampler(model, args.sampler_steps)
-        init = torch.randn(B, 1, HW, HW, device=dev, generator=g)
-        sampler.sample(init, ldct, use_graph=use_graph)      # warm-up
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        sampler.sample(init, ldct, use_graph=use_graph)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        ds = torch.tensor([time.perf_counter() - t0], device=dev)
-        if world > 1:
-            dist.all_reduce(ds, op=dist.ReduceOp.MAX)
-        ds = float(ds.item())
+        from fmdiff.pipelines.schedulers import DDPMScheduler
+        from fmdiff.pipelines.utils import model_throughput
+
+        def time_sampler(sampler, noise=None):
+            """One untimed call (capture + warm-up), then one call timed between barriers (max over ranks)."""
+            init = torch.randn(B, 1, HW, HW, device=dev, generator=g)
+            sampler.sample(init, ldct, use_graph=use_graph, generator=g)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            timing = {}
+            t0 = time.perf_counter()
+            sampler.sample(init, ldct, use_graph=use_graph, generator=g, timing=timing)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ds = torch.tensor([time.perf_counter() - t0], device=dev)
+            if world > 1:
+                dist.all_reduce(ds, op=dist.ReduceOp.MAX)
+            return float(ds.item()), timing
+
+        # config B: the 50-step FlowMatchEuler sampler (the metric's "sampler steps/sec")
+        ds, timing = time_sampler(FusedFlowSampler(model, args.sampler_steps))
         samp = dict(sampler_images_per_sec=world * B / ds, sampler_steps_per_sec=args.sampler_steps / ds,
                     sampler_ms_per_step=ds / args.sampler_steps * 1e3, sampler_steps=args.sampler_steps,
                     sampler_mfma_frac=(world * B / ds) * args.sampler_steps * FWD_GFLOP_PER_IMAGE
-                    / (world * PEAK_BF16_TFLOPS * 1e3))
+                    / (world * PEAK_BF16_TFLOPS * 1e3),
+                    # the reference's evaluate-side fields (diffusion_like.py:287-313), this rank's loop
+                    sampler_model_throughput=model_throughput(timing, B))
         log(f"[bench] sampler: {samp['sampler_images_per_sec']:.2f} img/s, {samp['sampler_ms_per_step']:.2f} ms/step")
+        # config C: DDPM sampling of the same 113 M EfficientUNetND (configs/diffusion/ldct_ddpm.json betas),
+        # 50 leading-spaced steps (the graph-replayed FusedSampler; variance noise drawn up front)
+        ddpm = FusedSampler(model, DDPMScheduler(1000, beta_start=0.00085, beta_end=0.012), args.sampler_steps)
+        dd, _ = time_sampler(ddpm)
+        samp.update(ddpm_sampler_images_per_sec=world * B / dd, ddpm_sampler_ms_per_step=dd / args.sampler_steps * 1e3,
+                    ddpm_sampler_steps=args.sampler_steps)
+        log(f"[bench] ddpm sampler: {samp['ddpm_sampler_images_per_sec']:.2f} img/s, "
+            f"{samp['ddpm_sampler_ms_per_step']:.2f} ms/step")
 
     if rank != 0:
         if world > 1:

@@ -79,6 +79,13 @@ FMD_DEV int xcd_remap(int b, int nwg) {
 // makes later ds_reads wait for it (its builtin form drains vmcnt before every following LDS read),
 // so the pipeline's own counted waits in step_barrier() are the only ones.  lds_dst: wave-uniform
 // LDS byte address; lane i lands at lds_dst + 16 i.
+// Scalar-base form: lane address = sbase + voff (a fixed 32-bit per-lane byte offset, "saddr" addressing), so
+// a stream whose lanes always fetch the same offsets of consecutive blocks needs no per-DMA vector arithmetic.
+FMD_DEV void glds16s(const void* sbase, unsigned voff, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
+}
 FMD_DEV void glds16(const void* gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"

@@ -166,19 +166,17 @@ void conv3x3_halo(const HArgs A) {
   }
 
   // ---- weights: one contiguous 8 KiB tile per tap, copied global -> LDS by the DMA path
-  // slot = tap index over the whole reduction: 9 per 3x3 chunk, then 1 per 1x1 chunk; wtile = 0..3
+  // slot = tap index over the whole reduction: 9 per 3x3 chunk, then 1 per 1x1 chunk; wtile = 0..3.
+  // Wave-uniform source base (SGPRs) + this lane's fixed 16-byte offset: no per-DMA vector address math.
+  static_assert(WDMA == 1, "one 16-byte weight DMA per thread and tap");
+  const int T1 = A.nchunk1 * 9;
+  const bf16r* const wbase1 = A.wt + (size_t)tco * T1 * WBUF;
+  const bf16r* const wbase2 = A.wt2 + (size_t)tco * A.nchunk2 * WBUF;
+  const unsigned wvoff = (unsigned)tid * 16;
+  const unsigned wdst0 = __builtin_amdgcn_readfirstlane(lds_base + SM_W + (unsigned)(wid * 64 * 8) * 2);
   auto load_w = [&](int slot, int wtile) {
-    const bf16r* src;
-    if (slot < A.nchunk1 * 9) {
-      src = A.wt + ((size_t)tco * A.nchunk1 * 9 + slot) * WBUF;
-    } else {
-      src = A.wt2 + ((size_t)tco * A.nchunk2 + (slot - A.nchunk1 * 9)) * WBUF;
-    }
-#pragma unroll
-    for (int k = 0; k < WDMA; ++k) {
-      const unsigned dst = lds_base + SM_W + (unsigned)(wtile * WBUF + (wid * 64 + k * NT) * 8) * 2;
-      glds16(src + (tid + k * NT) * 8, __builtin_amdgcn_readfirstlane(dst));
-    }
+    const bf16r* src = slot < T1 ? wbase1 + (size_t)slot * WBUF : wbase2 + (size_t)(slot - T1) * WBUF;
+    glds16s(src, wvoff, wdst0 + (unsigned)(wtile * WBUF * 2));
   };
 
   // ---- halo staging through registers (the GN/SiLU transform happens between load and LDS store)
@@ -190,6 +188,8 @@ void conv3x3_halo(const HArgs A) {
   int cch = 0;               // its first channel (GN affine table index)
   bool cok = false;
   int srcsl = n;             // stored source image of the chunk being staged (3-D: depth-tap slice)
+  const int HWs = d.Hs * d.Ws;
+  int cimg = n * HWs;        // its first pixel
 
   auto setup = [&](int chunk) {
     if (chunk < A.nchunk1) {
@@ -201,6 +201,7 @@ void conv3x3_halo(const HArgs A) {
         const int zl = zz + kz - 1;                 // logical input depth == output depth (stride 1)
         zok = zl >= 0 && zl < A.depth;
         srcsl = smp * A.dsrc + (UP ? zl >> 1 : zl);
+        cimg = srcsl * HWs;
       }
       const int c = cb * BK + kc * 8;
       cok = c < A.C && zok;
@@ -272,6 +273,25 @@ void conv3x3_halo(const HArgs A) {
 
   f32x4 acc[4][WR];
 
+  // per-thread staging geometry of a main chunk, the same for every chunk of the tile: the piece of staging
+  // step q (0..3) is halo position ppos0 + q * PC1 / 4 of channel group kc (PC1 % 32 == 0)
+  static_assert(LPT == 1 && PC1 % 32 == 0, "one staged piece per thread and step");
+  const int ppos0 = piece_pos(tid);
+  int spix0, spix1, spix2, spix3;   // its pixel inside the stored image; -1 zero padding; -2 nothing to stage
+  {
+    int sp[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pos = ppos0 + q * (PC1 / 4);
+      const bool on = tid < PC1 && q * PC1 + tid < TOT1 && pos < HPOS;
+      const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
+      const int y = hy0 + py, x = hx0 + px;
+      sp[q] = !on ? -2 : (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? y * d.Ws + x : -1;
+    }
+    spix0 = sp[0]; spix1 = sp[1]; spix2 = sp[2]; spix3 = sp[3];
+  }
+  const int sl0 = (kc * HPAD + ppos0) * 8;
+
   auto compute = [&](int hb_i, int tap, bool seg2, int wb_i) {
     const bf16r* hb = hbuf + hb_i * HBUF;
     const bf16r* wb = wbuf + wb_i * WBUF;
@@ -303,7 +323,6 @@ void conv3x3_halo(const HArgs A) {
   const int split = blockIdx.y;
   const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
   const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
-  const int T1 = A.nchunk1 * 9;
   const int slot_end = n_seg2 ? T1 + n_seg2 : c_hi * 9;   // one past the last weight slot of this split
   auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
 
@@ -350,20 +369,23 @@ void conv3x3_halo(const HArgs A) {
         // one halo load per step, always (a dummy in-bounds read when nothing is staged): the register
         // then has the same load -> consume pattern on every path, so hipcc's waits stay counted
         if (issue && ps == 0) setup(nx);
-#pragma unroll
-        for (int k = 0; k < LPT; ++k) {
-          const int t = tid + NT * k;
-          const int h = ps * (nseg2 ? SEG2 / 4 : PC1) + t;
-          const bool act = issue && (nseg2 ? t < SEG2 / 4 : (t < PC1 && h < TOT1));
-          int off;
-          const bf16r* src = piece_src(h, act, nseg2, off);
-          if (HDBG(1)) {
-            rh[k] = u32x4{0u, 0u, 0u, 0u};
-          } else {
-            rh[k] = *(const u32x4*)src;
-          }
-          hoff[k] = off;
+        int off;
+        const bf16r* src;
+        if (!nseg2) {   // main chunk: the precomputed geometry of step ps (uniform select chain)
+          const int sp = ps == 0 ? spix0 : ps == 1 ? spix1 : ps == 2 ? spix2 : ps == 3 ? spix3 : -2;
+          const bool act = issue && sp != -2;
+          const bool valid = act && cok && sp >= 0;
+          src = cbase + (valid ? cimg + sp : 0) * cs;
+          off = !act ? -1 : (sl0 + ps * (PC1 / 4) * 8) | (valid ? 0 : (1 << 30));
+        } else {
+          src = piece_src(ps * (SEG2 / 4) + tid, issue && tid < SEG2 / 4, true, off);
         }
+        if (HDBG(1)) {
+          rh[0] = u32x4{0u, 0u, 0u, 0u};
+        } else {
+          rh[0] = *(const u32x4*)src;
+        }
+        hoff[0] = off;
       };
       auto consume = [&]() {   // the previous step's halo loads are consumed here, on every path
 #pragma unroll

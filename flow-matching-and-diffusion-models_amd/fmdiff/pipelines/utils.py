@@ -164,6 +164,18 @@ def select_timesteps(timesteps: torch.Tensor, start_step=None, last_n_steps=None
     return timesteps
 
 
+def model_throughput(timing: Dict, count: int) -> Dict:
+    """The evaluate-side throughput fields of the reference (``src/pipelines/samplers/diffusion_like.py:287-313``):
+    from the sampling loop's ``model_seconds`` / ``model_calls`` accumulators and the number of samples produced,
+    ``model_samples_per_second = count / model_seconds`` and ``model_seconds_per_sample = model_seconds / count``
+    (0 when undefined), formatted as the reference's metrics row formats them."""
+    secs = float(timing.get("model_seconds", 0.0))
+    sps = count / secs if secs > 0 else 0.0
+    spp = secs / count if count else 0.0
+    return {"samples": int(count), "model_seconds": f"{secs:.6f}", "model_samples_per_second": f"{sps:.6f}",
+            "model_seconds_per_sample": f"{spp:.8f}", "model_calls": int(timing.get("model_calls", 0))}
+
+
 def sample_with_scheduler(model, scheduler, num_inference_steps: int, sample_shape: Tuple[int, ...],
                           device: torch.device, conditioning_mode: str | None = None,
                           conditioning_batch: torch.Tensor | None = None, latent_norm: str | None = None,

@@ -243,3 +243,13 @@ def test_dp_allreduce_equals_global_batch(golden):
     sc.backward()
     want = torch.cat([p.grad.reshape(-1) for p in sd.values()])
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-6)
+
+
+def test_model_throughput_fields_match_reference_formulas():
+    """pipelines.utils.model_throughput: the evaluate-side fields of diffusion_like.py:287-313."""
+    from fmdiff.pipelines.utils import model_throughput
+    row = model_throughput({"model_seconds": 2.0, "model_calls": 100}, 8)
+    assert row == {"samples": 8, "model_seconds": "2.000000", "model_samples_per_second": "4.000000",
+                   "model_seconds_per_sample": "0.25000000", "model_calls": 100}
+    empty = model_throughput({}, 0)
+    assert empty["model_samples_per_second"] == "0.000000" and empty["model_seconds_per_sample"] == "0.00000000"

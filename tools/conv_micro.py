@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--hw", type=int, default=256)
     ap.add_argument("--c", type=int, default=128)
     ap.add_argument("--dbg", default="", help="comma list of halo ablation flag values to time as well")
-    ap.add_argument("--variants", default="2", help="comma list of halo kernel variants to time (1, 2)")
+    ap.add_argument("--variants", default="1", help="(kept for the output format)")
     ap.add_argument("--staggers", default="", help="comma list of v2 stagger values to time (default: library's)")
     ap.add_argument("--warm", type=int, default=300, help="back-to-back launches before the first timing (clock ramp)")
     ap.add_argument("--cold", action="store_true", help="evict L2 / Infinity Cache (512 MiB write) before every call")
