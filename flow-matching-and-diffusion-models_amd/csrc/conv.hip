@@ -33,6 +33,10 @@ struct KArgs {
   int par;        // stride-2 transposed 3x3: one launch z-slice per output parity class (sub-pixel
                   // decomposition: only the 1/2/2/4 taps that hit a class are iterated, not all 9)
   int Mfull;      // N*Ho*Wo (== M unless par)
+  int pack;       // 1: the input has exactly 8 (padded) channels -- one 16-byte chunk per tap -- and a K-iteration
+                  // covers BK/8 consecutive TAPS (chunk j = tap kk*BK/8 + j, channels 0..7) instead of BK
+                  // channels of one tap: the UNet's input conv and the 1-channel head's data gradient (K = 9
+                  // or 27 taps x 8) run in ceil(T/(BK/8)) K-iterations, not T (7/8 of each was zero padding)
 };
 
 template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
@@ -119,7 +123,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
 
   auto load = [&](int kk) {
     int c, tap = 0, seg;
-    if (kk < nk1) {
+    if (kk < nk1 && A.pack) {
+      tap = kk * CH + cch;   // per-thread tap; >= T past the end (zeros)
+      c = 0;
+      seg = 0;
+    } else if (kk < nk1) {
       const int cb = kk / Tc;
       tap = kk - cb * Tc;
       if (A.par) {   // class-local tap -> 3x3 tap
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
       u32x4 v = {0u, 0u, 0u, 0u};
       if (r < BCO && co < d.K) {
         if (seg == 0) {
-          if (c < A.C) v = *(const u32x4*)(w1 + ((size_t)co * A.T + tap) * A.C + c);
+          if (c < A.C && tap < A.T) v = *(const u32x4*)(w1 + ((size_t)co * A.T + tap) * A.C + c);
         } else {
           if (c < C23) v = *(const u32x4*)(w2 + (size_t)co * C23 + c);
         }
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
           }
           ok = ok && sy < d.Hs && sx < d.Ws && sz < Dsz;
         }
-        ok = ok && c < A.C;
+        ok = ok && c < A.C && tap < A.T;
         if (ok) {
           const size_t pix = (((size_t)n * Dsz + sz) * d.Hs + sy) * d.Ws + sx;
           ptr = (c < d.C0) ? s0 + pix * d.C0 + c : s1 + pix * d.C1 + (c - d.C0);
@@ -664,13 +672,14 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   A.M = d->N * Dz * d->Ho * d->Wo;
   A.T = d->ks * d->ks * (d->Do > 0 ? d->ks : 1);
   A.C = d->C0 + d->C1;
-  A.nk1 = ((A.C + BK - 1) / BK) * A.T;
+  A.pack = A.C == 8 && BK >= 16 && !GNA;
+  A.nk1 = A.pack ? (A.T + BK / 8 - 1) / (BK / 8) : ((A.C + BK - 1) / BK) * A.T;
   A.nk = A.nk1 + (d->src2 ? (d->C2 + d->C3 + BK - 1) / BK : 0);
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nk + splits - 1) / splits;
   A.Mfull = A.M;
   A.par = d->Do == 0 && d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
-          !d->stats && !d->src2 && !GNA;
+          !d->stats && !d->src2 && !GNA && !A.pack;
   if (A.par) A.M = d->N * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
   A.ntp = (A.M + BPX - 1) / BPX;
   A.ntc = (d->K + BCO - 1) / BCO;

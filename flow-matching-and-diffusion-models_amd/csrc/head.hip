@@ -33,9 +33,10 @@ constexpr int NTH = 256;
 FMD_DEV int hp_pos(int h) { return (h >> 5) * 8 + (h & 7); }
 FMD_DEV int hp_kc(int h) { return (h >> 3) & (KCP - 1); }
 
-// stage the GN+SiLU-transformed halo of channels [c0, c0+32) of tile (n, ty0, tx0) into halo[4][336]
-FMD_DEV void stage_halo(u32x4* halo, const bf16r* __restrict__ h, int n, int H, int W, int C, int ty0, int tx0,
-                        int c0, const float* __restrict__ pa, const float* __restrict__ pb, int tid) {
+// stage the GN+SiLU-transformed halo of channels [c0, c0+32) of tile (ty0, tx0) of slice sl (= n*D + z;
+// sample n's GroupNorm affine) into halo[4][336]
+FMD_DEV void stage_halo(u32x4* halo, const bf16r* __restrict__ h, int sl, int n, int H, int W, int C, int ty0,
+                        int tx0, int c0, const float* __restrict__ pa, const float* __restrict__ pb, int tid) {
   constexpr int TOT = ((HPOS + 7) / 8) * 8 * KCP;   // 1312 pieces
   for (int q = tid; q < TOT; q += NTH) {
     const int pos = hp_pos(q), kc = hp_kc(q);
@@ -44,7 +45,7 @@ FMD_DEV void stage_halo(u32x4* halo, const bf16r* __restrict__ h, int n, int H, 
     u32x4 v = {0u, 0u, 0u, 0u};
     if (y >= 0 && y < H && x >= 0 && x < W) {
       const int c = c0 + kc * 8;
-      const u32x4 r = *(const u32x4*)(h + ((size_t)(n * H + y) * W + x) * C + c);
+      const u32x4 r = *(const u32x4*)(h + ((size_t)(sl * H + y) * W + x) * C + c);
       const f32x4 a0 = *(const f32x4*)(pa + (size_t)n * C + c), a1 = *(const f32x4*)(pa + (size_t)n * C + c + 4);
       const f32x4 b0 = *(const f32x4*)(pb + (size_t)n * C + c), b1 = *(const f32x4*)(pb + (size_t)n * C + c + 4);
       const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
@@ -58,39 +59,58 @@ FMD_DEV void stage_halo(u32x4* halo, const bf16r* __restrict__ h, int n, int H, 
 }
 
 struct HeadArgs {
-  const bf16r* h;       // [N][H][W][C] GN input
+  const bf16r* h;       // [N][D][H][W][C] GN input (D = 1 for 2-D data)
   const float* pa;      // [N][C]
   const float* pb;
-  const float* w;       // [K][C][3][3]
+  const float* w;       // [K][C][T] (T = 9: [3][3]; T = 27: [3][3][3])
   const float* bias;    // [K] or null
   const bf16r* dpred;   // [N][H][W][8]
   float* out;           // fp32 [N][H][W][Kp]
   bf16r* dz;            // [N][H][W][C]
   float* stats;         // [N*H*W/64][C][2]
   float* ws;            // wgrad partials
-  int N, H, W, C, K, Kp;
+  int N, D, H, W, C, K, Kp, T;
   int tiles_x, tiles_y, ntiles, tiles_per_wg;
 };
 
-template <int KT>
+// tile -> (slice sl = n*D + z, sample n, depth z, tile origin); tiles run x, then y, then slice
+struct TilePos {
+  int sl, n, z, ty0, tx0;
+};
+FMD_DEV TilePos tile_pos(const HeadArgs& A, int t) {
+  const int per = A.tiles_x * A.tiles_y;
+  TilePos P;
+  P.sl = t / per;
+  const int tr = t - P.sl * per;
+  P.n = P.sl / A.D;
+  P.z = P.sl - P.n * A.D;
+  P.ty0 = (tr / A.tiles_x) * HT;
+  P.tx0 = (tr % A.tiles_x) * HT;
+  return P;
+}
+
+// KZ = 1: 2-D; KZ = 3: 3-D (one depth plane of taps per pass over the chunk, zero depth padding)
+template <int KT, int KZ>
 __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
   __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
   __shared__ __attribute__((aligned(16))) unsigned int wl[KT][9][CK / 2];   // chunk weights [k][tap][c pair], bf16x2
   const int tid = threadIdx.x;
-  const int tile = blockIdx.x, per = A.tiles_x * A.tiles_y;
-  const int n = tile / per, tr = tile - n * per;
-  const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+  const TilePos P = tile_pos(A, blockIdx.x);
+  const int n = P.n, ty0 = P.ty0, tx0 = P.tx0;
   const int py = tid >> 4, px = tid & 15;
   // two accumulators per output channel (the 8-channel pieces alternate), fp32 throughout
   float acc[KT][2];
 #pragma unroll
   for (int k = 0; k < KT; ++k) acc[k][0] = acc[k][1] = 0.f;
-  for (int c0 = 0; c0 < A.C; c0 += CK) {
-    stage_halo(halo, A.h, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
+  for (int c0 = 0; c0 < A.C; c0 += CK)
+  for (int kz = 0; kz < KZ; ++kz) {
+    const int zz = P.z + kz - KZ / 2;
+    if (zz < 0 || zz >= A.D) continue;   // zero depth padding (uniform over the workgroup)
+    stage_halo(halo, A.h, P.sl + zz - P.z, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
     for (int i = tid; i < KT * 9 * (CK / 2); i += NTH) {
       const int k = i / (9 * (CK / 2)), r = i - k * 9 * (CK / 2), tap = r / (CK / 2), cp = r - tap * (CK / 2);
-      const size_t w0 = ((size_t)k * A.C + c0 + 2 * cp) * 9 + tap;
-      wl[k][tap][cp] = k < A.K ? pack2(A.w[w0], A.w[w0 + 9]) : 0u;
+      const size_t w0 = ((size_t)k * A.C + c0 + 2 * cp) * (9 * KZ) + kz * 9 + tap;
+      wl[k][tap][cp] = k < A.K ? pack2(A.w[w0], A.w[w0 + 9 * KZ]) : 0u;
     }
     __syncthreads();
     // bf16 operands straight from LDS into v_dot2c_f32_bf16 (two products per op, fp32 accumulate):
@@ -119,7 +139,7 @@ __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
     }
     __syncthreads();
   }
-  const size_t p = ((size_t)(n * A.H) + ty0 + py) * A.W + tx0 + px;
+  const size_t p = ((size_t)(P.sl * A.H) + ty0 + py) * A.W + tx0 + px;
   float* o = A.out + p * A.Kp;
   for (int k = 0; k < A.Kp; k += 4) {
     f32x4 v;
@@ -136,31 +156,33 @@ __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
   }
 }
 
-// dz[p][c] = silu'(a x + b) * sum_{tap,k} dpred[p - tap + 1][k] W[k][c][tap]; stats (sum dz, sum dz*x)
-template <int KT>
+// dz[p][c] = silu'(a x + b) * sum_{tap,k} dpred[p - tap + 1][k] W[k][c][tap]; stats (sum dz, sum dz*x).
+// KZ = 3 (3-D): the dpred halos of slices z+1, z, z-1 (depth taps 0, 1, 2) and all 27 taps' weights in LDS
+template <int KT, int KZ>
 __global__ __launch_bounds__(256) void head_dgrad(const HeadArgs A) {
-  __shared__ __attribute__((aligned(16))) float dp[HPOS][KT];          // dpred halo (fp32)
-  __shared__ __attribute__((aligned(16))) float wl[9][KT][128];        // weights of this 128-channel block
+  __shared__ __attribute__((aligned(16))) float dp[KZ][HPOS][KT];          // dpred halos (fp32)
+  __shared__ __attribute__((aligned(16))) float wl[9 * KZ][KT][128];       // weights of this 128-channel block
   const int tid = threadIdx.x;
-  const int tile = blockIdx.x, per = A.tiles_x * A.tiles_y;
-  const int n = tile / per, tr = tile - n * per;
-  const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+  const TilePos P = tile_pos(A, blockIdx.x);
+  const int n = P.n, ty0 = P.ty0, tx0 = P.tx0;
   const int cb0 = blockIdx.y * 128;
   const int g = tid & 15, r = tid >> 4;   // 8 channels x one tile row
-  for (int pos = tid; pos < HPOS; pos += NTH) {
+  for (int i = tid; i < KZ * HPOS; i += NTH) {
+    const int kz = i / HPOS, pos = i - kz * HPOS;
+    const int zz = P.z - kz + KZ / 2;
     const int y = ty0 - 1 + pos / HR, x = tx0 - 1 + pos % HR;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (y >= 0 && y < A.H && x >= 0 && x < A.W) {
-      const u32x4 q = *(const u32x4*)(A.dpred + ((size_t)(n * A.H + y) * A.W + x) * 8);
+    if (zz >= 0 && zz < A.D && y >= 0 && y < A.H && x >= 0 && x < A.W) {
+      const u32x4 q = *(const u32x4*)(A.dpred + ((size_t)((P.sl + zz - P.z) * A.H + y) * A.W + x) * 8);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[2 * e] = bf_lo(q[e]); v[2 * e + 1] = bf_hi(q[e]); }
     }
 #pragma unroll
-    for (int k = 0; k < KT; ++k) dp[pos][k] = v[k];
+    for (int k = 0; k < KT; ++k) dp[kz][pos][k] = v[k];
   }
-  for (int i = tid; i < 9 * KT * 128; i += NTH) {
+  for (int i = tid; i < 9 * KZ * KT * 128; i += NTH) {
     const int tap = i / (KT * 128), rr = i - tap * KT * 128, k = rr / 128, c = rr - k * 128;
-    wl[tap][k][c] = (k < A.K && cb0 + c < A.C) ? A.w[((size_t)k * A.C + cb0 + c) * 9 + tap] : 0.f;
+    wl[tap][k][c] = (k < A.K && cb0 + c < A.C) ? A.w[((size_t)k * A.C + cb0 + c) * (9 * KZ) + tap] : 0.f;
   }
   __syncthreads();
   const int c = cb0 + g * 8;
@@ -177,19 +199,19 @@ __global__ __launch_bounds__(256) void head_dgrad(const HeadArgs A) {
   for (int x = 0; x < HT; ++x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
+    for (int tap = 0; tap < 9 * KZ; ++tap) {
+      const int ky = (tap % 9) / 3, kx = tap % 3;
       const int pos = (r + 2 - ky) * HR + x + 2 - kx;
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
-        const float d = dp[pos][k];
+        const float d = dp[tap / 9][pos][k];
         const f32x4 w0 = *(const f32x4*)&wl[tap][k][g * 8], w1 = *(const f32x4*)&wl[tap][k][g * 8 + 4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) { acc[e] += d * w0[e]; acc[4 + e] += d * w1[e]; }
       }
     }
     if (cok) {
-      const size_t p = ((size_t)(n * A.H) + ty0 + r) * A.W + tx0 + x;
+      const size_t p = ((size_t)(P.sl * A.H) + ty0 + r) * A.W + tx0 + x;
       const u32x4 xr = *(const u32x4*)(A.h + p * A.C + c);
       u32x4 o;
 #pragma unroll
@@ -213,7 +235,7 @@ __global__ __launch_bounds__(256) void head_dgrad(const HeadArgs A) {
     s2[e] += __shfl_xor(s2[e], 32, 64);
   }
   if ((r & 3) == 0 && cok) {
-    const int srow = tile * 4 + (r >> 2);
+    const int srow = blockIdx.x * 4 + (r >> 2);
     float* sp = A.stats + ((size_t)srow * A.C + c) * 2;
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sp[2 * e] = s1[e]; sp[2 * e + 1] = s2[e]; }
@@ -221,44 +243,48 @@ __global__ __launch_bounds__(256) void head_dgrad(const HeadArgs A) {
 }
 
 // per-workgroup partials: slot[wg] = {[k][c][tap] (reference layout per k), [k] bias}; the workgroup
-// owns tiles [wg*tpw, (wg+1)*tpw) and keeps its sums in registers across them, chunk by chunk
-template <int KT>
+// owns tiles [wg*tpw, (wg+1)*tpw) and keeps its sums in registers across them, chunk by chunk (3-D: and
+// depth tap by depth tap, the halo taken from slice z + kz - 1; the bias sums ride on the centre pass)
+template <int KT, int KZ>
 __global__ __launch_bounds__(256) void head_wgrad(const HeadArgs A) {
   __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
   __shared__ __attribute__((aligned(16))) float dp[256][KT];
   __shared__ __attribute__((aligned(16))) float red[7][36][KT * 8];
   __shared__ float bsum[4][KT];
   const int tid = threadIdx.x;
-  const int per = A.tiles_x * A.tiles_y;
   const int combo = tid % 36, phase = tid / 36;   // 7 phases x 36 (kc, tap); threads 252..255 only stage
   const int kc = combo / 9, tap = combo % 9;
-  const size_t slot = (size_t)KT * A.C * 9 + KT;
+  const size_t slot = (size_t)KT * A.C * 9 * KZ + KT;
   float* wsw = A.ws + (size_t)blockIdx.x * slot;
   const int t0 = blockIdx.x * A.tiles_per_wg, t1 = min(A.ntiles, t0 + A.tiles_per_wg);
   float dbs[KT];
 #pragma unroll
   for (int k = 0; k < KT; ++k) dbs[k] = 0.f;
-  for (int c0 = 0; c0 < A.C; c0 += CK) {
+  for (int c0 = 0; c0 < A.C; c0 += CK)
+  for (int kz = 0; kz < KZ; ++kz) {
+    const bool bias_pass = c0 == 0 && kz == KZ / 2;
     float acc[KT][8];
 #pragma unroll
     for (int k = 0; k < KT; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
     for (int t = t0; t < t1; ++t) {
-      const int n = t / per, tr = t - n * per;
-      const int ty0 = (tr / A.tiles_x) * HT, tx0 = (tr % A.tiles_x) * HT;
+      const TilePos P = tile_pos(A, t);
+      const int ty0 = P.ty0, tx0 = P.tx0;
+      const int zz = P.z + kz - KZ / 2;
+      if (zz < 0 || zz >= A.D) continue;   // zero depth padding: no contribution (uniform over the workgroup)
       {
         const int py = tid >> 4, px = tid & 15;
-        const u32x4 q = *(const u32x4*)(A.dpred + (((size_t)(n * A.H) + ty0 + py) * A.W + tx0 + px) * 8);
+        const u32x4 q = *(const u32x4*)(A.dpred + (((size_t)(P.sl * A.H) + ty0 + py) * A.W + tx0 + px) * 8);
         const float v[8] = {bf_lo(q[0]), bf_hi(q[0]), bf_lo(q[1]), bf_hi(q[1]),
                             bf_lo(q[2]), bf_hi(q[2]), bf_lo(q[3]), bf_hi(q[3])};
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
           dp[tid][k] = v[k];
-          if (c0 == 0) dbs[k] += v[k];
+          if (bias_pass) dbs[k] += v[k];
         }
       }
-      stage_halo(halo, A.h, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
+      stage_halo(halo, A.h, P.sl + zz - P.z, P.n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
       __syncthreads();
       if (phase < 7) {
         for (int p = phase; p < 256; p += 7) {
@@ -289,7 +315,7 @@ __global__ __launch_bounds__(256) void head_wgrad(const HeadArgs A) {
       float sum = 0.f;
 #pragma unroll
       for (int ph = 0; ph < 7; ++ph) sum += red[ph][cmb][r];
-      wsw[((size_t)k * A.C + c0 + (cmb / 9) * 8 + e) * 9 + cmb % 9] = sum;
+      wsw[((size_t)k * A.C + c0 + (cmb / 9) * 8 + e) * (9 * KZ) + kz * 9 + cmb % 9] = sum;
     }
     __syncthreads();
   }
@@ -316,115 +342,119 @@ __global__ void slot_sum(const float* __restrict__ in, int nslots, size_t stride
   out[(size_t)blockIdx.y * len + i] = s0 + s1;
 }
 
-// dw[k][c][tap] += sum_s part[s][k][c][tap];  db[k] += sum_s part[s][KT*C*9 + k]
-__global__ void head_wgrad_finish(const float* __restrict__ part, int ns, int KT, int K, int C, float* __restrict__ dw,
-                                  float* __restrict__ db) {
-  const int len = KT * C * 9 + KT;
+// dw[k][c][tap] += sum_s part[s][k][c][tap];  db[k] += sum_s part[s][KT*C*T + k]  (T = 9 or 27 taps)
+__global__ void head_wgrad_finish(const float* __restrict__ part, int ns, int KT, int K, int C, int T,
+                                  float* __restrict__ dw, float* __restrict__ db) {
+  const int len = KT * C * T + KT;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   float s = 0.f;
-  if (i < K * C * 9) {
+  if (i < K * C * T) {
     for (int g = 0; g < ns; ++g) s += part[(size_t)g * len + i];
     dw[i] += s;
-  } else if (db && i >= KT * C * 9 && i < KT * C * 9 + K) {
+  } else if (db && i >= KT * C * T && i < KT * C * T + K) {
     for (int g = 0; g < ns; ++g) s += part[(size_t)g * len + i];
-    db[i - KT * C * 9] += s;
+    db[i - KT * C * T] += s;
   }
 }
 
 int kt_of(int K) { return K <= 1 ? 1 : K <= 2 ? 2 : K <= 4 ? 4 : 8; }
 
-HeadArgs make(const void* h, int N, int H, int W, int C, const float* pa, const float* pb, const float* w, int K) {
+// D == 0: 2-D data and [K][C][3][3] weights; D >= 1: 3-D data [N][D][H][W][C] and [K][C][3][3][3] weights
+HeadArgs make(const void* h, int N, int D, int H, int W, int C, const float* pa, const float* pb, const float* w,
+              int K) {
   HeadArgs A{};
   A.h = (const bf16r*)h;
   A.pa = pa;
   A.pb = pb;
   A.w = w;
-  A.N = N; A.H = H; A.W = W; A.C = C; A.K = K; A.Kp = 8;
+  A.N = N; A.D = D > 0 ? D : 1; A.H = H; A.W = W; A.C = C; A.K = K; A.Kp = 8;
+  A.T = D > 0 ? 27 : 9;
   A.tiles_x = W / HT;
   A.tiles_y = H / HT;
-  A.ntiles = N * A.tiles_x * A.tiles_y;
+  A.ntiles = N * A.D * A.tiles_x * A.tiles_y;
   return A;
 }
 
-bool shape_ok(int N, int H, int W, int C, int K) {
-  return N > 0 && H % HT == 0 && W % HT == 0 && C % CK == 0 && K >= 1 && K <= 8 &&
-         (long long)N * H * W * C < (1LL << 31);
+// 3-D: K <= 2 (the dgrad kernel keeps all 27 taps' weights of a 128-channel block in LDS)
+bool shape_ok(int N, int D, int H, int W, int C, int K) {
+  return N > 0 && D >= 0 && H % HT == 0 && W % HT == 0 && C % CK == 0 && K >= 1 && K <= (D > 0 ? 2 : 8) &&
+         (long long)N * (D > 0 ? D : 1) * H * W * C < (1LL << 31);
 }
 
 constexpr int WG_WGRAD = 1024;  // head_wgrad workgroups (each loops over its share of tiles; 4 per CU at 256^2)
 constexpr int RED_SPLIT = 32;   // first reduction stage: WG_WGRAD slots -> RED_SPLIT partial sums
 
+// launch KERNEL<KT, KZ> for the runtime (K, D): KZ = 3 for 3-D (KT <= 2 there), 1 for 2-D
+#define HEAD_LAUNCH(KERNEL, grid, A, st)                                                          \
+  do {                                                                                            \
+    if ((A).T == 27) {                                                                            \
+      if (kt_of((A).K) == 1) hipLaunchKernelGGL((KERNEL<1, 3>), grid, dim3(NTH), 0, st, A);      \
+      else hipLaunchKernelGGL((KERNEL<2, 3>), grid, dim3(NTH), 0, st, A);                         \
+    } else {                                                                                      \
+      switch (kt_of((A).K)) {                                                                     \
+        case 1: hipLaunchKernelGGL((KERNEL<1, 1>), grid, dim3(NTH), 0, st, A); break;             \
+        case 2: hipLaunchKernelGGL((KERNEL<2, 1>), grid, dim3(NTH), 0, st, A); break;             \
+        case 4: hipLaunchKernelGGL((KERNEL<4, 1>), grid, dim3(NTH), 0, st, A); break;             \
+        default: hipLaunchKernelGGL((KERNEL<8, 1>), grid, dim3(NTH), 0, st, A); break;            \
+      }                                                                                           \
+    }                                                                                             \
+  } while (0)
+
 }  // namespace
 
 extern "C" {
 
-int fmd_head_fwd(const void* h, int32_t N, int32_t H, int32_t W, int32_t C, const float* pro_a, const float* pro_b,
-                 const float* w, const float* bias, int32_t K, float* out, fmd_stream_t s) {
-  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b) return -1;
-  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, w, K);
+int fmd_head_fwd(const void* h, int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, const float* pro_a,
+                 const float* pro_b, const float* w, const float* bias, int32_t K, float* out, fmd_stream_t s) {
+  if (!shape_ok(N, D, H, W, C, K) || !pro_a || !pro_b) return -1;
+  HeadArgs A = make(h, N, D, H, W, C, pro_a, pro_b, w, K);
   A.bias = bias;
   A.out = out;
-  const dim3 g(A.ntiles);
   hipStream_t st = (hipStream_t)s;
-  switch (kt_of(K)) {
-    case 1: hipLaunchKernelGGL(head_fwd<1>, g, dim3(NTH), 0, st, A); break;
-    case 2: hipLaunchKernelGGL(head_fwd<2>, g, dim3(NTH), 0, st, A); break;
-    case 4: hipLaunchKernelGGL(head_fwd<4>, g, dim3(NTH), 0, st, A); break;
-    default: hipLaunchKernelGGL(head_fwd<8>, g, dim3(NTH), 0, st, A); break;
-  }
+  HEAD_LAUNCH(head_fwd, dim3(A.ntiles), A, st);
   return (int)hipGetLastError();
 }
 
 int fmd_head_dgrad(const void* dpred, const float* w, int32_t K, const void* h, const float* pro_a, const float* pro_b,
-                   int32_t N, int32_t H, int32_t W, int32_t C, void* dz, float* stats, fmd_stream_t s) {
-  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b || !stats) return -1;
-  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, w, K);
+                   int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, void* dz, float* stats, fmd_stream_t s) {
+  if (!shape_ok(N, D, H, W, C, K) || !pro_a || !pro_b || !stats) return -1;
+  HeadArgs A = make(h, N, D, H, W, C, pro_a, pro_b, w, K);
   A.dpred = (const bf16r*)dpred;
   A.dz = (bf16r*)dz;
   A.stats = stats;
-  const dim3 g(A.ntiles, (C + 127) / 128);
   hipStream_t st = (hipStream_t)s;
-  switch (kt_of(K)) {
-    case 1: hipLaunchKernelGGL(head_dgrad<1>, g, dim3(NTH), 0, st, A); break;
-    case 2: hipLaunchKernelGGL(head_dgrad<2>, g, dim3(NTH), 0, st, A); break;
-    case 4: hipLaunchKernelGGL(head_dgrad<4>, g, dim3(NTH), 0, st, A); break;
-    default: hipLaunchKernelGGL(head_dgrad<8>, g, dim3(NTH), 0, st, A); break;
-  }
+  HEAD_LAUNCH(head_dgrad, dim3(A.ntiles, (C + 127) / 128), A, st);
   return (int)hipGetLastError();
 }
 
-int64_t fmd_head_wgrad_workspace(int32_t N, int32_t H, int32_t W, int32_t C, int32_t K) {
+int64_t fmd_head_wgrad_workspace(int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, int32_t K) {
   (void)N; (void)H; (void)W;
   const int kt = kt_of(K);
-  return (int64_t)(WG_WGRAD + RED_SPLIT) * ((int64_t)kt * C * 9 + kt);
+  return (int64_t)(WG_WGRAD + RED_SPLIT) * ((int64_t)kt * C * (D > 0 ? 27 : 9) + kt);
 }
 
 int fmd_head_wgrad(const void* dpred, int32_t K, const void* h, const float* pro_a, const float* pro_b, int32_t N,
-                   int32_t H, int32_t W, int32_t C, float* dw, float* db, float* ws, fmd_stream_t s) {
-  if (!shape_ok(N, H, W, C, K) || !pro_a || !pro_b || !ws || !dw) return -1;
-  HeadArgs A = make(h, N, H, W, C, pro_a, pro_b, nullptr, K);
+                   int32_t D, int32_t H, int32_t W, int32_t C, float* dw, float* db, float* ws, fmd_stream_t s) {
+  if (!shape_ok(N, D, H, W, C, K) || !pro_a || !pro_b || !ws || !dw) return -1;
+  HeadArgs A = make(h, N, D, H, W, C, pro_a, pro_b, nullptr, K);
   A.dpred = (const bf16r*)dpred;
   A.ws = ws;
   const int nwg = A.ntiles < WG_WGRAD ? A.ntiles : WG_WGRAD;
   A.tiles_per_wg = (A.ntiles + nwg - 1) / nwg;
   const int kt = kt_of(K);
   hipStream_t st = (hipStream_t)s;
-  switch (kt) {
-    case 1: hipLaunchKernelGGL(head_wgrad<1>, dim3(nwg), dim3(NTH), 0, st, A); break;
-    case 2: hipLaunchKernelGGL(head_wgrad<2>, dim3(nwg), dim3(NTH), 0, st, A); break;
-    case 4: hipLaunchKernelGGL(head_wgrad<4>, dim3(nwg), dim3(NTH), 0, st, A); break;
-    default: hipLaunchKernelGGL(head_wgrad<8>, dim3(nwg), dim3(NTH), 0, st, A); break;
-  }
+  HEAD_LAUNCH(head_wgrad, dim3(nwg), A, st);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  const int len = kt * C * 9 + kt;
+  const int len = kt * C * A.T + kt;
   float* part = ws + (size_t)WG_WGRAD * len;
   const int per_split = (nwg + RED_SPLIT - 1) / RED_SPLIT;
   hipLaunchKernelGGL(slot_sum, dim3((len + 255) / 256, RED_SPLIT), dim3(256), 0, st, ws, nwg, (size_t)len, len,
                      per_split, part);
   rc = (int)hipGetLastError();
   if (rc) return rc;
-  hipLaunchKernelGGL(head_wgrad_finish, dim3((len + 255) / 256), dim3(256), 0, st, part, RED_SPLIT, kt, K, C, dw, db);
+  hipLaunchKernelGGL(head_wgrad_finish, dim3((len + 255) / 256), dim3(256), 0, st, part, RED_SPLIT, kt, K, C, A.T, dw,
+                     db);
   return (int)hipGetLastError();
 }
 

@@ -22,7 +22,8 @@ constexpr int BCO = 128, BCI = 128, BKP = 32;
 struct WArgs {
   fmd_wgrad_desc d;
   int M, T, C, ntc, nci, per_split, nsteps, ldy;
-  int merged;   // C*T <= BCI: the (tap, cin) pairs share one column tile (a narrow stem conv)
+  int merged;   // C < BCI: the column tiles run over the flattened (tap, cin) pairs (narrow convs: the stem, the
+                // 3-D input conv with 27 taps x 8 channels = 2 tiles instead of 27 tiles of 8 valid columns)
 };
 
 // 8-byte unit swizzle for the [32][128] bf16 tile (256-B rows): conflict-free
@@ -45,8 +46,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   const int co0 = tco * BCO, ci0 = tci * BCI;
   // this thread's gather column chunk -> (tap, channel); merged mode spreads the taps over the chunks
   const int cpt = A.C >> 3;                        // 8-channel chunks per tap
-  const int my_tap = A.merged ? (tid & 15) / cpt : tap;
-  const int my_c = A.merged ? ((tid & 15) - my_tap * cpt) * 8 : ci0 + (tid & 15) * 8;
+  const int qc = tci * (BCI / 8) + (tid & 15);     // merged: flattened (tap, chunk) index of this column chunk
+  const int my_tap = A.merged ? qc / cpt : tap;
+  const int my_c = A.merged ? (qc - my_tap * cpt) * 8 : ci0 + (tid & 15) * 8;
   const bool col_ok = A.merged ? my_tap < A.T : my_c < A.C;
   const int kk2 = d.ks * d.ks;
   const int kz = my_tap / kk2, t2 = my_tap - (my_tap / kk2) * kk2;   // kz = 0 in 2-D
@@ -210,8 +212,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = wn * 64 + 16 * j + l16;
-      const int ci = A.merged ? col % A.C : ci0 + col;
-      const int ct = A.merged ? col / A.C : tap;
+      const int fq = tci * BCI + col;   // merged: flattened (tap, cin) column
+      const int ci = A.merged ? fq % A.C : ci0 + col;
+      const int ct = A.merged ? fq / A.C : tap;
       if (A.merged ? ct >= A.T : ci >= A.C) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -318,7 +321,8 @@ WArgs make_args(const fmd_wgrad_desc* d) {
   A.ldy = d->ldy > 0 ? d->ldy : d->K;
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nsteps + splits - 1) / splits;
-  A.merged = A.T > 1 && A.C * A.T <= BCI;
+  A.merged = A.T > 1 && A.C < BCI;
+  if (A.merged) A.nci = (A.T * A.C + BCI - 1) / BCI;   // column tiles of flattened (tap, cin) pairs
   return A;
 }
 
@@ -340,7 +344,7 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int splits = d->splits > 1 ? d->splits : 1;
   int rc = d->force_generic ? 1 : fmd_wgrad_halo(d, stream);
   if (rc == 1) {
-    dim3 grid(A.ntc * (A.merged ? 1 : A.nci * A.T), splits);
+    dim3 grid(A.ntc * (A.merged ? A.nci : A.nci * A.T), splits);
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, s, A);
     rc = (int)hipGetLastError();
   }

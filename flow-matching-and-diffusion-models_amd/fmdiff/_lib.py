@@ -136,10 +136,10 @@ SIGNATURES = {
     "fmd_fill_from_table": [p, p, p, i32, p],
     "fmd_gather_row": [p, p, i64, p, p],
     "fmd_counter_add": [p, i32, p],
-    "fmd_head_fwd": [p, i32, i32, i32, i32, p, p, p, p, i32, p, p],
-    "fmd_head_dgrad": [p, p, i32, p, p, p, i32, i32, i32, i32, p, p, p],
-    "fmd_head_wgrad_workspace": [i32, i32, i32, i32, i32],
-    "fmd_head_wgrad": [p, i32, p, p, p, i32, i32, i32, i32, p, p, p, p],
+    "fmd_head_fwd": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, p, p],
+    "fmd_head_dgrad": [p, p, i32, p, p, p, i32, i32, i32, i32, i32, p, p, p],
+    "fmd_head_wgrad_workspace": [i32, i32, i32, i32, i32, i32],
+    "fmd_head_wgrad": [p, i32, p, p, p, i32, i32, i32, i32, i32, p, p, p, p],
 }
 _RESTYPE = {"fmd_linear_attention_workspace": i64, "fmd_linear_attention_state": i64, "fmd_wgrad_workspace": i64, "fmd_head_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_grouped_linear_bwd_workspace": i64}
 

@@ -882,7 +882,8 @@ class UNetEngine:
         K = conv.out_channels
         Kp = max(CPAD, -(-K // 8) * 8)
         a, b, mr = ops.gn_prep(_stats(h), None, N, HW, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
-        if not bf16_out and Kp == CPAD and len(sp) == 2 and ops.head_eligible(*sp, Cc, K):
+        if (not bf16_out and Kp == CPAD and len(sp) in (2, 3)
+                and ops.head_eligible(*sp[-2:], Cc, K, sp[0] if len(sp) == 3 else 0)):
             # VALU head kernels (csrc/head.hip): the GN/SiLU transform once per element, no MFMA padding
             out = ops.head_fwd(h.t, (a, b), conv.weight, conv.bias, K, Kp)
             if ctx.tape is not None:

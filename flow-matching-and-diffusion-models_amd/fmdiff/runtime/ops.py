@@ -384,36 +384,44 @@ def conv_combine(ws, K, out_shape, *, bias=None, bias2=None, bias_nc=None, resid
     return out, st
 
 
-def head_eligible(H, W, C, K) -> bool:
-    """Mirror of the head kernels' shape test (csrc/head.hip)."""
-    return H % 16 == 0 and W % 16 == 0 and C % 32 == 0 and 1 <= K <= 8
+def head_eligible(H, W, C, K, D=0) -> bool:
+    """Mirror of the head kernels' shape test (csrc/head.hip); D > 0: 3-D data of depth D."""
+    return H % 16 == 0 and W % 16 == 0 and C % 32 == 0 and 1 <= K <= (2 if D else 8)
+
+
+def _head_dims(h):
+    """(N, D, H, W, C) of a 2-D NHWC (D = 0) or 3-D NDHWC head input."""
+    if h.dim() == 4:
+        N, H, W, Cc = h.shape
+        return N, 0, H, W, Cc
+    return tuple(h.shape)
 
 
 def head_fwd(h, pro, w, bias, K, Kp=8):
-    """out fp32 NHWC [N,H,W,Kp] = conv3x3(SiLU(a*h+b)) for the first K channels (csrc/head.hip)."""
+    """out fp32 channels-last [..., Kp] = conv3x3(x3)(SiLU(a*h+b)) for the first K channels (csrc/head.hip)."""
     _need_cuda(h, "head_fwd")
-    N, H, W, Cc = h.shape
-    out = torch.empty((N, H, W, Kp), device=h.device, dtype=F32)
-    _lib.call("fmd_head_fwd", _p(h), N, H, W, Cc, _p(pro[0]), _p(pro[1]), _p(w.contiguous()), _p(bias), K, _p(out),
-              stream())
+    N, D, H, W, Cc = _head_dims(h)
+    out = torch.empty((*h.shape[:-1], Kp), device=h.device, dtype=F32)
+    _lib.call("fmd_head_fwd", _p(h), N, D, H, W, Cc, _p(pro[0]), _p(pro[1]), _p(w.contiguous()), _p(bias), K,
+              _p(out), stream())
     return out
 
 
 def head_dgrad(dpred, w, K, h, pro):
-    """(dz bf16 NHWC, Stats(sum dz, sum dz*h)) of the head conv (csrc/head.hip)."""
-    N, H, W, Cc = h.shape
+    """(dz bf16 channels-last, Stats(sum dz, sum dz*h)) of the head conv (csrc/head.hip)."""
+    N, D, H, W, Cc = _head_dims(h)
     dz = torch.empty_like(h)
-    slab = torch.empty((N * H * W // 64, Cc, 2), device=h.device, dtype=F32)
-    _lib.call("fmd_head_dgrad", _p(dpred), _p(w.contiguous()), K, _p(h), _p(pro[0]), _p(pro[1]), N, H, W, Cc, _p(dz),
-              _p(slab), stream())
+    slab = torch.empty((h.numel() // Cc // 64, Cc, 2), device=h.device, dtype=F32)
+    _lib.call("fmd_head_dgrad", _p(dpred), _p(w.contiguous()), K, _p(h), _p(pro[0]), _p(pro[1]), N, D, H, W, Cc,
+              _p(dz), _p(slab), stream())
     return dz, Stats(slab, 64)
 
 
 def head_wgrad(dpred, K, h, pro, dw, db):
-    N, H, W, Cc = h.shape
-    n = int(_lib.lib().fmd_head_wgrad_workspace(N, H, W, Cc, K))
+    N, D, H, W, Cc = _head_dims(h)
+    n = int(_lib.lib().fmd_head_wgrad_workspace(N, D, H, W, Cc, K))
     ws = torch.empty((n,), device=h.device, dtype=F32)
-    _lib.call("fmd_head_wgrad", _p(dpred), K, _p(h), _p(pro[0]), _p(pro[1]), N, H, W, Cc, _p(dw), _p(db), _p(ws),
+    _lib.call("fmd_head_wgrad", _p(dpred), K, _p(h), _p(pro[0]), _p(pro[1]), N, D, H, W, Cc, _p(dw), _p(db), _p(ws),
               stream())
 
 

@@ -119,19 +119,20 @@ int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* 
 /* UNet output head: out = conv3x3(SiLU(a*h + b)) to K <= 8 channels, fp32 NHWC [N][H][W][8]
  * (channels >= K zero), replacing the final GroupNorm -> SiLU -> ConvND of
  * src/models/unet/unet.py:286-293 (unet_diffusers_nd.py conv_norm_out/conv_act/conv_out).
- * h: bf16 NHWC [N][H][W][C]; pro_a/pro_b: [N][C] GroupNorm affine; w: fp32 [K][C][3][3] (reference
- * layout); H, W multiples of 16, C a multiple of 32. */
-int fmd_head_fwd(const void* h, int32_t N, int32_t H, int32_t W, int32_t C, const float* pro_a, const float* pro_b,
-                 const float* w, const float* bias, int32_t K, float* out, fmd_stream_t s);
-/* Data gradient of the head: dz = silu'(a*h + b) * conv3x3^T(dpred) (bf16 [N][H][W][C]) and the
- * GroupNorm-backward sums (sum dz, sum dz*h) per 64-pixel slab row: stats [N*H*W/64][C][2].
- * dpred: bf16 NHWC [N][H][W][8]. */
+ * D == 0: 2-D, h bf16 NHWC [N][H][W][C], w fp32 [K][C][3][3] (reference layout).
+ * D >= 1: 3-D (ConvND with dims=3), h [N][D][H][W][C], w [K][C][3][3][3], out [N][D][H][W][8], zero depth
+ * padding; K <= 2.  pro_a/pro_b: [N][C] GroupNorm affine; H, W multiples of 16, C a multiple of 32. */
+int fmd_head_fwd(const void* h, int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, const float* pro_a,
+                 const float* pro_b, const float* w, const float* bias, int32_t K, float* out, fmd_stream_t s);
+/* Data gradient of the head: dz = silu'(a*h + b) * conv^T(dpred) (bf16, h's layout) and the
+ * GroupNorm-backward sums (sum dz, sum dz*h) per 64-pixel slab row: stats [N*D*H*W/64][C][2].
+ * dpred: bf16 [..][8] in h's layout; D as in fmd_head_fwd. */
 int fmd_head_dgrad(const void* dpred, const float* w, int32_t K, const void* h, const float* pro_a, const float* pro_b,
-                   int32_t N, int32_t H, int32_t W, int32_t C, void* dz, float* stats, fmd_stream_t s);
-/* Weight gradient of the head: dw[K][C][3][3] += sum_p dpred (x) SiLU(a*h + b), db[K] += sum_p dpred. */
-int64_t fmd_head_wgrad_workspace(int32_t N, int32_t H, int32_t W, int32_t C, int32_t K);
+                   int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, void* dz, float* stats, fmd_stream_t s);
+/* Weight gradient of the head: dw[K][C][taps] += sum_p dpred (x) SiLU(a*h + b), db[K] += sum_p dpred. */
+int64_t fmd_head_wgrad_workspace(int32_t N, int32_t D, int32_t H, int32_t W, int32_t C, int32_t K);
 int fmd_head_wgrad(const void* dpred, int32_t K, const void* h, const float* pro_a, const float* pro_b, int32_t N,
-                   int32_t H, int32_t W, int32_t C, float* dw, float* db, float* ws, fmd_stream_t s);
+                   int32_t D, int32_t H, int32_t W, int32_t C, float* dw, float* db, float* ws, fmd_stream_t s);
 
 /* Weight-gradient GEMM: dW[K][C][kh][kw] (+)= sum_p dY[p][K] x gather(src)[p][tap][C]
  * with the same gather/prologue as the forward; db[K] (+)= sum_p dY[p][K].

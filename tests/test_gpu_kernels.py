@@ -651,6 +651,47 @@ def test_head_kernels_vs_torch(K):
     torch.testing.assert_close(s[..., 1], (dzd * xs).sum(1), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("K", [1, 2])
+def test_head_kernels_3d_vs_torch(K):
+    """csrc/head.hip with depth (D > 0): GN-affine+SiLU -> 3x3x3 conv (zero depth padding) to K <= 2
+    channels, its data gradient + GN-backward sums and its weight/bias gradients, vs torch fp32 conv3d
+    autograd on the same bf16 inputs (the ConvND(dims=3) head of src/models/unet/unet.py:286-293).
+    Tolerance: 1e-2 x max|ref| as in the 2-D test."""
+    O = ops()
+    N, D, H, W, C = 2, 5, 16, 32, 64
+    g = torch.Generator().manual_seed(21)
+    h = (torch.randn(N, D, H, W, C, generator=g)).to(torch.bfloat16)
+    a = torch.rand(N, C, generator=g) + 0.5
+    b = torch.randn(N, C, generator=g) * 0.2
+    w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)
+    bias = torch.randn(K, generator=g) * 0.1
+    dpred = (torch.randn(N, D, H, W, 8, generator=g) * 0.5).to(torch.bfloat16)
+    dpred[..., K:] = 0
+    hd, ad, bd = h.to(DEV), a.to(DEV), b.to(DEV)
+    out = O.head_fwd(hd, (ad, bd), w.to(DEV), bias.to(DEV), K)
+    bc = (slice(None), slice(None), None, None, None)
+    z = h.float().permute(0, 4, 1, 2, 3) * a[bc] + b[bc]
+    wr = w.clone().requires_grad_()
+    br = bias.clone().requires_grad_()
+    zr = z.clone().requires_grad_()
+    ref = F.conv3d(F.silu(zr), wr, br, padding=1)
+    _close(out[..., :K], ref.permute(0, 2, 3, 4, 1), rel=1e-2)
+    assert out[..., K:].abs().max().item() == 0.0
+    ref.backward(dpred.float().permute(0, 4, 1, 2, 3)[:, :K])
+    dw = torch.zeros(K, C, 3, 3, 3, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    O.head_wgrad(dpred.to(DEV), K, hd, (ad, bd), dw, db)
+    _close(dw, wr.grad, rel=1e-2)
+    _close(db, br.grad, rel=1e-2)
+    dz, st = O.head_dgrad(dpred.to(DEV), w.to(DEV), K, hd, (ad, bd))
+    _close(dz, zr.grad.permute(0, 2, 3, 4, 1), rel=1e-2)
+    s = st.slab.double().cpu().view(N, -1, C, 2).sum(1)
+    xs = h.double().view(N, -1, C)
+    dzd = dz.double().cpu().view(N, -1, C)
+    torch.testing.assert_close(s[..., 0], dzd.sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(s[..., 1], (dzd * xs).sum(1), rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("C0,C1,Kd", [(128, 128, 128), (64, 0, 256), (256, 128, 128)])
 def test_conv1x1_gn_apply_vs_torch(C0, C1, Kd):
     """fmd_conv_gn_apply: the ResBlock skip-conv data gradient (dy @ W_skip) fused into the GroupNorm

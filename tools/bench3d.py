@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--graph", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))   # as bench.py: all work on a created stream
     from fmdiff.models.generators import DiffusionUNetFactory
     from fmdiff.pipelines.train.fused import FusedTrainStep
     torch.manual_seed(0)

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))   # as bench.py: all work on a created stream
     from fmdiff.models.generators import DiffusionUNetFactory
     from fmdiff.models.vae import AutoencoderKL
     from fmdiff.pipelines.latent import decode_vae_batch, encode_vae_batch
