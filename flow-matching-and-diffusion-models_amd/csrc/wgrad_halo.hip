@@ -78,8 +78,9 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
   const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
 
-  // this thread's staging slots: x channel group kx8 (fixed), dY channel group dc (fixed)
-  const int kx8 = tid & 7;
+  // this thread's staging slots: x channel group kx8 (fixed) at halo positions (tid & 7) + 8 * (tid >> 6) + 64 k,
+  // so the 8-lane groups of ds_write_b128 store 8 consecutive positions of one plane (32 distinct banks)
+  const int kx8 = (tid >> 3) & 7;
   const int c = ci0 + kx8 * 8;
   const bf16r* xsrc = (c < d.C0) ? s0 + c : s1 + (c - d.C0);
   const int xcs = (c < d.C0) ? d.C0 : d.C1;
@@ -115,8 +116,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
     const int srcsl = A.depth ? smp * A.dsrc + (d.upsample ? zl >> 1 : zl) : n;
 #pragma unroll
     for (int k = 0; k < XLD; ++k) {
-      const int q = tid + NT * k;
-      const int pos = q >> 3;
+      const int pos = (tid & 7) + 8 * (tid >> 6) + (NT / 8) * k;
       const bool act = pos < HPOSW;
       const int hy = act ? pos / HR : 0, hx = act ? pos - (pos / HR) * HR : 0;
       // logical (possibly nearest-x2-upsampled) input coordinates; the upsample is a gather of the
