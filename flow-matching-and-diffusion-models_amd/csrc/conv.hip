@@ -30,8 +30,9 @@ struct KArgs {
   int per_split;  // K-iterations per split
   int ntp, ntc;   // pixel tiles, cout tiles
   int stats_rows; // pixels per stats slab row (64) or 0
-  int par;        // stride-2 transposed 3x3: one launch z-slice per output parity class (sub-pixel
-                  // decomposition: only the 1/2/2/4 taps that hit a class are iterated, not all 9)
+  int par;        // stride-2 transposed 3x3(x3): one launch z-slice per output parity class (sub-pixel
+                  // decomposition: only the 1/2/2/4 taps that hit a class are iterated, not all 9; in 3-D
+                  // 8 classes of 1..8 of the 27 taps)
   int Mfull;      // N*Ho*Wo (== M unless par)
   int pack;       // 1: the input has exactly 8 (padded) channels -- one 16-byte chunk per tap -- and a K-iteration
                   // covers BK/8 consecutive TAPS (chunk j = tap kk*BK/8 + j, channels 0..7) instead of BK
@@ -64,10 +65,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   const int tco = b % A.ntc, tpx = b / A.ntc;
   const int co0 = tco * BCO, px0 = tpx * BPX;
   const int split = blockIdx.y;
-  // parity class (par): output pixels (2qy + cy, 2qx + cx); taps ky in {1} (cy = 0) or {0, 2} (cy = 1)
-  const int cy = A.par ? (int)(blockIdx.z >> 1) : 0, cx = A.par ? (int)(blockIdx.z & 1) : 0;
-  const int nkx = cx ? 2 : 1;
-  const int Tc = A.par ? (cy ? 2 : 1) * nkx : A.T;
+  // parity class (par): output pixels (2qz + cz, 2qy + cy, 2qx + cx); taps ky in {1} (cy = 0) or {0, 2}
+  // (cy = 1), likewise kx, kz (cz = 0 in 2-D)
+  const bool d3 = d.Do > 0;
+  const int cz = A.par && d3 ? (int)(blockIdx.z >> 2) : 0;
+  const int cy = A.par ? (int)((blockIdx.z >> 1) & 1) : 0, cx = A.par ? (int)(blockIdx.z & 1) : 0;
+  const int nkx = cx ? 2 : 1, nky = cy ? 2 : 1;
+  const int Tc = A.par ? (cz ? 2 : 1) * nky * nkx : A.T;
   const int nk1 = A.par ? ((A.C + BK - 1) / BK) * Tc : A.nk1;
   const int nkt = A.par ? nk1 : A.nk;
   const int per_split = A.par ? (nkt + (int)gridDim.y - 1) / (int)gridDim.y : A.per_split;
@@ -75,12 +79,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
   const int kk1 = min(nkt, kk0 + per_split);
   const int Wq = A.par ? d.Wo >> 1 : d.Wo;
   const int Dz = d.Do > 0 ? d.Do : 1;                       // output depth (3-D problems), 1 in 2-D
-  const int HWq = A.par ? (d.Ho >> 1) * Wq : Dz * d.Ho * d.Wo;
+  const int HWq = A.par ? (d3 ? Dz >> 1 : 1) * (d.Ho >> 1) * Wq : Dz * d.Ho * d.Wo;   // pixels per image
+  const int HWp = A.par ? (d.Ho >> 1) * Wq : d.Ho * d.Wo;   // pixels per output depth slice
   // pixel index of the layout (output tensor / split-K slab) for tile pixel p
   auto pmap = [&](int p) -> int {
     if (!A.par) return p;
-    const int n = p / HWq, rem = p - n * HWq, qy = rem / Wq, qx = rem - qy * Wq;
-    return (n * d.Ho + 2 * qy + cy) * d.Wo + 2 * qx + cx;
+    const int n = p / HWq, r0 = p - n * HWq, qz = r0 / HWp, rem = r0 - qz * HWp, qy = rem / Wq, qx = rem - qy * Wq;
+    return ((n * Dz + (d3 ? 2 * qz + cz : 0)) * d.Ho + 2 * qy + cy) * d.Wo + 2 * qx + cx;
   };
 
   const int HWo = Dz * d.Ho * d.Wo;
@@ -89,7 +94,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
 
   // per-thread pixel rows
   int pn[AX], poz[AX], poy[AX], pox[AX];
-  const int HWp = A.par ? HWq : d.Ho * d.Wo;   // pixels per output depth slice
 #pragma unroll
   for (int j = 0; j < AX; ++j) {
     const int p = px0 + rbase + j * RPP;
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
       rem -= poz[j] * HWp;
       poy[j] = rem / Wq;
       pox[j] = rem - poy[j] * Wq;
-      if (A.par) { poy[j] = 2 * poy[j] + cy; pox[j] = 2 * pox[j] + cx; }
+      if (A.par) { poz[j] = d3 ? 2 * poz[j] + cz : 0; poy[j] = 2 * poy[j] + cy; pox[j] = 2 * pox[j] + cx; }
     } else {
       pn[j] = -1; poz[j] = 0; poy[j] = 0; pox[j] = 0;
     }
@@ -130,9 +134,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
     } else if (kk < nk1) {
       const int cb = kk / Tc;
       tap = kk - cb * Tc;
-      if (A.par) {   // class-local tap -> 3x3 tap
-        const int iy = tap / nkx, ix = tap - (tap / nkx) * nkx;
-        tap = (cy ? 2 * iy : 1) * 3 + (cx ? 2 * ix : 1);
+      if (A.par) {   // class-local tap -> 3x3(x3) tap
+        const int iz = tap / (nky * nkx), r2 = tap - iz * (nky * nkx);
+        const int iy = r2 / nkx, ix = r2 - (r2 / nkx) * nkx;
+        tap = (cy ? 2 * iy : 1) * 3 + (cx ? 2 * ix : 1) + (d3 ? (cz ? 2 * iz : 1) * 9 : 0);
       }
       c = cb * BK + cch * 8;
       seg = 0;
@@ -168,7 +173,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
       const bf16r* ptr = nullptr;
       if (seg == 0) {
         int sz = 0, sy, sx;
-        const bool d3 = d.Do > 0;
         if (!d.transposed) {
           const int iz = d3 ? poz[j] * d.stride + kz - d.pad : 0;
           const int iy = poy[j] * d.stride + ky - d.pad;
@@ -678,9 +682,9 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nk + splits - 1) / splits;
   A.Mfull = A.M;
-  A.par = d->Do == 0 && d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
-          !d->stats && !d->src2 && !GNA && !A.pack;
-  if (A.par) A.M = d->N * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
+  A.par = d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
+          !(d->Do & 1) && !d->stats && !d->src2 && !GNA && !A.pack;
+  if (A.par) A.M = d->N * (d->Do > 0 ? d->Do / 2 : 1) * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
   A.ntp = (A.M + BPX - 1) / BPX;
   A.ntc = (d->K + BCO - 1) / BCO;
   A.stats_rows = 64;
@@ -689,7 +693,7 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
     const int wrows = BPX / WN;
     if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
   }
-  dim3 grid(A.ntp * A.ntc, splits, A.par ? 4 : 1);
+  dim3 grid(A.ntp * A.ntc, splits, A.par ? (d->Do > 0 ? 8 : 4) : 1);
   hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);
   return (int)hipGetLastError();
 }

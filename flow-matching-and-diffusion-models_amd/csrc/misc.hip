@@ -700,19 +700,24 @@ __global__ void glinear_dx_reduce(const float* __restrict__ part, int np, int B,
 
 // ------------------------------------------------------------------ batched weight layouts
 // One launch re-derives every bf16 kernel layout of the UNet from the fp32 masters after the
-// optimizer step.  A block owns a 32 (k) x 32 (c) tile of one master weight w[K][C][T]: it reads the
+// optimizer step.  A block owns a PTK (k) x 32 (c) tile of one master weight w[K][C][T]: it reads the
 // tile once (contiguous T*32-float runs per k) into LDS and writes every requested layout of it with
-// contiguous 64-512 B runs.  Layouts (see fmd_prep_weights, fmd_tile_weights_halo):
+// contiguous 32-512 B runs.  Layouts (see fmd_prep_weights, fmd_tile_weights_halo):
 //   kind 0 base: mode 0 [R=Kpad][T][Cc=Cpad]; modes 1/3 [R=Cpad][T][Cc=Kpad] (3: taps flipped);
 //                mode 2 [R=Cpad][16][Cc=Kpad] (upsample + 3x3 data gradient, 4x4 effective taps)
 //   kind 1 halo tiles of a base layout: [ceil(R/128)][ceil(Cc/BK)][T][BK/8][128][8], BK = FMD_HALO_BK
+//   kind 2 (3x3x3 weights only) depth-packed halo tiles: the 2-D tiles of the [R][3 * Cr][3][3] view whose
+//          channel block kz * Cr + c holds depth tap kz of channel c (Cr = Cc rounded up to BK), i.e.
+//          [ceil(R/128)][3 * Cr / BK][9][BK/8][128][8] -- the depth-tap halo kernel's weights (modes 0, 3)
 // Job (16 x int64): w, K | C << 32, ks | nout << 32, first block | kt << 32 (k tiles),
 //                   then per output (<= 6): out, mode | kind << 8 | R << 16 | Cc << 40.
-constexpr int PT = 32;          // k and c tile
-constexpr int PTS = PT * 9 + 1; // LDS row stride (floats) per k: conflict-free transposed reads
+// TT: taps the LDS tile holds (9: ks <= 3 square kernels, T = ks * ks; 27: cubic 3x3x3 kernels, PTK = 16).
+constexpr int PT = 32;          // c tile
 
+template <int TT>
 FMD_DEV float ptile_value(const float* tile, int kl, int cl, int ks, int mode, int tap) {
-  const int T = ks * ks;
+  constexpr int PTS = PT * TT + 1;   // LDS row stride (floats) per k: conflict-free transposed reads
+  const int T = TT == 27 ? 27 : ks * ks;
   if (mode == 0 || mode == 1) return tile[kl * PTS + cl * T + tap];
   if (mode == 3) return tile[kl * PTS + cl * T + (T - 1 - tap)];
   const int ry = tap >> 2, rx = tap & 3;
@@ -724,8 +729,11 @@ FMD_DEV float ptile_value(const float* tile, int kl, int cl, int ks, int mode, i
   return v;
 }
 
+template <int TT>
 __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __restrict__ jobs, int njobs) {
-  __shared__ float tile[PT * PTS];
+  constexpr int PTK = TT == 27 ? 16 : 32;   // k tile
+  constexpr int PTS = PT * TT + 1;
+  __shared__ float tile[PTK * PTS];
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -737,20 +745,20 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
   const int ks = (int)(J[2] & 0xffffffff), nout = (int)(J[2] >> 32);
   const int kt = (int)(J[3] >> 32);
   const int b = (int)((long long)blockIdx.x - (J[3] & 0xffffffffLL));
-  const int k0 = (b % kt) * PT, c0 = (b / kt) * PT;
-  const int T = ks * ks;
-  // ---- master tile w[k0:k0+32][c0:c0+32][:] (zero outside K x C)
+  const int k0 = (b % kt) * PTK, c0 = (b / kt) * PT;
+  const int T = TT == 27 ? 27 : ks * ks;
+  // ---- master tile w[k0:k0+PTK][c0:c0+32][:] (zero outside K x C)
   if (((C * T) & 3) == 0 && c0 + PT <= C && ((size_t)w & 15) == 0) {
     // full-width tile: 16-byte loads along the contiguous (c, tap) run of each k
     const int nv = PT * T / 4;
-    for (int e = threadIdx.x; e < PT * nv; e += blockDim.x) {
+    for (int e = threadIdx.x; e < PTK * nv; e += blockDim.x) {
       const int kl = e / nv, v = e - kl * nv, k = k0 + kl;
       const float4 x = k < K ? *(const float4*)(w + ((size_t)k * C + c0) * T + v * 4) : float4{0.f, 0.f, 0.f, 0.f};
       float* t = tile + kl * PTS + v * 4;
       t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w;
     }
   } else {
-    for (int e = threadIdx.x; e < PT * PT * T; e += blockDim.x) {
+    for (int e = threadIdx.x; e < PTK * PT * T; e += blockDim.x) {
       const int kl = e / (PT * T), r = e - kl * (PT * T);   // r = cl * T + tap: contiguous in memory
       const int k = k0 + kl, c = c0 + r / T;
       tile[kl * PTS + r] = (k < K && c < C) ? w[((size_t)k * C + c0) * T + r] : 0.f;
@@ -763,13 +771,14 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
     const int mode = (int)(desc & 0xff), kind = (int)((desc >> 8) & 0xff);
     const int R = (int)((desc >> 16) & 0xffffff), Cc = (int)((desc >> 40) & 0xffffff);
     const int To = mode == 2 ? 16 : T;
-    // tile coordinates in the layout's (row, col) space
+    // tile coordinates in the layout's (row, col) space: NRB rows x NCB cols of this block
     const int r0 = mode == 0 ? k0 : c0, q0 = mode == 0 ? c0 : k0;
+    const int NRB = mode == 0 ? PTK : PT, NCB = mode == 0 ? PT : PTK;
     if (kind == 0) {
-      // [R][To][Cc]: for each (row, tap) a run of 32 cols, written as 16-byte groups of 8
+      // [R][To][Cc]: for each (row, tap) a run of NCB cols, written as 16-byte groups of 8
       const bool vec = (Cc & 7) == 0 && ((size_t)out & 15) == 0;
-      for (int e = threadIdx.x; e < PT * To * (PT / 8); e += blockDim.x) {
-        const int q8 = e % (PT / 8), r = e / (PT / 8), tap = r % To, rl = r / To;
+      for (int e = threadIdx.x; e < NRB * To * (NCB / 8); e += blockDim.x) {
+        const int q8 = e % (NCB / 8), r = e / (NCB / 8), tap = r % To, rl = r / To;
         const int row = r0 + rl, col8 = q0 + q8 * 8;
         if (row >= R || col8 >= Cc) continue;
         bf16r* dst = out + ((size_t)row * To + tap) * Cc + col8;
@@ -782,7 +791,7 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
             for (int u = 0; u < 2; ++u) {
               const int ql = q8 * 8 + 2 * h + u;
               const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
-              v2[u] = ptile_value(tile, kl, cl, ks, mode, tap);
+              v2[u] = ptile_value<TT>(tile, kl, cl, ks, mode, tap);
             }
             pk[h] = pack2(v2[0], v2[1]);
           }
@@ -791,16 +800,17 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
           for (int u = 0; u < 8 && col8 + u < Cc; ++u) {
             const int ql = q8 * 8 + u;
             const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
-            dst[u] = (bf16r)f2bf(ptile_value(tile, kl, cl, ks, mode, tap));
+            dst[u] = (bf16r)f2bf(ptile_value<TT>(tile, kl, cl, ks, mode, tap));
           }
         }
       }
     } else {
-      // [R/128][Cc/BK][To][BK/8][128][8]: 16-byte chunks of 8 cols, runs of 32 rows
+      // kind 1: [R/128][Cc/BK][To][BK/8][128][8]; kind 2: [R/128][3 * Cc/BK][9][BK/8][128][8] (chunk kz * nchunk + c / BK,
+      // tap9 = tap % 9): 16-byte chunks of 8 cols, runs of NRB rows
       constexpr int HBK = FMD_HALO_BK;
       const int nchunk = (Cc + HBK - 1) / HBK;
-      for (int e = threadIdx.x; e < To * (PT / 8) * PT; e += blockDim.x) {
-        const int rl = e % PT, r = e / PT, kq = r % (PT / 8), tap = r / (PT / 8);
+      for (int e = threadIdx.x; e < To * (NCB / 8) * NRB; e += blockDim.x) {
+        const int rl = e % NRB, r = e / NRB, kq = r % (NCB / 8), tap = r / (NCB / 8);
         const int row = r0 + rl, col8 = q0 + kq * 8;
         if (row >= ((R + 127) / 128) * 128 || col8 >= nchunk * HBK) continue;
         const int tr = row >> 7, co = row & 127, chunk = col8 / HBK, kc = (col8 % HBK) >> 3;
@@ -812,11 +822,17 @@ __global__ __launch_bounds__(256) void prep_batch_kernel(const long long* __rest
           for (int u = 0; u < 2; ++u) {
             const int ql = kq * 8 + 2 * h + u, col = q0 + ql;
             const int kl = mode == 0 ? rl : ql, cl = mode == 0 ? ql : rl;
-            v2[u] = (row < R && col < Cc) ? ptile_value(tile, kl, cl, ks, mode, tap) : 0.f;
+            v2[u] = (row < R && col < Cc) ? ptile_value<TT>(tile, kl, cl, ks, mode, tap) : 0.f;
           }
           pk[h] = pack2(v2[0], v2[1]);
         }
-        const size_t idx = ((((size_t)tr * nchunk + chunk) * To + tap) * (HBK / 8) + kc) * 128 + co;
+        size_t idx;
+        if (kind == 1) {
+          idx = ((((size_t)tr * nchunk + chunk) * To + tap) * (HBK / 8) + kc) * 128 + co;
+        } else {
+          const int kz = tap / 9, t9 = tap - kz * 9;
+          idx = ((((size_t)tr * 3 * nchunk + kz * nchunk + chunk) * 9 + t9) * (HBK / 8) + kc) * 128 + co;
+        }
         *(u32x4*)(out + idx * 8) = u32x4{pk[0], pk[1], pk[2], pk[3]};
       }
     }
@@ -850,7 +866,15 @@ int fmd_prep_weights_t(const float* w, int32_t K, int32_t C, int32_t T, int32_t 
 
 int fmd_prep_weights_batch(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s) {
   if (njobs < 1 || nblocks < 1) return njobs == 0 ? 0 : -1;
-  hipLaunchKernelGGL(prep_batch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)s, (const long long*)jobs, njobs);
+  hipLaunchKernelGGL(prep_batch_kernel<9>, dim3(nblocks), dim3(256), 0, (hipStream_t)s, (const long long*)jobs,
+                     njobs);
+  return (int)hipGetLastError();
+}
+
+int fmd_prep_weights_batch_cubic(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s) {
+  if (njobs < 1 || nblocks < 1) return njobs == 0 ? 0 : -1;
+  hipLaunchKernelGGL(prep_batch_kernel<27>, dim3(nblocks), dim3(256), 0, (hipStream_t)s, (const long long*)jobs,
+                     njobs);
   return (int)hipGetLastError();
 }
 

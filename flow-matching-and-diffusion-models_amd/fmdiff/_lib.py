@@ -99,6 +99,7 @@ SIGNATURES = {
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_t": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_batch": [p, i32, i32, p],
+    "fmd_prep_weights_batch_cubic": [p, i32, i32, p],
     "fmd_nchw_to_nhwc": [p, i32, i32, i32, i32, p, p],
     "fmd_nhwc_to_nchw": [p, i32, i32, i32, i32, i32, p, p],
     "fmd_sum_pool2": [p, i32, i32, i32, i32, p, i32, p],

@@ -108,9 +108,7 @@ class WeightCache:
     def __init__(self):
         self._c = {}
         self._force = set()
-        self._jobs_key = None
-        self._jobs = None
-        self._nblk = 0
+        self._tables = {}   # cubic (3x3x3 masters) or not -> (key, device job table, njobs, nblocks)
         # job tables replaced by a rebuild: a captured graph (train step, sampler) holds the raw pointer of
         # the table it recorded and replays fmd_prep_weights_batch on it, so a table lives as long as the cache
         self._retired: List[torch.Tensor] = []
@@ -123,8 +121,6 @@ class WeightCache:
         for key, e in self._c.items():          # fp32 derived buffers first: they feed the bf16 layouts
             if e["kind"] == "pad":
                 e["buf"][: e["src"].numel()].copy_(e["src"].detach().reshape(-1))
-            elif e["kind"] == "dpack":
-                self._dpack(e["src"], e["mode"], e["buf"])
             elif e["kind"] == "e1d":
                 self._embed1d(e["src"], e["buf"])
             elif e["kind"] == "ctr":
@@ -134,20 +130,22 @@ class WeightCache:
                 for w in e["src"]:
                     e["buf"][o:o + w.shape[0]].copy_(w.detach())
                     o += w.shape[0]
-        jobs = [(key, e) for key, e in self._c.items() if e["kind"] in ("prep", "tiled")]
-        if jobs:
-            self._launch_batch(jobs)
-        for key, e in self._c.items():          # cubic (3-D) kernels: the batched prep takes <= 9 taps
-            if e["kind"] == "prep3":
-                ops.prep_weights(e["src"].detach(), *e["job"], out=e["buf"])
+        for cubic in (False, True):   # square (<= 9 taps) and cubic (27 taps) masters: one launch each
+            jobs = [(key, e) for key, e in self._c.items()
+                    if e["kind"] in ("prep", "tiled") and (e["job"][7] == 27) == cubic]
+            if jobs:
+                self._launch_batch(jobs, cubic)
         for key, e in self._c.items():
             e["ver"] = self._ver(e["src"]) if e["kind"] != "fused" else tuple(self._ver(w) for w in e["src"])
         self._force.clear()
 
-    def _launch_batch(self, jobs):
-        """One fmd_prep_weights_batch job per fp32 master: every layout of it from one read of each tile."""
+    def _launch_batch(self, jobs, cubic=False):
+        """One fmd_prep_weights_batch job per fp32 master: every layout of it from one read of each tile
+        (``cubic``: 3x3x3 masters, fmd_prep_weights_batch_cubic, 16-row k tiles)."""
         key = tuple((e["src"].data_ptr(), e["buf"].data_ptr(), e["job"]) for _, e in jobs)
-        if key != self._jobs_key:
+        ptk = 16 if cubic else 32
+        tab = self._tables.get(cubic)
+        if tab is None or key != tab[0]:
             per_src = {}
             for src_ptr, buf_ptr, job in key:
                 per_src.setdefault(src_ptr, []).append((buf_ptr, job))
@@ -164,19 +162,18 @@ class WeightCache:
                         k_ext, c_ext2 = (r_ext, c_ext) if mode == 0 else (c_ext, r_ext)
                         kp, cp = max(kp, k_ext), max(cp, c_ext2)
                         descs += [buf_ptr, mode | (kind << 8) | (R << 16) | (Cc << 40)]
-                    kt, ct = -(-kp // 32), -(-cp // 32)
+                    kt, ct = -(-kp // ptk), -(-cp // 32)
                     row = [src_ptr, K | (C << 32), ks | (len(part) << 32), blk | (kt << 32)] + descs
                     rows.append(row + [0] * (16 - len(row)))
                     blk += kt * ct
             dev = jobs[0][1]["buf"].device
-            if self._jobs is not None:
-                self._retired.append(self._jobs)
-            self._jobs = torch.tensor(rows, dtype=torch.int64).to(dev)
-            self._njobs = len(rows)
-            self._nblk = blk
-            self._jobs_key = key
+            if tab is not None:
+                self._retired.append(tab[1])
+            tab = (key, torch.tensor(rows, dtype=torch.int64).to(dev), len(rows), blk)
+            self._tables[cubic] = tab
         from .. import _lib as L
-        L.call("fmd_prep_weights_batch", self._jobs.data_ptr(), self._njobs, self._nblk, ops.stream())
+        L.call("fmd_prep_weights_batch_cubic" if cubic else "fmd_prep_weights_batch", tab[1].data_ptr(), tab[2], tab[3],
+               ops.stream())
 
     def _fresh(self, key, src_ver):
         e = self._c.get(key)
@@ -219,12 +216,8 @@ class WeightCache:
         if not self._fresh(key, self._ver(w)):
             e = self._c.get(key)
             buf = ops.prep_weights(w.detach(), mode, Kpad, Cpad, out=None if e is None else e["buf"])
-            if w.dim() == 5:
-                self._c[key] = dict(kind="prep3", src=w, buf=buf, ver=self._ver(w), job=(mode, Kpad, Cpad))
-                self._force.discard(key)
-                return buf
             K, C = w.shape[0], w.shape[1]
-            ks = w.shape[2] if w.dim() == 4 else 1
+            ks = w.shape[2] if w.dim() >= 4 else 1
             R, T, Cc = buf.shape
             self._c[key] = dict(kind="prep", src=w, buf=buf, ver=self._ver(w),
                                 job=(K, C, ks, mode, R, Cc, 0, T, buf.numel()))
@@ -260,17 +253,21 @@ class WeightCache:
         v[:, :, :Cs].copy_(src.permute(0, 2, 1, 3, 4))
 
     def dtiled(self, w: torch.Tensor, mode: int):
-        """Halo-tiled depth-tap layout of a 3x3x3 weight (mode 0 forward, 3 data gradient)."""
-        key = (id(w), "dpack", mode)
+        """Halo-tiled depth-tap layout of a 3x3x3 weight (mode 0 forward, 3 data gradient): the 2-D tiles of the
+        ``_dpack`` view, re-derived by the cubic batched prep (kind 2) after each optimizer step; the first
+        fill goes through the fp32 view + fmd_tile_weights_halo (the same single bf16 rounding)."""
+        key = (id(w), "dtiled", mode)
         if not self._fresh(key, self._ver(w)):
             e = self._c.get(key)
-            R, Cs = (w.shape[0], w.shape[1]) if mode == 0 else (w.shape[1], w.shape[0])
-            buf = e["buf"] if e is not None else torch.empty((R, 3 * (-(-Cs // HALO_BK) * HALO_BK), 3, 3),
-                                                             device=w.device, dtype=F32)
-            self._dpack(w, mode, buf)
-            self._c[key] = dict(kind="dpack", src=w, mode=mode, buf=buf, ver=self._ver(w))
+            K, C = w.shape[0], w.shape[1]
+            R, Cs = (K, C) if mode == 0 else (C, K)
+            view = torch.empty((R, 3 * (-(-Cs // HALO_BK) * HALO_BK), 3, 3), device=w.device, dtype=F32)
+            self._dpack(w, mode, view)
+            buf = ops.tile_weights(ops.prep_weights(view, 0), out=None if e is None else e["buf"])
+            self._c[key] = dict(kind="tiled", src=w, buf=buf, ver=self._ver(w),
+                                job=(K, C, 3, mode, R, Cs, 2, 27, buf.numel()))
             self._force.discard(key)
-        return self.tiled(self._c[key]["buf"], 0)
+        return self._c[key]["buf"]
 
     def padded(self, v: torch.Tensor, n: int):
         key = (id(v), "pad", n)

@@ -226,6 +226,11 @@ int fmd_prep_weights_t(const float* w, int32_t K, int32_t C, int32_t T, int32_t 
  * (R rows x T x Cc), kind 1 = its halo tiles.  A block covers a 32x32 (k, c) tile of one master; jobs
  * sorted by first block; nblocks = total. */
 int fmd_prep_weights_batch(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s);
+/* The same for cubic 3x3x3 masters w[K][C][27] (job ks = 3): blocks cover 16 (k) x 32 (c) tiles (ktiles counts
+ * 16-row k tiles); kinds 0 / 1 as above with T = 27, and kind 2 = the depth-tap halo kernel's tiles of the
+ * [R][3*Cr][3][3] view (channel block kz*Cr + c = depth tap kz of channel c; Cr = Cc rounded up to 32):
+ * [ceil(R/128)][3*Cr/32][9][4][128][8] (modes 0 and 3). */
+int fmd_prep_weights_batch_cubic(const void* jobs, int32_t njobs, int32_t nblocks, fmd_stream_t s);
 int fmd_nchw_to_nhwc(const float* x, int32_t N, int32_t C, int32_t HW, int32_t Cpad, void* y, fmd_stream_t s);
 int fmd_nhwc_to_nchw(const void* y, int32_t src_f32, int32_t N, int32_t C, int32_t HW, int32_t Cs, float* x,
                      fmd_stream_t s);

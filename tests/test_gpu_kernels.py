@@ -605,6 +605,30 @@ def test_weight_cache_batched_refresh_matches_individual_preps():
         assert torch.equal(got, ref), (kind, wi, mode, kp)
 
 
+def test_weight_cache_cubic_batched_refresh_matches_individual_preps():
+    """fmd_prep_weights_batch_cubic (3x3x3 masters: base layouts with 27 taps, and the depth-tap halo tiles
+    of WeightCache.dtiled, kind 2) == the per-weight fmd_prep_weights_t / fp32 depth-packed view +
+    fmd_tile_weights_halo first fills, bit for bit; channel counts off the 16 / 32 tiles included."""
+    from fmdiff.runtime.engine import WeightCache
+    torch.manual_seed(4)
+    wc = WeightCache()
+    ws = [torch.randn(128, 128, 3, 3, 3, device=DEV), torch.randn(136, 72, 3, 3, 3, device=DEV),
+          torch.randn(64, 8, 3, 3, 3, device=DEV), torch.randn(8, 128, 3, 3, 3, device=DEV)]
+    want = {}
+    for wi in range(len(ws)):
+        for mode in (0, 1, 3):
+            want[("b", wi, mode)] = wc.get(ws[wi], mode).clone()
+        for mode in (0, 3):
+            want[("d", wi, mode)] = wc.dtiled(ws[wi], mode).clone()
+    for e in wc._c.values():
+        e["buf"].zero_()
+    wc.invalidate()
+    torch.cuda.synchronize()
+    for (kind, wi, mode), ref in want.items():
+        got = wc.get(ws[wi], mode) if kind == "b" else wc.dtiled(ws[wi], mode)
+        assert torch.equal(got, ref), (kind, wi, mode)
+
+
 @pytest.mark.parametrize("K", [1, 3])
 def test_head_kernels_vs_torch(K):
     """csrc/head.hip: GN-affine+SiLU -> 3x3 conv to K <= 8 channels (fp32 out, Kp = 8), its data gradient
