@@ -81,7 +81,10 @@ FMD_DEV int xcd_remap(int b, int nwg) {
 // LDS byte address; lane i lands at lds_dst + 16 i.
 // Scalar-base form: lane address = sbase + voff (a fixed 32-bit per-lane byte offset, "saddr" addressing), so
 // a stream whose lanes always fetch the same offsets of consecutive blocks needs no per-DMA vector arithmetic.
-FMD_DEV void glds16s(const void* sbase, unsigned voff, unsigned lds_dst) {
+FMD_DEV void glds16s(const void* sbase_, unsigned voff, unsigned lds_dst) {
+  const unsigned long long sb = (unsigned long long)sbase_;   // wave-uniform: pinned to SGPRs for the "s" operand
+  const void* sbase = (const void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(sb >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)sb));
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");

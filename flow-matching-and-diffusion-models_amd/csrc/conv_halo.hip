@@ -59,6 +59,7 @@ struct HArgs {
                           // kz, 32-channel block cb) = kz*ncb + cb, reading logical input slice z + kz - 1
                           // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
+  unsigned long long* tbuf;    // per-wave phase timestamps (compiled in only with -DFMD_HALO_TIME)
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
 };
@@ -70,6 +71,23 @@ struct HArgs {
 #endif
 
 static int g_dbg = 0;
+static unsigned long long* g_tbuf = nullptr;
+
+// Phase timeline instrumentation (-DFMD_HALO_TIME; tools/halo_timeline.py): lane 0 of waves 0 and 4 of every
+// workgroup stores s_memtime at fixed points: [0] HW_ID, [1] XCC_ID, [2] start, [24] tables loaded, [25] first
+// halo loads issued, [26] first halo stored, [3] prologue barrier, [4..23] after each main-loop step barrier,
+// [30] loop done, [27] epilogue tile packed, [28] epilogue barrier, [31] end.  Vector stores only; the buffer
+// must be armed (fmd_debug_halo_timebuf) before any launch of an instrumented build.
+#ifdef FMD_HALO_TIME
+#define HTIME(slot)                                                                                    \
+  do {                                                                                                 \
+    if ((threadIdx.x & 255) == 0)                                                                      \
+      A.tbuf[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 2 + (threadIdx.x >> 8)) * 32 + (slot)] = \
+          __builtin_amdgcn_s_memtime();                                                                \
+  } while (0)
+#else
+#define HTIME(slot) do {} while (0)
+#endif
 
 // staged piece h (16 bytes) of a chunk: blocks of 32 = 8 consecutive positions x KC channel groups
 FMD_DEV int piece_pos(int h) { return (h >> 5) * 8 + (h & 7); }
@@ -126,7 +144,15 @@ void conv3x3_halo(const HArgs A) {
 
   const fmd_conv_desc& d = A.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid / NWH, wpx = wid % NWH;   // 2 x NWH waves: 64 couts x WR pixel rows each
+  const int wco = wid / NWH, wpx = wid % NWH;
+#ifdef FMD_HALO_TIME
+  HTIME(2);
+  if ((tid & 255) == 0) {
+    unsigned long long* tb = A.tbuf + ((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 2 + (wid >> 2)) * 32;
+    tb[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    tb[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+  }
+#endif   // 2 x NWH waves: 64 couts x WR pixel rows each
   const int l16 = lane & 15, lq = lane >> 4;
   const int kc = piece_kc(tid);              // staged pieces start at multiples of 32: the channel group is fixed
 
@@ -327,19 +353,23 @@ void conv3x3_halo(const HArgs A) {
   auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
 
   // ---- prologue: the full halo of the first chunk (always a 3x3 chunk) + the weights of its first step
+  HTIME(24);
   __syncthreads();   // affine + epilogue tables (no DMA in flight yet)
   setup(c_lo);
   load_w(c_lo * 9, 0);
   if (c_lo * 9 + 1 < slot_end) load_w(c_lo * 9 + 1, 1);
 #pragma unroll
   for (int k = 0; k < LPRO; ++k) load_main(k, tid + NT * k, tid + NT * k < TOT1);
+  HTIME(25);
 #pragma unroll
   for (int k = 0; k < LPRO; ++k) store(c_lo & 1, k, true, cch);
+  HTIME(26);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < WR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   step_barrier<0>();
+  HTIME(3);
 
   // ---- 3x3 chunks: 5 steps of taps (0,1) (2,3) (4,5) (6,7) (8).  The next chunk's halo is staged in
   //      4 pieces: piece i is loaded into registers in step i (after that step's weight DMA, so the
@@ -413,6 +443,7 @@ void conv3x3_halo(const HArgs A) {
       pc = cch;
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
       step_barrier<LPT>();
+      HTIME(4 + (chunk - c_lo) * 5 + ps);
       wb ^= 1;
     }
   }
@@ -438,6 +469,7 @@ void conv3x3_halo(const HArgs A) {
     wb ^= 1;
   }
 
+  HTIME(30);
   if (HDBG(4)) return;
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
@@ -553,7 +585,9 @@ void conv3x3_halo(const HArgs A) {
         }
       }
     }
+    HTIME(27);
     __syncthreads();
+    HTIME(28);
 #pragma unroll
     for (int k = 0; k < TH * TW * BCO / 8 / NT; ++k) {
       const int q = tid + NT * k, pi = q >> 4, c16 = q & 15;
@@ -645,6 +679,7 @@ void conv3x3_halo(const HArgs A) {
       }
     }
   }
+  HTIME(31);
 }
 
 // [K][T][C] kernel-layout bf16 weights -> halo tiles [ntc][nchunk][T][KC][BCO][8] (zero padded)
@@ -710,6 +745,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
   A.dbg = g_dbg;
+  A.tbuf = g_tbuf;
   const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < g_halo_min_wg) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
@@ -731,6 +767,12 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
 // Debug hook (not part of the public ABI): ablation flags of the next launches (see HArgs::dbg).
 extern "C" int fmd_debug_halo_flags(int flags) {
   g_dbg = flags;
+  return 0;
+}
+
+// Debug hook (not part of the public ABI): phase-timestamp buffer of an instrumented build (see HTIME).
+extern "C" int fmd_debug_halo_timebuf(void* buf) {
+  g_tbuf = (unsigned long long*)buf;
   return 0;
 }
 
