@@ -50,22 +50,46 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def conv_roofline(dev, iters=20):
-    """Time the dominant kernel live with HIP events: the fused GN+SiLU -> 3x3 conv implicit GEMM
-    at the 256^2 level (128 -> 128 channels, batch 8), the problem that carries 8+3 of the 96
-    convs and ~55% of the UNet's FLOPs."""
+def conv_roofline(dev, iters=20, prob="fwd"):
+    """Time the dominant kernels live with HIP events at the 256^2 level (128 -> 128 channels, batch 8),
+    the problem that carries 8+3 of the 96 convs and ~55% of the UNet's FLOPs:
+    ``fwd``   fused GN+SiLU -> 3x3 conv (conv3x3_halo<false,2>, statistics epilogue) -- the roofline line;
+    ``dgrad`` its data gradient (conv3x3_halo<false,0>, flipped taps, SiLU' + GN-backward-sums epilogue);
+    ``wgrad`` its weight gradient (wgrad_halo_kernel<2>, GN+SiLU recomputed; + the split-K reduce)."""
     from fmdiff.runtime import ops
     N, H, W, C, K = 8, 256, 256, 128, 128
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
-    w = ops.prep_weights(torch.randn(K, C, 3, 3, device=dev, generator=g) * 0.03, 0)
+    wf = torch.randn(K, C, 3, 3, device=dev, generator=g) * 0.03
     a = torch.rand(N, C, device=dev) + 0.5
     b = torch.randn(N, C, device=dev) * 0.1
     bias = torch.zeros(K, device=dev)
-    wt = ops.tile_weights(w)
     out = torch.empty(N, H, W, K, device=dev, dtype=torch.bfloat16)
+    if prob == "fwd":
+        w = ops.prep_weights(wf, 0)
+        wt = ops.tile_weights(w)
+
+        def fn():
+            ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
+        kernel = "conv3x3_halo<false> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)"
+    elif prob == "dgrad":
+        w = ops.prep_weights(wf, 3)
+        wt = ops.tile_weights(w)
+        dy = torch.randn(N, H, W, K, device=dev, generator=g).to(torch.bfloat16)
+
+        def fn():
+            ops.conv(dy, C, w, out=out, want_stats=True, ep=(x, None, a, b), wgt_tiled=wt)
+        kernel = "conv3x3_halo<false,0> data gradient (flipped taps, SiLU' + GN-backward-sums epilogue, 8x256x256x128->128)"
+    else:
+        dy = torch.randn(N, H, W, K, device=dev, generator=g).to(torch.bfloat16)
+        dw = torch.zeros(K, C, 3, 3, device=dev)
+        db = torch.zeros(K, device=dev)
+
+        def fn():
+            ops.wgrad(x, dy, dw, pro=(a, b, True), db=db)
+        kernel = "wgrad_halo_kernel<2> + wgrad_reduce (GN+SiLU recomputed, 8x256x256x128->128x3x3, fp32 dW)"
     for _ in range(3):
-        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
+        fn()
     # In the train step the 134 MB input arrives cold (written by an earlier kernel, evicted by the ones
     # in between); a back-to-back loop would serve it from the 256 MB Infinity Cache.  So every timed
     # launch follows a 512 MB write that evicts it, and only the conv itself is inside the events.
@@ -75,14 +99,13 @@ def conv_roofline(dev, iters=20):
     for e0, e1 in evs:
         flush.fill_(1)
         e0.record()
-        ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
+        fn()
         e1.record()
     torch.cuda.synchronize()
     ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / iters
     del flush
     flops = 2.0 * N * H * W * K * C * 9
-    return dict(kernel="conv3x3_halo<false> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)",
-                ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
+    return dict(kernel=kernel, ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
 
 
 def pmc_traffic():
@@ -286,6 +309,13 @@ def main():
         return
     roof = conv_roofline(dev)
     log(f"[bench] dominant conv: {roof['ms']:.3f} ms, {roof['tflops']:.1f} TFLOP/s")
+    # the same problem's backward kernels (the step's next two largest buckets), same protocol
+    back = {}
+    for prob in ("dgrad", "wgrad"):
+        r = conv_roofline(dev, prob=prob)
+        back[prob] = {"achieved": r["tflops"], "frac": r["tflops"] / PEAK_BF16_TFLOPS, "kernel": r["kernel"],
+                      "kernel_ms": r["ms"], "flops_per_launch": r["flops_per_launch"]}
+        log(f"[bench] {prob}: {r['ms']:.3f} ms, {r['tflops']:.1f} TFLOP/s")
     step_tflops = train_ips / world * TRAIN_GFLOP_PER_IMAGE / 1e3
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -316,6 +346,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(), "kernel": roof["kernel"],
                      "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]},
+        "roofline_backward": {"peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", **back},
         "cpu_baseline": cpu,
     }
     print(json.dumps(res), flush=True)
