@@ -708,6 +708,7 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->C1 && !d->src1) return -2;
   if (d->src2 && !d->wgt2 && !d->wgt2_tiled) return -3;
   if (d->pro_a && !d->pro_b) return -4;
+  if (d->gout && !d->pro_a) return -9;
   const int M = d->N * (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
   const int HWo = (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
   // split-K: the combine kernel produces the channel statistics (16-pixel rows) instead of the main kernel
@@ -721,6 +722,7 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
     rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
+    if (d->gout) return -9;                            // the prologue side output exists only on the halo path
     if (d->K <= 16)
       rc = launch<16, 256, 1, 4, 64>(&dm, s);
     else if (d->K <= 64)

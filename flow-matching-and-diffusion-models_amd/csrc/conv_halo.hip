@@ -108,7 +108,8 @@ static_assert(SM_BYTES <= 163840 / 2, "two workgroups per CU");
 // would drain the halo prefetch that is meant to stay in flight across the barrier.
 template <int KEEP>
 FMD_DEV void step_barrier() {
-  if constexpr (KEEP == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+  if constexpr (KEEP == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+  else if constexpr (KEEP == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
   else if constexpr (KEEP == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -121,7 +122,8 @@ constexpr int WR = 4;    // output rows per wave
 constexpr int NWH = 4;   // waves per cout half
 
 // PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU (fused prologue, applied once per halo element)
-template <bool UP, int PRO>
+// GOUT: also write the prologue's output G to d.gout (the tile's own pixels of every main chunk it stages)
+template <bool UP, int PRO, bool GOUT = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void conv3x3_halo(const HArgs A) {
   constexpr int WDMA = WBUF / (NT * 8);                    // 16-byte weight DMAs per thread per tap
@@ -376,6 +378,45 @@ void conv3x3_halo(const HArgs A) {
   //      DMA's counted wait leaves it in flight across the barrier) and transformed + stored in step
   //      i+1.  Waves of the two cout halves share a SIMD pairwise: wco 0 stores before its first tap,
   //      wco 1 after it, so one wave's GroupNorm/SiLU VALU work overlaps the other's MFMAs.
+  // G side output (GOUT): the tile's own pixels of a main chunk's staged (transformed) halo image, copied
+  // LDS -> d.gout ((C0+C1) % 32 == 0, checked on the host).  Chunk c's image is copied in step 0 of chunk
+  // c + 1 after that step's loads, so the step barrier's counted wait leaves these stores in flight (they are
+  // the youngest vector-memory ops); the last chunk's image right after the loop.  Returns the stores this
+  // wave issued.
+  auto copy_g = [&](int gc) -> int {
+    if constexpr (!GOUT) {
+      return 0;
+    } else {
+      constexpr int IH = UP ? TH / 2 : TH, IW = UP ? TW / 2 : TW;   // the tile's own stored pixels
+      constexpr int NPG = IH * IW * KC;                            // 16-byte pieces (1024 | 256)
+      static_assert(NPG % NT == 0 || NPG * 2 == NT, "whole waves per copied piece row");
+      int cb = gc, kzc = 1;
+      if (A.depth) { kzc = gc / A.ncb; cb = gc - kzc * A.ncb; }
+      // 3-D: the centre depth tap only; under nearest-x2 the even output slice of each stored slice
+      if (kzc != 1 || (A.depth && UP && (zz & 1))) return 0;
+      // opaque copies: the address math stays here instead of being hoisted out of the chunk loop
+      int t_ = tid, ty_ = ty0, tx_ = tx0, img = A.depth ? smp * A.dsrc + (UP ? zz >> 1 : zz) : n;
+      asm volatile("" : "+v"(t_), "+v"(ty_), "+v"(tx_), "+v"(img));
+      const int oy = UP ? ty_ >> 1 : ty_, ox = UP ? tx_ >> 1 : tx_;
+      const bf16r* hb = hbuf + (gc & 1) * HBUF;
+      int nst = 0;
+#pragma unroll
+      for (int q = 0; q < (NPG + NT - 1) / NT; ++q) {
+        if (NPG >= NT || wid < NPG / 64) {   // wave-uniform
+          const int h = t_ + q * NT;
+          // 4 consecutive lanes = the chunk's 64 contiguous bytes of one pixel
+          const int kq = h & (KC - 1), px = (h / KC) % IW, py = h / (KC * IW);
+          const int c = cb * BK + kq * 8;
+          const u32x4 v = *(const u32x4*)(hb + (kq * HPAD + (py + 1) * HROW + px + 1) * 8);
+          const size_t pix = ((size_t)img * d.Hs + oy + py) * d.Ws + ox + px;
+          *(u32x4*)((bf16r*)d.gout + pix * A.C + c) = v;
+          ++nst;
+        }
+      }
+      return nst;
+    }
+  };
+
   int wb = 0;   // weight double-buffer of the current step (tiles 2*wb, 2*wb+1)
   int pc = 0;   // affine-table channel of the pending piece
   for (int chunk = c_lo; chunk < c_hi; ++chunk) {
@@ -429,26 +470,37 @@ void conv3x3_halo(const HArgs A) {
       };
       // Waves w and w+4 share a SIMD: the wco 0 wave stages (GN/SiLU VALU work) before its first tap,
       // the wco 1 wave after it, so one wave's transform overlaps the other's MFMAs.
+      int gst = 0;   // G stores issued by this wave this step (younger than its loads)
       if (wco == 0) {
         consume();
         store_pending();
         issue_loads();
+        if (GOUT && ps == 0 && chunk > c_lo) gst = copy_g(chunk - 1);
         compute(chunk & 1, 2 * ps, false, 2 * wb);
       } else {
         compute(chunk & 1, 2 * ps, false, 2 * wb);
         consume();
         store_pending();
         issue_loads();
+        if (GOUT && ps == 0 && chunk > c_lo) gst = copy_g(chunk - 1);
       }
       pc = cch;
       if (two) compute(chunk & 1, 2 * ps + 1, false, 2 * wb + 1);
-      step_barrier<LPT>();
+      if (GOUT && gst == 2) step_barrier<LPT + 2>();
+      else if (GOUT && gst == 1) step_barrier<LPT + 1>();
+      else step_barrier<LPT>();
       HTIME(4 + (chunk - c_lo) * 5 + ps);
       wb ^= 1;
     }
   }
 #pragma unroll
   for (int k = 0; k < LPT; ++k) asm volatile("" ::"v"(rh[k]));
+  if (GOUT && c_hi > c_lo) {   // the last main chunk's image, before the 1x1 staging / epilogue reuse its LDS
+    copy_g(c_hi - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
   // ---- 1x1 chunks (ResBlock skip conv over src2|src3): one step each, next chunk staged whole
   for (int chunk = A.nchunk1; chunk < A.nchunk1 + n_seg2; ++chunk) {
     const int nx = chunk + 1;
@@ -723,6 +775,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
   if (d->pro_a && d->C0 + d->C1 > CMAX) return 1;   // the GN affine table holds CMAX channels
+  if (d->gout && (d->C0 + d->C1) % BK) return 1;     // G side output: whole 32-channel chunks
   if ((long long)Nn * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
       (long long)Nn * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
   HArgs A;
@@ -752,6 +805,16 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);
   const dim3 blk(NT);
+  if (d->gout) {   // prologue side output (fmd_conv checked pro_a)
+    if (d->upsample) {
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2, true>), g, blk, 0, st, A);
+      else hipLaunchKernelGGL((conv3x3_halo<true, 1, true>), g, blk, 0, st, A);
+    } else {
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<false, 2, true>), g, blk, 0, st, A);
+      else hipLaunchKernelGGL((conv3x3_halo<false, 1, true>), g, blk, 0, st, A);
+    }
+    return (int)hipGetLastError();
+  }
   if (d->upsample) {
     if (pro == 2) hipLaunchKernelGGL((conv3x3_halo<true, 2>), g, blk, 0, st, A);
     else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo<true, 1>), g, blk, 0, st, A);

@@ -53,6 +53,11 @@ DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
 MAT_MIN_HW = 128 * 128
 # ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); FMD_POINT_1X1=0 for A/B runs
 POINT_1X1 = os.environ.get("FMD_POINT_1X1", "1") == "1"
+# training: halo convs with a GN+SiLU prologue write G = SiLU(GN(x)) for the weight gradient (fmd_conv_desc.gout)
+# instead of the weight-gradient kernel recomputing it.  Default: 3-D convs only ("3d"), whose weight gradient
+# recomputes G once per depth tap (3x); on 2-D the extra 2 B/element of HBM writes cost the forward more than the
+# weight gradient saves.  FMD_GOUT=all | 3d | 0 for A/B runs.
+GOUT = os.environ.get("FMD_GOUT", "3d")
 
 
 class Act:
@@ -597,10 +602,13 @@ class UNetEngine:
         mat2 = _materialise(halo2, None, Cout, HW) or bool(drop)   # dropout acts on the materialised operand
         fuse2 = mat2 and ops.gn_fused_eligible(HW, Cout, Cout, g2.num_groups)
         src1 = x1.t if (x1 is not None and t1 is None) else None
+        keep_g = ctx.tape is not None and (GOUT == "all" or (GOUT == "3d" and len(sp) == 3))
+        gg1 = (torch.empty((N, *sp, Cin), device=x0.t.device, dtype=torch.bfloat16)
+               if keep_g and t1 is None and halo1 and not point and Cin % HALO_BK == 0 else None)
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=add or not fuse2,
-                          wgt_tiled=w1t, **pk)
+                          wgt_tiled=w1t, gout=gg1, **pk)
         t2 = None
         if fuse2:
             a2, b2, mr2, t2 = ops.gn_fused_apply(h, None, g2.num_groups, g2.eps, g2.weight, g2.bias,
@@ -632,8 +640,10 @@ class UNetEngine:
             t2 = ops.gn_apply_fwd(h, None, a2, b2)
         if drop:
             ops.dropout_apply(t2, drop, seed, salt, out=t2)
+        gg2 = (torch.empty_like(h) if keep_g and t2 is None and halo2 and not point2 and Cout % HALO_BK == 0
+               else None)
         out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
-                            bias=c2.bias, want_stats="free", wgt_tiled=w2t, **kw)
+                            bias=c2.bias, want_stats="free", wgt_tiled=w2t, gout=gg2, **kw)
         o = Act(out, ost)
         if ctx.tape is None:
             return o
@@ -642,8 +652,8 @@ class UNetEngine:
             dy = o.grad
 
             def wg2():
-                if t2 is not None:
-                    ops.wgrad(t2, dy, c2.weight.grad, db=c2.bias.grad)
+                if t2 is not None or gg2 is not None:   # materialised operand / the forward's G side output
+                    ops.wgrad(t2 if t2 is not None else gg2, dy, c2.weight.grad, db=c2.bias.grad)
                 else:
                     ops.wgrad(h, dy, c2.weight.grad, pro=(a2, b2, True), db=c2.bias.grad)
                 if not isinstance(sk, Identity):
@@ -678,8 +688,9 @@ class UNetEngine:
             dh = torch.empty_like(h)
             ops.gn_bwd_apply(dz2, h, None, P2, Q2, R2, None, dh, 0)
             del dz2
-            if t1 is not None:
-                self._wg(lambda: ops.wgrad(t1, dh, c1.weight.grad, db=c1.bias.grad), N * HW)
+            if t1 is not None or gg1 is not None:
+                self._wg(lambda: ops.wgrad(t1 if t1 is not None else gg1, dh, c1.weight.grad, db=c1.bias.grad),
+                         N * HW)
             else:
                 self._wg(lambda: ops.wgrad(x0.t, dh, c1.weight.grad, src1=x1.t if x1 else None, pro=(a1, b1, True),
                                            db=c1.bias.grad), N * HW)

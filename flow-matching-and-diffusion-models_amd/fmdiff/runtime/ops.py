@@ -254,11 +254,14 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
          pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
          out_f32=False,
          accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
-         wgt2_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+         wgt2_tiled=None, gout=None) -> Tuple[torch.Tensor, Optional[Stats]]:
     """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``.
     ``want_stats``: True = per-channel statistics of the output (a separate fmd_channel_stats pass when the
     kernel cannot emit them); "free" = only when the kernel emits them (else None: Act statistics are then
-    derived on demand, and a small-level consumer that computes its own GroupNorm never pays for them)."""
+    derived on demand, and a small-level consumer that computes its own GroupNorm never pays for them).
+    ``gout``: bf16 tensor shaped like the (concatenated) input; the halo path writes the prologue's output
+    G = SiLU(a*x+b) into it (the weight gradient's operand).  Requires ``pro``, (C0+C1) % 32 == 0 and a
+    halo-eligible problem (:func:`halo_eligible`); raises otherwise."""
     _need_cuda(src0, "conv")
     # 3-D (spatial_dims = 3): NDHWC tensors, cubic kernels; ``out_hw_`` is then (Do, Ho, Wo)
     d3 = src0.dim() == 5
@@ -317,6 +320,11 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
                                                    C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
+    if gout is not None:
+        want = (N, Ds, Hs, Ws, C0 + C1) if d3 else (N, Hs, Ws, C0 + C1)
+        if pro is None or not halo or (C0 + C1) % HALO_BK or tuple(gout.shape) != want or gout.dtype != BF16:
+            raise ValueError(f"gout {tuple(gout.shape)} needs a GN prologue, the halo path and shape {want} bf16")
+        d.gout = _p(gout)
     if halo:
         splits = halo_splits(N * max(Do, 1), Ho, Wo, K, C0 + C1, 3 if d3 else 1)
         bpx = 256

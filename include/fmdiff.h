@@ -74,6 +74,11 @@ typedef struct fmd_conv_desc {
   const void* wgt2_tiled;   /* wgt2 re-tiled likewise (T = 1) */
   int32_t Ds, Do;           /* 3-D problems (spatial_dims = 3, NDHWC): stored / output depth; 0 = 2-D.
                                Cubic kernel (ks^3 taps, wgt [K][ks^3][C]); implicit-GEMM path only */
+  void* gout;               /* optional bf16 [N][Hs][Ws][C0+C1] (3-D: [N][Ds][Hs][Ws][C]): the prologue's output
+                               G = SiLU(pro_a*x+pro_b) (or the affine alone), written once per element by the
+                               halo path -- the weight gradient's operand, so the backward does not recompute
+                               the GroupNorm+SiLU.  Requires pro_a, (C0+C1) % 32 == 0 and the halo path (fmd_conv
+                               returns -9 otherwise); NULL = off */
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the

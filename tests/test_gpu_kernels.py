@@ -1090,3 +1090,66 @@ def test_adamw_sched_matches_torch_with_cosine_warmup(n, offset):
         O.adamw_sched(p, buf(g), m, v, ctr, 2e-3, 2, 6, wd=0.01)
         O.counter_add(ctr)
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["plain", "concat", "upsample", "split", "affine", "d3", "d3_up"])
+def test_halo_conv_gout_side_output(case):
+    """fmd_conv_desc.gout: the halo kernel copies its prologue's output G = SiLU(a*x+b) (or the affine alone)
+    for the tile's own pixels out of each staged halo image.  Checks: (1) the conv output is bit-identical
+    with and without the side output; (2) every element of G is written (NaN-filled beforehand) and equals
+    the fp32 torch transform rounded to bf16 within one bf16 ulp (the kernel's SiLU uses v_exp / v_rcp);
+    (3) the weight gradient from G (no prologue) is bit-identical to the one that recomputes GN + SiLU."""
+    O = ops()
+    d3 = case.startswith("d3")
+    up = case in ("upsample", "d3_up")
+    if d3:
+        N, D, H, W, C0, C1, K = 2, 66, 16, 16, 64, 32, 128
+        Ds, Hs, Ws = (D // 2, H // 2, W // 2) if up else (D, H, W)
+        C1 = 0 if up else C1
+        x0 = _rand_ndhwc(N, Ds, Hs, Ws, C0, 91).to(DEV)
+        x1 = _rand_ndhwc(N, Ds, Hs, Ws, C1, 92).to(DEV) if C1 else None
+    else:
+        N, H, W, C0, C1, K = 4, 128, 128, 128, 0, 128
+        if case == "split":
+            N, H, W, C0, K = 4, 32, 32, 512, 256
+        if case == "concat":
+            C1 = 128
+        Hs, Ws = (H // 2, W // 2) if up else (H, W)
+        x0 = _rand_nhwc(N, Hs, Ws, C0, 91).to(DEV)
+        x1 = _rand_nhwc(N, Hs, Ws, C1, 92).to(DEV) if C1 else None
+    Ct = C0 + C1
+    g = torch.Generator().manual_seed(93)
+    a = (torch.rand(N, Ct, generator=g) + 0.5).to(DEV)
+    b = (torch.randn(N, Ct, generator=g) * 0.3).to(DEV)
+    silu = case != "affine"
+    wf = (torch.randn(K, Ct, *((3,) * (3 if d3 else 2)), generator=g) / math.sqrt(Ct * 9)).to(DEV)
+    from fmdiff.runtime.engine import WeightCache
+    wc = WeightCache()
+    wt = wc.dtiled(wf, 0) if d3 else O.tile_weights(O.prep_weights(wf, 0))
+    kw = dict(src1=x1, pro=(a, b, silu), bias=(torch.randn(K, generator=g) * 0.1).to(DEV), upsample=up,
+              want_stats=case != "split", wgt_tiled=wt)
+    if d3:
+        kw["out_hw_"] = (D, H, W)
+    gout = torch.full((*x0.shape[:-1], Ct), float("nan"), device=DEV, dtype=torch.bfloat16)
+    y0, _ = O.conv(x0, K, None, **kw)
+    y1, _ = O.conv(x0, K, None, gout=gout, **kw)
+    assert torch.equal(y0, y1), "the side output changed the conv result"
+    xf = torch.cat([x0, x1], -1).float() if x1 is not None else x0.float()
+    shp = (N,) + (1,) * (xf.dim() - 2) + (Ct,)
+    z = xf * a.view(shp) + b.view(shp)
+    ref = (F.silu(z) if silu else z).to(torch.bfloat16).float()
+    got = gout.float()
+    assert not torch.isnan(got).any(), f"{torch.isnan(got).sum().item()} elements of G never written"
+    err = (got - ref).abs()
+    print(f"{case}: G max err {err.max().item():.3e}, {(err > 0).float().mean().item():.2e} of elements differ")
+    assert (err <= ref.abs() * 2.0 ** -7 + 1e-6).all()
+    if case in ("split", "affine"):
+        return
+    dy = (_rand_ndhwc(N, D, H, W, K, 94) if d3 else _rand_nhwc(N, H, W, K, 94)).to(DEV)
+    dw0 = torch.zeros(K, Ct, *((3,) * (3 if d3 else 2)), device=DEV)
+    dw1 = torch.zeros_like(dw0)
+    O.wgrad(x0, dy, dw0, src1=x1, pro=(a, b, True), upsample=up)
+    O.wgrad(gout, dy, dw1, upsample=up)
+    rel = ((dw1 - dw0).norm() / dw0.norm()).item()
+    print(f"{case}: wgrad from G vs recomputed prologue rel L2 {rel:.3e} (bit-identical: {torch.equal(dw0, dw1)})")
+    assert rel < 1e-3
