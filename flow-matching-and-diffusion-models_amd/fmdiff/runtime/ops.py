@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -207,6 +208,7 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
     return max(1, min(nk // SPLIT_MIN_STEPS, -(-SPLIT_CU_MULT * NUM_CU // tiles), SPLIT_CAP))
 
 
+_CONV_LOG = os.environ.get("FMD_CONV_LOG", "0") == "1"   # debug: one line per conv launch on stderr
 HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
 HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
 SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
@@ -350,6 +352,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         slab = torch.empty((M // rows, K, 2), device=dev, dtype=F32)
         d.stats = _p(slab)
         st = Stats(slab, rows)
+    if _CONV_LOG:
+        print(f"[conv] N={N} in={Ds}x{Hs}x{Ws}x{C0}+{C1} out={Do}x{Ho}x{Wo}x{K} ks={ks} s={stride} tr={int(transposed)} "
+              f"up={int(upsample)} pro={int(pro is not None)} ep={int(ep is not None)} seg2={int(src2 is not None)} "
+              f"stats={int(fused_stats)} halo={int(halo)} splits={splits}", file=sys.stderr)
     _lib.call("fmd_conv", C.byref(d), stream())
     if want_stats == "free":   # only statistics the kernel emits for free; the consumer derives others lazily
         return out, st
