@@ -506,8 +506,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
     }
   }
   if (stats) {
-    // reduce over the 16 pixel lanes of each quad-row; the wave's pixels are one image
-    const int srow = (px0 + wn * (BPX / WN)) / A.stats_rows;
+    // reduce over the 16 pixel lanes of each quad-row; the wave's pixels are one image.  Parity classes:
+    // rows stay image-major (image n owns rows [n HW/64, (n+1) HW/64)), class c the c-th HWq/64 of them --
+    // a class row holds strided pixels, which GroupNorm's per-(image, channel) sums do not mind
+    const int pw = px0 + wn * (BPX / WN);
+    int srow = pw / A.stats_rows;
+    if (A.par) {
+      const int ncls = d3 ? 8 : 4, cls = (int)blockIdx.z, rpi = HWq / A.stats_rows;
+      const int n = pw / HWq;
+      srow = (n * ncls + cls) * rpi + (pw - n * HWq) / A.stats_rows;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -682,8 +690,10 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   const int splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.nk + splits - 1) / splits;
   A.Mfull = A.M;
+  // parity classes; with fused statistics every class must tile its images by whole 64-pixel rows
+  const int HWq = (d->Do > 0 ? d->Do / 2 : 1) * (d->Ho / 2) * (d->Wo / 2);
   A.par = d->transposed && d->stride == 2 && d->ks == 3 && d->pad == 1 && !(d->Ho & 1) && !(d->Wo & 1) &&
-          !(d->Do & 1) && !d->stats && !d->src2 && !GNA && !A.pack;
+          !(d->Do & 1) && (!d->stats || (HWq % 64 == 0 && (d->N * HWq) % BPX == 0)) && !d->src2 && !GNA && !A.pack;
   if (A.par) A.M = d->N * (d->Do > 0 ? d->Do / 2 : 1) * (d->Ho / 2) * (d->Wo / 2);   // pixels per parity class
   A.ntp = (A.M + BPX - 1) / BPX;
   A.ntc = (d->K + BCO - 1) / BCO;
@@ -691,7 +701,8 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   if (d->stats) {
     // every wave's pixel range must be one image and full
     const int wrows = BPX / WN;
-    if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1) return -11;
+    if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1 || (A.par && HWq % 64))
+      return -11;
   }
   dim3 grid(A.ntp * A.ntc, splits, A.par ? (d->Do > 0 ? 8 : 4) : 1);
   hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);

@@ -1153,3 +1153,35 @@ def test_halo_conv_gout_side_output(case):
     rel = ((dw1 - dw0).norm() / dw0.norm()).item()
     print(f"{case}: wgrad from G vs recomputed prologue rel L2 {rel:.3e} (bit-identical: {torch.equal(dw0, dw1)})")
     assert rel < 1e-3
+
+
+@pytest.mark.parametrize("hw", [32, 64])
+def test_conv_s2_dgrad_parity_classes_with_fused_stats(hw):
+    """Stride-2 data gradient with the SiLU' epilogue and fused GroupNorm-backward statistics (the
+    DownsampleND backward whose input feeds a GroupNorm): the parity-class launch (one z-slice per output
+    parity, only the 1/2/2/4 taps that reach it) writes its statistics in image-major rows.  Output vs torch
+    (conv_transpose2d then SiLU'), statistics per (image, channel) vs the split-K path's independent reduce."""
+    O = ops()
+    N, H, W, C, K = 2, hw, hw, 64, 128
+    g = torch.Generator().manual_seed(61)
+    w = _w(K, C, 3, 62)
+    dy = _rand_nhwc(N, H // 2, W // 2, K, 63)
+    xe = _rand_nhwc(N, H, W, C, 64)
+    a = torch.rand(N, C, generator=g) + 0.5
+    b = torch.randn(N, C, generator=g) * 0.2
+    wk = O.prep_weights(w.to(DEV), 1)
+    kw = dict(ks=3, stride=2, pad=1, transposed=True, out_hw_=(H, W), want_stats=True,
+              ep=(xe.to(DEV), None, a.to(DEV), b.to(DEV)))
+    got, st = O.conv(dy.to(DEV), C, wk, splits=1, **kw)
+    ref2, st2 = O.conv(dy.to(DEV), C, wk, splits=3, **kw)
+    dx = F.conv_transpose2d(_to_nchw(dy), _bfw(w), stride=2, padding=1, output_padding=1)
+    z = _to_nchw(xe) * a[:, :, None, None] + b[:, :, None, None]
+    sg = torch.sigmoid(z)
+    ref = (dx * sg * (1 + z * (1 - sg))).permute(0, 2, 3, 1)
+    _close(got, ref)
+    assert st.rows == 64
+    t1 = st.slab.double().view(N, -1, C, 2).sum(1)
+    t2 = st2.slab.double().view(N, -1, C, 2).sum(1)
+    rel = ((t1 - t2).norm() / t2.norm()).item()
+    print(f"hw={hw}: parity-class statistics vs split-K reduce rel L2 {rel:.3e}")
+    assert rel < 1e-2
