@@ -1185,3 +1185,33 @@ def test_conv_s2_dgrad_parity_classes_with_fused_stats(hw):
     rel = ((t1 - t2).norm() / t2.norm()).item()
     print(f"hw={hw}: parity-class statistics vs split-K reduce rel L2 {rel:.3e}")
     assert rel < 1e-2
+
+
+def test_conv3d_s2_dgrad_parity_classes_with_fused_stats():
+    """3-D stride-2 data gradient with the SiLU' epilogue and fused statistics: 8 parity classes, image-major
+    slab rows (class c owns the c-th eighth of each image's rows).  Output vs torch conv_transpose3d then
+    SiLU'; statistics per (image, channel) vs the split-K path's independent reduce."""
+    O = ops()
+    N, D, H, W, C, K = 2, 16, 16, 16, 64, 128
+    g = torch.Generator().manual_seed(71)
+    w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)
+    dy = _rand_ndhwc(N, D // 2, H // 2, W // 2, K, 72)
+    xe = _rand_ndhwc(N, D, H, W, C, 73)
+    a = torch.rand(N, C, generator=g) + 0.5
+    b = torch.randn(N, C, generator=g) * 0.2
+    wk = O.prep_weights(w.to(DEV), 1)
+    kw = dict(ks=3, stride=2, pad=1, transposed=True, out_hw_=(D, H, W), want_stats=True,
+              ep=(xe.to(DEV), None, a.to(DEV), b.to(DEV)))
+    got, st = O.conv(dy.to(DEV), C, wk, splits=1, **kw)
+    _, st2 = O.conv(dy.to(DEV), C, wk, splits=3, **kw)
+    dyc = dy.float().permute(0, 4, 1, 2, 3)
+    dx = F.conv_transpose3d(dyc, _bfw(w), stride=2, padding=1, output_padding=1)
+    z = xe.float().permute(0, 4, 1, 2, 3) * a[:, :, None, None, None] + b[:, :, None, None, None]
+    sg = torch.sigmoid(z)
+    ref = (dx * sg * (1 + z * (1 - sg))).permute(0, 2, 3, 4, 1)
+    _close(got, ref)
+    t1 = st.slab.double().view(N, -1, C, 2).sum(1)
+    t2 = st2.slab.double().view(N, -1, C, 2).sum(1)
+    rel = ((t1 - t2).norm() / t2.norm()).item()
+    print(f"3-D parity-class statistics vs split-K reduce rel L2 {rel:.3e}")
+    assert rel < 1e-2
