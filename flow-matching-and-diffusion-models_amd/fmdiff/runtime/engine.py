@@ -48,6 +48,8 @@ HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdif
 # least MAT_MIN_HW pixels, where the streaming pass costs less than the in-kernel transform it removes
 MAT_PRO = os.environ.get("FMD_MAT_PRO", "0") == "1"   # measured net-negative at batch 8
 MAT_CMAX = 128
+# 3-D: materialise the GN+SiLU operand of depth-tap halo convs (FMD_MAT3D=0: fused prologue + G side output)
+MAT3D = os.environ.get("FMD_MAT3D", "1") == "1"
 # 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
 DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
 MAT_MIN_HW = 128 * 128
@@ -93,11 +95,15 @@ def _gdest(a: Optional[Act]):
     return a.grad, 1
 
 
-def _materialise(halo: bool, x1, Cin: int, HW: int) -> bool:
+def _materialise(halo: bool, x1, Cin: int, HW: int, d3: bool = False) -> bool:
     """Materialise the GN+SiLU prologue (fmd_gn_apply_fwd) instead of fusing it into the conv: always on
     the generic implicit-GEMM path (small levels), whose gather would redo the transform once per tap
-    (9x, VALU-bound at the low occupancy of those levels); on the halo path only if MAT_PRO."""
+    (9x, VALU-bound at the low occupancy of those levels); on the 3-D depth-tap halo path when MAT3D (its
+    chunks stage every input slice for 3 depth taps, so the fused transform runs ~3.8x per element, and the
+    weight gradient reads the same materialised operand); on the 2-D halo path only if MAT_PRO."""
     if not halo:
+        return True
+    if d3 and MAT3D:
         return True
     return MAT_PRO and x1 is None and Cin <= MAT_CMAX and HW >= MAT_MIN_HW
 
@@ -583,7 +589,7 @@ class UNetEngine:
         else:   # the embedding projection feeds nothing (or the block has none: VAE ResBlocks)
             eo, es = None, 0
         halo1 = self._halo_ok(N, sp, Cout, Cin, pro=True)
-        mat1 = _materialise(halo1, x1, Cin, HW)
+        mat1 = _materialise(halo1, x1, Cin, HW, len(sp) == 3)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
             halo1 = self._halo_ok(N, sp, Cout, Cin)
         # a 1x1 level (the bottom of a small latent UNet): the 3x3 convs are their centre taps (exact)
@@ -599,7 +605,7 @@ class UNetEngine:
                                       g1.bias)
             t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
         halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
-        mat2 = _materialise(halo2, None, Cout, HW) or bool(drop)   # dropout acts on the materialised operand
+        mat2 = _materialise(halo2, None, Cout, HW, len(sp) == 3) or bool(drop)   # dropout acts on the materialised operand
         fuse2 = mat2 and ops.gn_fused_eligible(HW, Cout, Cout, g2.num_groups)
         src1 = x1.t if (x1 is not None and t1 is None) else None
         keep_g = ctx.tape is not None and (GOUT == "all" or (GOUT == "3d" and len(sp) == 3))
