@@ -14,6 +14,7 @@
 // DownsampleND (upsampling.py:49-56), torch.cat([h, skip]) (src/models/unet/unet.py:322),
 // the 1x1 skip conv + residual add (residual.py:77-82,120), and their autograd
 // data gradients (transposed gather).
+#include <cstdlib>
 #include "common.h"
 #include "../../include/fmdiff.h"
 
@@ -713,6 +714,15 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
 
 extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  // largest output (pixels) run on 64-pixel tiles when split-K (FMD_BPX64_M; mirrored by ops.BPX64_M)
+  static const int small_m = [] {
+    const char* e = getenv("FMD_BPX64_M");
+    return e && *e ? atoi(e) : 2048;
+  }();
+  static const int tiny_m = [] {
+    const char* e = getenv("FMD_BPX32_M");
+    return e && *e ? atoi(e) : 128;
+  }();
   const int C = d->C0 + d->C1;
   if ((d->C0 % 8) || (d->C1 % 8) || (d->C2 % 8) || (d->C3 % 8) || d->ks < 1 || d->N < 1) return -1;
   if (d->C3 && !d->src3) return -6;
@@ -738,6 +748,10 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
       rc = launch<16, 256, 1, 4, 64>(&dm, s);
     else if (d->K <= 64)
       rc = launch<64, 128, 2, 2, 64>(&dm, s);
+    else if (M <= tiny_m && d->splits > 1)    // tinier: 32-pixel tiles
+      rc = launch<128, 32, 2, 2, 64>(&dm, s);
+    else if (M <= small_m && d->splits > 1)   // tiny levels: 64-pixel tiles, half the split-K slabs
+      rc = launch<128, 64, 2, 2, 64>(&dm, s);
     else
       rc = launch<128, 128, 2, 2, 64>(&dm, s);
   }

@@ -199,6 +199,11 @@ def out_hw(Hs, ks, stride, pad, upsample):
 SPLIT_MIN_STEPS = int(os.environ.get("FMD_SPLIT_MIN_STEPS", "2"))
 SPLIT_CU_MULT = int(os.environ.get("FMD_SPLIT_CU_MULT", "2"))
 SPLIT_CAP = int(os.environ.get("FMD_SPLIT_CAP", "64"))
+# outputs of at most BPX64_M pixels (K > 64, split-K) run on 64-pixel tiles (csrc/conv.hip small_m, FMD_BPX64_M)
+# (train step 24.94 / 25.03 -> 24.83 / 24.87 ms, config D batch 8 77 -> 82.6 images/s); at most BPX32_M: 32-pixel
+# tiles (the latent UNet's 4x4 .. 1x1 levels: 82.3 -> 83.1 images/s)
+BPX64_M = int(os.environ.get("FMD_BPX64_M", "2048") or 0)
+BPX32_M = int(os.environ.get("FMD_BPX32_M", "128") or 0)
 
 
 def _choose_splits(M, K, nk, bpx=128, bco=128):
@@ -313,7 +318,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
             raise ValueError(f"halo-tiled weights ({tw.numel()} elements) too small for K={K}, C={cc}")
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
-    bpx = 256 if K <= 16 else 128
+    bpx = 256 if K <= 16 else (128 if K <= 64 or M > BPX64_M else (32 if M <= BPX32_M else 64))
     if d3:   # depth-tap chunks on the halo kernel: pre-tiled (kz, channel block) weights are required
         halo = (not force_generic and wgt_tiled is not None and Do == (2 * Ds if upsample else Ds) and
                 halo_eligible(N * Do, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
