@@ -233,7 +233,7 @@ def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
     workgroups, else enough chunk-range splits (>= 2 chunks each) to reach ~256; 0 = not eligible
     (fewer than HALO_MIN_WG workgroups)."""
     nwg = N * (Ho // 16) * (Wo // 16) * -(-K // 128)
-    if nwg >= 128:
+    if nwg >= max(128, HALO_MIN_WG):   # the kernel's own threshold (fmd_halo_set_min_workgroups) may be higher
         return 1
     nch = -(-max(Cin, 1) // HALO_BK) * ztaps
     sp = min(-(-HALO_SPLIT_WG // max(nwg, 1)), nch // HALO_MIN_CHUNKS, HALO_SPLIT_CAP)
