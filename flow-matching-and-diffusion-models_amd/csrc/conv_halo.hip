@@ -61,7 +61,8 @@ struct HArgs {
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
   unsigned long long* tbuf;    // per-wave phase timestamps (compiled in only with -DFMD_HALO_TIME)
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
-                               // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop
+                               // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop,
+                               // 16 no SiLU' in the epilogue, 32 no statistics, 64 no side-tile loads
 };
 
 #ifdef FMD_HALO_DBG
@@ -581,7 +582,7 @@ void conv3x3_halo(const HArgs A) {
         const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
                            : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
                                            : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-        sv[k] = *(const u32x4*)src;
+        sv[k] = HDBG(64) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
       }
 #pragma unroll
       for (int k = 0; k < SK; ++k) {
