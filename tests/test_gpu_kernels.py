@@ -497,7 +497,10 @@ def test_halo_conv_matches_generic(case):
     if want:
         ta = sa.slab.view(N, -1, K, 2).sum(1)
         tb = sb.slab.view(N, -1, K, 2).sum(1)
-        torch.testing.assert_close(ta, tb, rtol=2e-3, atol=1e-2)
+        # both paths take the statistics on their own bf16-rounded outputs, and the two fp32 summation orders round
+        # some outputs one bf16 step apart; the epilogue / bias / affine draws come from the global RNG, so the
+        # worst sum moves with test order (seen: 0.029 on a sum of 6.6 when run after a subset of the suite)
+        torch.testing.assert_close(ta, tb, rtol=5e-3, atol=3e-2)
 
 
 @pytest.mark.parametrize("case", ["fwd_pro_stats", "dgrad_ep_stats"])
