@@ -120,6 +120,41 @@ def pmc_traffic():
         return float(json.load(f)["traffic_bytes_per_launch"])
 
 
+CONFIG_E_FWD_GFLOP = 32854.2   # forward GFLOP per 128^3 sample (torch flop counter on the reference)
+
+
+def config_e_leg(dev, size=128, steps=5, warmup=2):
+    """BASELINE.json configs[4] on one GPU: EfficientUNetND with spatial_dims=3 from the same ldct_flow_matching.json
+    model block (308,246,913 parameters), one graph-captured FM train step on a synthetic (1,1,128,128,128) volume
+    (+ its concatenated LDCT volume), batch 1 (the per-rank batch of the 8-GPU DDP config).  Returns ms/step,
+    samples/s and the step's fraction of the dense bf16 MFMA peak at 3 x forward FLOPs."""
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    torch.manual_seed(0)
+    model = DiffusionUNetFactory().build(dict(LDCT_FM_UNET, spatial_dims=3, sample_size=size), "concatenate", 1).to(dev)
+    nparam = sum(p.numel() for p in model.parameters())
+    g = torch.Generator(device=dev).manual_seed(7)
+    clean = torch.rand(1, 1, size, size, size, device=dev, generator=g)
+    ldct = (clean + 0.05 * torch.randn(1, 1, size, size, size, device=dev, generator=g)).clamp(0, 1)
+    tr = FusedTrainStep(model, lr=1e-4, warmup=500, total_steps=100000, num_train_timesteps=1000)
+    tr.capture(clean, ldct, warmup_iters=2)
+    for _ in range(warmup):
+        tr.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = tr.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    gflop = 3 * CONFIG_E_FWD_GFLOP * (size / 128) ** 3
+    out = dict(workload=f"config E: EfficientUNetND spatial_dims=3, {size}^3, batch 1, graph-captured FM train step",
+               params=nparam, ms_per_step=dt * 1e3, samples_per_sec=1.0 / dt, tflops=gflop / dt / 1e3,
+               mfma_frac=gflop / dt / 1e3 / PEAK_BF16_TFLOPS, loss=float(loss), steps=steps)
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -184,6 +219,21 @@ def cpu_baseline(iters=3, batch=2, sampler_steps=3):
                        f"to the 50-step loop)")
 
 
+def _launch_ranks(n: int) -> int:
+    """Run this script under ``python -m torch.distributed.run --nproc-per-node n`` (rendezvous on 127.0.0.1, a
+    free port) as a child process; returns its exit code.  Called before any GPU work in this process."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,9 +245,18 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sampler", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the per-kernel roofline legs")
+    ap.add_argument("--no-config-e", action="store_true", help="skip the config E (3-D 128^3) leg")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` outside a launcher: start N rank processes (torch.distributed.run, the reference's
+        # torchrun launch, README.md:56-59) BEFORE this process touches the GPU, and exit with their status;
+        # rank 0 prints the JSON line
+        sys.exit(_launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting the launcher's world size")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; FMD_DIST_BACKEND=gloo + more ranks than GPUs rehearses the N-rank path (split graph
@@ -307,15 +366,27 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    roof = conv_roofline(dev)
-    log(f"[bench] dominant conv: {roof['ms']:.3f} ms, {roof['tflops']:.1f} TFLOP/s")
-    # the same problem's backward kernels (the step's next two largest buckets), same protocol
-    back = {}
-    for prob in ("dgrad", "wgrad"):
-        r = conv_roofline(dev, prob=prob)
-        back[prob] = {"achieved": r["tflops"], "frac": r["tflops"] / PEAK_BF16_TFLOPS, "kernel": r["kernel"],
-                      "kernel_ms": r["ms"], "flops_per_launch": r["flops_per_launch"]}
-        log(f"[bench] {prob}: {r['ms']:.3f} ms, {r['tflops']:.1f} TFLOP/s")
+    roofline = back = None
+    if not args.no_roofline:
+        roof = conv_roofline(dev)
+        log(f"[bench] dominant conv: {roof['ms']:.3f} ms, {roof['tflops']:.1f} TFLOP/s")
+        roofline = {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(), "kernel": roof["kernel"],
+                    "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]}
+        # the same problem's backward kernels (the step's next two largest buckets), same protocol
+        back = {"peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s"}
+        for prob in ("dgrad", "wgrad"):
+            r = conv_roofline(dev, prob=prob)
+            back[prob] = {"achieved": r["tflops"], "frac": r["tflops"] / PEAK_BF16_TFLOPS, "kernel": r["kernel"],
+                          "kernel_ms": r["ms"], "flops_per_launch": r["flops_per_launch"]}
+            log(f"[bench] {prob}: {r['ms']:.3f} ms, {r['tflops']:.1f} TFLOP/s")
+    cfg_e = None
+    if world == 1 and not args.no_config_e:
+        try:
+            cfg_e = config_e_leg(dev)
+            log(f"[bench] config E: {cfg_e['ms_per_step']:.1f} ms/step, {cfg_e['mfma_frac']:.3f} of peak")
+        except Exception as e:  # pragma: no cover
+            cfg_e = dict(error=str(e))
     step_tflops = train_ips / world * TRAIN_GFLOP_PER_IMAGE / 1e3
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -343,10 +414,10 @@ def main():
         "train_loss": loss_v,
         "train_mfma_frac": step_tflops / PEAK_BF16_TFLOPS,
         **samp,
-        "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(), "kernel": roof["kernel"],
-                     "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]},
-        "roofline_backward": {"peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", **back},
+        "roofline": roofline,
+        "roofline_backward": back,
+        "config_e_ms_per_step": cfg_e.get("ms_per_step") if cfg_e else None,
+        "config_e": cfg_e,
         "cpu_baseline": cpu,
     }
     print(json.dumps(res), flush=True)

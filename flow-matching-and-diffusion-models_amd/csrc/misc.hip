@@ -382,10 +382,12 @@ __global__ void flow_euler_kernel(float* __restrict__ x, const float* __restrict
 //   x0 = clip((x - sqrt_b*eps)/sqrt_a);  prev = c_x0*x0 + c_xt*x + c_eps*eps + std*z
 __global__ void ddpm_step_kernel(float* __restrict__ x, const float* __restrict__ eps, int Kpad,
                                  const float* __restrict__ coef, const int* __restrict__ index,
-                                 const float* __restrict__ noise, int N, int Cx, int HW, const float* __restrict__ cond,
-                                 int Cc, int Cpad, bf16r* __restrict__ next) {
+                                 const float* __restrict__ noise, int noise_base, int N, int Cx, int HW,
+                                 const float* __restrict__ cond, int Cc, int Cpad, bf16r* __restrict__ next) {
 #pragma clang fp contract(off)
   const int idx = index[0];
+  // variance-noise row: noise_base >= 0 -> a per-step table whose row 0 is step noise_base; < 0 -> one buffer
+  const size_t nrow = noise_base >= 0 ? (size_t)(idx - noise_base) : 0;
   const float* cf = coef + idx * 7;
   const float sqrt_b = cf[0], sqrt_a = cf[1], cx0 = cf[2], cxt = cf[3], sd = cf[4], clip = cf[5], ceps = cf[6];
   const long long total = (long long)N * HW;
@@ -401,7 +403,7 @@ __global__ void ddpm_step_kernel(float* __restrict__ x, const float* __restrict_
       if (clip > 0.f) x0 = fminf(fmaxf(x0, -clip), clip);
       float pv = cxt != 0.f ? cx0 * x0 + cxt * xv : cx0 * x0;
       if (ceps != 0.f) pv = pv + ceps * e;
-      if (noise && sd > 0.f) pv = pv + sd * noise[(size_t)idx * N * Cx * HW + xi];
+      if (noise && sd > 0.f) pv = pv + sd * noise[nrow * N * Cx * HW + xi];
       x[xi] = pv;
       if (next) next[p * Cpad + c] = (bf16r)f2bf(pv);
     }
@@ -492,6 +494,17 @@ __global__ void sched_step_kernel(const fmd_sched_step_desc D) {
       for (int ch = 0; ch < D.Cc; ++ch) nx[p * D.Cpad + D.Cx + ch] = (bf16r)f2bf(D.cond[((size_t)n * D.Cc + ch) * D.HW + hw]);
       for (int ch = D.Cx + D.Cc; ch < D.Cpad; ++ch) nx[p * D.Cpad + ch] = 0;
     }
+  }
+}
+
+// y = x with channels [0, C) of every NHWC bf16 pixel mapped to s*x + b (fp32 arithmetic, one rounding), the
+// padded channels copied: UNetDiffusersND(center_input_sample=True)'s ``2 * x - 1.0`` on the packed model input
+// (unet_diffusers_nd.py:156-157)
+__global__ void affine_channels_kernel(const bf16r* __restrict__ x, int C, int Cpad, long long npix, float sc,
+                                       float sh, bf16r* __restrict__ y) {
+  GRID_STRIDE(i, npix * Cpad) {
+    const int c = (int)(i % Cpad);
+    y[i] = c < C ? (bf16r)f2bf(sc * bf2f(x[i]) + sh) : x[i];
   }
 }
 
@@ -1000,9 +1013,10 @@ int fmd_flow_euler(float* x, const float* v, int32_t Kpad, const float* sigmas, 
 }
 
 int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, const int32_t* index,
-                  const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
-                  void* next, fmd_stream_t s) {
-  LAUNCH(ddpm_step_kernel, grid_for((long long)N * HW), x, eps, Kpad, coef, index, noise, N, Cx, HW, cond, Cc, Cpad,
+                  const float* noise, int32_t noise_base, int32_t N, int32_t Cx, int32_t HW, const float* cond,
+                  int32_t Cc, int32_t Cpad, void* next, fmd_stream_t s) {
+  LAUNCH(ddpm_step_kernel, grid_for((long long)N * HW), x, eps, Kpad, coef, index, noise, noise_base, N, Cx, HW, cond,
+         Cc, Cpad,
          (bf16r*)next);
 }
 
@@ -1012,6 +1026,13 @@ int fmd_fill_from_table(const float* table, const int32_t* index, float* out, in
 }
 
 int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s) { LAUNCH(counter_add_kernel, 1, c, v); }
+
+int fmd_affine_channels(const void* x, int32_t C, int32_t Cpad, int64_t npix, float scale, float shift, void* y,
+                        fmd_stream_t s) {
+  if (!x || !y || C < 0 || C > Cpad || npix < 0) return -1;
+  LAUNCH(affine_channels_kernel, grid_for(npix * Cpad), (const bf16r*)x, C, Cpad, (long long)npix, scale, shift,
+         (bf16r*)y);
+}
 
 int fmd_lincomb(const fmd_lincomb_desc* d, fmd_stream_t s) {
   if (!d || !d->out || d->nin < 1 || d->nin > FMD_LINCOMB_MAX || d->n < 0) return -1;

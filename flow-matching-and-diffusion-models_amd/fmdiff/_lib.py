@@ -133,7 +133,8 @@ SIGNATURES = {
     "fmd_mse": [p, i32, p, p, f32, i32, i32, i32, f32, p, i32, p, p, p],
     "fmd_adamw": [p, p, p, p, i64, f32, f32, f32, f32, f32, f32, f32, p],
     "fmd_flow_euler": [p, p, i32, p, p, i32, i32, i32, p, i32, i32, p, p],
-    "fmd_ddpm_step": [p, p, i32, p, p, p, i32, i32, i32, p, i32, i32, p, p],
+    "fmd_affine_channels": [p, i32, i32, i64, f32, f32, p, p],
+    "fmd_ddpm_step": [p, p, i32, p, p, p, i32, i32, i32, i32, p, i32, i32, p, p],
     "fmd_fill_from_table": [p, p, p, i32, p],
     "fmd_gather_row": [p, p, i64, p, p],
     "fmd_counter_add": [p, i32, p],

@@ -29,8 +29,6 @@ class BaseUNetND(nn.Module):
         from ...runtime.engine import unet_apply
         if context_ca is not None:
             self._prepare_input(x, None, context_ca)   # reference validation (unet.py:301)
-        if getattr(self, "center_input_sample", False):
-            raise NotImplementedError("center_input_sample is not yet on the fmdiff HIP engine")
         t = self._normalize_timesteps(t, x)
         # the channel concat of `context` is fused into the NHWC staging kernel
         return unet_apply(self, x, t, context, context_ca)

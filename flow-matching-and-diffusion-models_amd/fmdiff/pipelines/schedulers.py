@@ -537,7 +537,10 @@ class UniPCMultistepScheduler(_MultistepBase):
 
     def plan(self, start: int = 0) -> torch.Tensor:
         """Coefficient rows of fmd_sched_step (corrector + predictor) for steps ``start`` .. end of the schedule,
-        in the order ``step`` takes them from a fresh state: [n - start][12] fp32."""
+        in the order ``step`` takes them from a fresh state: [n - start][12] fp32.  A row holds at most 3 history
+        coefficients (corrector and predictor), so solver_order > 3 is the eager ``step``'s only."""
+        if int(self.config.solver_order) > 3:
+            raise NotImplementedError("UniPC plan(): solver_order > 3 has no table step; use the eager step")
         n = len(self.timesteps)
         saved = (self._step_index, self.this_order)
         rows, lon, this_order = [], 0, None

@@ -42,19 +42,18 @@ def _own_stream(fn):
     inf) -- with the graphs replayed on the null stream, with a host synchronisation between the replay and the
     all-reduce, and also with this hand-off to a private stream; with the whole process on a created stream
     (``torch.cuda.set_stream`` before any work, as bench.py and the trainer loop do) every run was bit-identical
-    to the eager reference.  Multi-rank callers on the null stream therefore get a warning."""
+    to the eager reference.  The cause is not established, so a multi-rank step from the null stream is refused
+    (RuntimeError) rather than run on possibly corrupt gradients; single-process callers keep the hand-off."""
     @functools.wraps(fn)
     def wrapped(self, *a, **kw):
         cur = torch.cuda.current_stream()
         if cur != torch.cuda.default_stream(cur.device):
             return fn(self, *a, **kw)
-        if getattr(self, "world", 1) > 1 and not getattr(self, "_warned_stream", False):
-            import warnings
-            warnings.warn("FusedTrainStep with several ranks on the default (null) HIP stream: collectives next to "
-                          "graph replays on that stream corrupted gradients on this stack; call "
-                          "torch.cuda.set_stream(torch.cuda.Stream()) before building the model (as bench.py and "
-                          "the trainer loop do)", RuntimeWarning)
-            self._warned_stream = True
+        if getattr(self, "world", 1) > 1:
+            raise RuntimeError("FusedTrainStep with several ranks on the default (null) HIP stream: collectives next "
+                               "to graph replays on that stream corrupted gradients on this stack; call "
+                               "torch.cuda.set_stream(torch.cuda.Stream()) before building the model (as bench.py "
+                               "and fmdiff.pipelines.train.loop do)")
         st = self.__dict__.get("_work_stream")
         if st is None or st.device != cur.device:
             st = self._work_stream = torch.cuda.Stream(device=cur.device)
@@ -409,7 +408,9 @@ class FusedSampler:
 
     * FlowMatchEuler: ``fmd_flow_euler`` (sigmas on the device);
     * DDPM / DDIM (eta 0): ``fmd_ddpm_step`` with a per-step coefficient table (``scheduler.coefficients``)
-      and, for DDPM, the variance noise of every step drawn up front into one [S][N,C,*S] buffer (or injected);
+      and, for DDPM, the variance noise: an injected [S][N,C,*S] table (the S steps that run), or one
+      [N,C,*S] buffer refilled from ``generator`` before every step (outside the graph, so any generator works
+      and memory does not grow with the schedule length: 1000 steps of a 512^2 batch would be 8 GB);
     * DPM-Solver(++) / UniPC: ``fmd_sched_step`` over ``scheduler.plan()`` (the host bookkeeping of the
       eager ``step``: order warm-up, lower-order final steps, corrector) and a 4-slot data-prediction ring.
 
@@ -471,8 +472,9 @@ class FusedSampler:
         self.inp = ops.noise_prepare(None, self.x, None, None, self.cond, max(8, -(-(Cx + Cc) // 8) * 8))
         self.tbuf = torch.empty(init.shape[0], device=dev, dtype=torch.float32)
         self.noise = None
-        if self.kind == "ddpm":   # row i = step i's variance noise (NCHW), all steps of the schedule
-            self.noise = torch.empty((len(self.sched.timesteps), *init.shape), device=dev, dtype=torch.float32)
+        self.noise_base = -1
+        if self.kind == "ddpm":   # one step's variance noise (NCHW); _arm_noise swaps in an injected table
+            self.noise = torch.empty(init.shape, device=dev, dtype=torch.float32)
         self.ring = self.last = None
         if self.kind == "ms":
             self.ring = [torch.zeros_like(self.x) for _ in range(4)]
@@ -481,13 +483,31 @@ class FusedSampler:
         self.eng.set_time_table(self.ts, init.shape[0], self.idx)
         self._tt = self.eng._tt   # the captured step reads these tables: keep them alive with the graph
 
-    def _draw(self, noise, generator):
-        if self.noise is None:
-            return
-        if noise is not None:
-            self.noise[self.S0:].copy_(noise.reshape(self.S, *self.noise.shape[1:]))
-        else:
-            self.noise[self.S0:].normal_(generator=generator)
+    def _arm_noise(self, noise, captured: bool):
+        """DDPM variance noise for this call: an injected [S, *shape] table (row 0 = step S0) or the per-step
+        buffer.  A captured graph keeps the buffer it was recorded with, so a cached graph re-armed with the
+        other mode is dropped (returns False)."""
+        if self.kind != "ddpm":
+            return True
+        want_table = noise is not None
+        if captured and want_table != (self.noise_base >= 0):
+            return False
+        if want_table:
+            rows = noise.reshape(self.S, *self.x.shape).float()
+            if self.noise_base >= 0 and self.noise.shape == rows.shape:
+                self.noise.copy_(rows)
+            else:
+                self.noise = rows.contiguous().clone()
+            self.noise_base = self.S0
+        elif self.noise_base >= 0 or self.noise is None:
+            self.noise = torch.empty(self.x.shape, device=self.x.device, dtype=torch.float32)
+            self.noise_base = -1
+        return True
+
+    def _pre(self, generator):
+        """Before each step: a fresh variance-noise draw into the per-step buffer (DDPM without injection)."""
+        if self.kind == "ddpm" and self.noise_base < 0:
+            self.noise.normal_(generator=generator)
 
     def _refresh(self, init, cond, context_ca):
         """Re-arm the cached graph's static buffers for a new call (same shapes): sample, conditioning, the
@@ -521,7 +541,7 @@ class FusedSampler:
         if self.kind == "fm":
             ops.flow_euler(self.x, out, self.sig, self.idx, self.cond, self.inp)
         elif self.kind in ("ddpm", "ddim"):
-            ops.ddpm_step(self.x, out, self.coef, self.idx, self.noise, self.cond, self.inp)
+            ops.ddpm_step(self.x, out, self.coef, self.idx, self.noise, self.cond, self.inp, self.noise_base)
         else:
             ops.sched_step(self.x, out, self.ring, self.last if self._unipc() else None, self.coef, self.idx,
                            self.cond, self.inp)
@@ -539,40 +559,50 @@ class FusedSampler:
         """``cond``: concatenated conditioning; ``context_ca``: cross-attention conditioning; ``noise``: DDPM
         variance noise of the S steps ([S, *init.shape]; drawn with ``generator`` when None).  ``timing``: the
         reference's ``model_seconds`` / ``model_calls`` accumulators (pipelines/utils.py:196-200), here the
-        whole replayed loop (UNet + scheduler update) between two device synchronisations.
+        S steps of the loop (UNet + scheduler update, which the reference times apart) between two device
+        synchronisations; a first call's graph capture is excluded.
 
         With ``use_graph`` the step is captured once per input shape and the graph is kept: a later call
         with the same shapes only re-arms the static buffers (``_refresh``) and replays it S times.  The
         returned tensor is a copy of the sample buffer."""
         key = self._key(init, cond, context_ca)
         t0 = None
-        if use_graph and self._graph is not None and self._gkey == key:
+        if use_graph and self._graph is not None and self._gkey == key and self._arm_noise(noise, True):
             self._refresh(init, cond, context_ca)
-            self._draw(noise, generator)
             if timing is not None:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
             for _ in range(self.S):
+                self._pre(generator)
                 self._graph.replay()
             return self._finish(timing, t0)
         self._graph = None
         self._prepare(init, cond)
-        self._draw(noise, generator)
+        self._arm_noise(noise, False)
         self.cca = context_ca.float().contiguous() if context_ca is not None else None
         if timing is not None:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
         if not use_graph:
             for _ in range(self.S):
+                self._pre(generator)
                 self._one()
             return self._finish(timing, t0)
         self.eng.invalidate_weights()
+        self._pre(generator)
         self._one()   # the first step eagerly: re-derives the bf16 weights and warms the allocator
         g = torch.cuda.CUDAGraph()
         mode = "thread_local" if torch.distributed.is_available() and torch.distributed.is_initialized() else "global"
+        if timing is not None:   # the capture is set-up, not model time: keep it out of model_seconds
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
         with torch.cuda.graph(g, capture_error_mode=mode):   # records, does not execute: the counter stays
             self._one()
+        if timing is not None:
+            torch.cuda.synchronize()
+            t0 += time.perf_counter() - tc
         for _ in range(self.S - 1):
+            self._pre(generator)
             g.replay()
         self._graph, self._gkey = g, key
         return self._finish(timing, t0)

@@ -43,23 +43,15 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 CPAD = 8      # NHWC channel padding of the model input / output (16-byte rows)
 HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdiff.h)
-# GN+SiLU prologue materialised by fmd_gn_apply_fwd (one streaming pass) instead of recomputed inside the
-# halo conv and its weight gradient, for single-source inputs of at most MAT_CMAX channels at levels of at
-# least MAT_MIN_HW pixels, where the streaming pass costs less than the in-kernel transform it removes
-MAT_PRO = os.environ.get("FMD_MAT_PRO", "0") == "1"   # measured net-negative at batch 8
-MAT_CMAX = 128
 # 3-D: materialise the GN+SiLU operand of depth-tap halo convs (FMD_MAT3D=0: fused prologue + G side output)
 MAT3D = os.environ.get("FMD_MAT3D", "1") == "1"
 # 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
 DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
-MAT_MIN_HW = 128 * 128
 # ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); FMD_POINT_1X1=0 for A/B runs
 POINT_1X1 = os.environ.get("FMD_POINT_1X1", "1") == "1"
-# training: halo convs with a GN+SiLU prologue write G = SiLU(GN(x)) for the weight gradient (fmd_conv_desc.gout)
-# instead of the weight-gradient kernel recomputing it.  Default: 3-D convs only ("3d"), whose weight gradient
-# recomputes G once per depth tap (3x); on 2-D the extra 2 B/element of HBM writes cost the forward more than the
-# weight gradient saves.  FMD_GOUT=all | 3d | 0 for A/B runs.
-GOUT = os.environ.get("FMD_GOUT", "3d")
+# training, 3-D fused-prologue halo convs (FMD_MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
+# (fmd_conv_desc.gout), which would otherwise recompute G once per depth tap.  Not on 2-D: there the extra
+# 2 B/element of HBM writes cost the forward more than the weight gradient saves.
 
 
 class Act:
@@ -100,12 +92,11 @@ def _materialise(halo: bool, x1, Cin: int, HW: int, d3: bool = False) -> bool:
     the generic implicit-GEMM path (small levels), whose gather would redo the transform once per tap
     (9x, VALU-bound at the low occupancy of those levels); on the 3-D depth-tap halo path when MAT3D (its
     chunks stage every input slice for 3 depth taps, so the fused transform runs ~3.8x per element, and the
-    weight gradient reads the same materialised operand); on the 2-D halo path only if MAT_PRO."""
+    weight gradient reads the same materialised operand); never on the 2-D halo path (a 41 us streaming pass
+    per 256^2 conv against ~23 us of in-kernel transform saved: measured net-negative)."""
     if not halo:
         return True
-    if d3 and MAT3D:
-        return True
-    return MAT_PRO and x1 is None and Cin <= MAT_CMAX and HW >= MAT_MIN_HW
+    return bool(d3 and MAT3D)
 
 
 class WeightCache:
@@ -345,17 +336,6 @@ class UNetEngine:
         self.wc = WeightCache()
         self._tt = None   # precomputed per-step time embeddings (set_time_table)
         self.gl, self.gl_slot = self._group_emb_layers(model)
-        # weight gradients (+ their split-K reductions) may run on a second HIP stream beside the
-        # data-gradient chain (they are off its critical path until the optimizer step).  Off by default:
-        # measured on MI355X the halo wgrad/dgrad kernels then contend for LDS and the step does not
-        # get faster (28.9 vs 28.8 ms).
-        # FMD_SIDE_WGRAD: unset / 0 off, 1 every weight gradient, N > 1 only problems of <= N output pixels
-        # (the small levels, where both chains are launch-latency bound)
-        side = int(os.environ.get("FMD_SIDE_WGRAD", "0") or 0)
-        self.side_stream_wgrad = side > 0
-        self.side_px_max = side if side > 1 else None
-        self._side = None
-        self._side_keep = []
         # spatial_dims = 1: signals run as (L, 1) images -- 1-D k-tap weights embedded as k x k
         # (WeightCache.embed1d), resampling along the first dim only
         self.dims1 = next(c for c in model.modules() if isinstance(c, Conv)).dims == 1
@@ -499,24 +479,13 @@ class UNetEngine:
         return o
 
     def _wg(self, fn, px=None):
-        """Issue ``fn`` (weight-gradient work) on the side stream after everything queued so far on the
-        current stream; ``fn`` (and so every tensor it references) is kept alive until ``_join``.  ``px``:
-        output pixels of the problem (``side_px_max`` keeps larger ones on the current stream)."""
-        if not self.side_stream_wgrad or (self.side_px_max is not None and (px is None or px > self.side_px_max)):
-            fn()
-            return
-        main = torch.cuda.current_stream()
-        if self._side is None or self._side.device != main.device:
-            self._side = torch.cuda.Stream(device=main.device)
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            fn()
-        self._side_keep.append(fn)
+        """Weight-gradient work, issued in line on the current stream.  (A side-stream variant beside the
+        data-gradient chain measured no gain on MI355X -- the halo wgrad / dgrad kernels contend for LDS and
+        the issue port -- and was retired in round 4.)"""
+        fn()
 
     def _join(self):
-        if self._side is not None and self._side_keep:
-            torch.cuda.current_stream().wait_stream(self._side)
-        self._side_keep = []
+        pass
 
     def _wts(self, w, mode, halo: bool, Kpad=None, Cpad=None):
         """(base, tiled) kernel layouts of ``w``: only the one the chosen conv path reads is derived
@@ -608,7 +577,7 @@ class UNetEngine:
         mat2 = _materialise(halo2, None, Cout, HW, len(sp) == 3) or bool(drop)   # dropout acts on the materialised operand
         fuse2 = mat2 and ops.gn_fused_eligible(HW, Cout, Cout, g2.num_groups)
         src1 = x1.t if (x1 is not None and t1 is None) else None
-        keep_g = ctx.tape is not None and (GOUT == "all" or (GOUT == "3d" and len(sp) == 3))
+        keep_g = ctx.tape is not None and len(sp) == 3
         gg1 = (torch.empty((N, *sp, Cin), device=x0.t.device, dtype=torch.bfloat16)
                if keep_g and t1 is None and halo1 and not point and Cin % HALO_BK == 0 else None)
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
@@ -1000,6 +969,8 @@ class UNetEngine:
         N = xin.shape[0]
         if xin.dim() == 3:   # 1-D signal [N][L][C] -> an (L, 1) image
             xin = xin.unsqueeze(2)
+        if getattr(m, "center_input_sample", False):   # x = 2 * cat(x, context) - 1 (unet_diffusers_nd.py:156-157)
+            xin = ops.affine_channels(xin, m.conv_in.in_channels, 2.0, -1.0)
         ctx = self.time_mlp(t, save, N, t_scale, t_trunc)
         ctx.cca = context_ca
         x = Act(xin, need_grad=False)

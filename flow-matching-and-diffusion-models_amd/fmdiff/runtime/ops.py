@@ -252,8 +252,10 @@ def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, trans
     """Mirror of fmd_conv_halo's applicability test (csrc/conv_halo.hip): 3x3 s1 p1 forward gather,
     16x16 output tiles, K > 16, at least 128 workgroups (with split-K over channel chunks when the
     level is small), GN-prologue inputs of at most HALO_CMAX channels."""
+    Ws = Wo // 2 if upsample else Wo
     return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed and not (pro and Cin > HALO_CMAX)
             and Ho % 16 == 0 and Wo % 16 == 0 and (Ho == 2 * Hs if upsample else Ho == Hs)
+            and N * Hs * Ws * max(Cin, 1) < (1 << 31)   # the kernel's 32-bit element offsets (conv_halo.hip)
             and halo_splits(N, Ho, Wo, K, Cin, ztaps) > 0)
 
 
@@ -318,7 +320,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
             raise ValueError(f"halo-tiled weights ({tw.numel()} elements) too small for K={K}, C={cc}")
     nk = -(-(C0 + C1) // 64) * T + (-(-(d.C2 + d.C3) // 64) if src2 is not None else 0)
     bco = 16 if K <= 16 else (64 if K <= 64 else 128)
-    bpx = 256 if K <= 16 else (128 if K <= 64 or M > BPX64_M else (32 if M <= BPX32_M else 64))
+    # pixel tile the generic kernel will use IF it runs split-K (csrc/conv.hip fmd_conv: the 64 / 32-pixel tiles
+    # exist only for splits > 1); re-decided below once the split count is known
+    bpx_split = 256 if K <= 16 else (128 if K <= 64 or M > BPX64_M else (32 if M <= BPX32_M else 64))
+    bpx = bpx_split
     if d3:   # depth-tap chunks on the halo kernel: pre-tiled (kz, channel block) weights are required
         halo = (not force_generic and wgt_tiled is not None and Do == (2 * Ds if upsample else Ds) and
                 halo_eligible(N * Do, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed, C0 + C1,
@@ -342,6 +347,8 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.wgt_tiled, d.wgt2_tiled = _p(wgt_tiled), _p(wgt2_tiled)
     if splits is None:
         splits = _choose_splits(M, K, nk, bpx, bco)
+    if not halo and splits <= 1 and K > 64:
+        bpx = 128   # the kernel's rule: small-pixel tiles only with split-K
     ws = None
     if splits > 1:
         ws = torch.empty((splits, M, K), device=dev, dtype=F32)
@@ -901,11 +908,23 @@ def flow_euler(x, v_nhwc, sigmas, index, cond, next_inp):
               next_inp.shape[-1] if next_inp is not None else 0, _p(next_inp), stream())
 
 
-def ddpm_step(x, eps_nhwc, coef, index, noise, cond, next_inp):
+def affine_channels(x, C: int, scale: float, shift: float):
+    """y = x (channels-last bf16) with channels [0, C) mapped to scale * x + shift (fmd_affine_channels)."""
+    _need_cuda(x, "affine_channels")
+    y = torch.empty_like(x)
+    _lib.call("fmd_affine_channels", _p(x), int(C), x.shape[-1], x.numel() // x.shape[-1], float(scale), float(shift),
+              _p(y), stream())
+    return y
+
+
+def ddpm_step(x, eps_nhwc, coef, index, noise, cond, next_inp, noise_base=-1):
+    """``noise``: one [N,Cx,*S] buffer (``noise_base`` < 0) or a per-step table [rows][N,Cx,*S] whose row 0 is step
+    ``noise_base`` (fmd_ddpm_step)."""
     N, Cx = x.shape[:2]
     HW = x[0, 0].numel()
     Cc = cond.shape[1] if cond is not None else 0
-    _lib.call("fmd_ddpm_step", _p(x), _p(eps_nhwc), eps_nhwc.shape[-1], _p(coef), _p(index), _p(noise), N, Cx, HW,
+    _lib.call("fmd_ddpm_step", _p(x), _p(eps_nhwc), eps_nhwc.shape[-1], _p(coef), _p(index), _p(noise),
+              int(noise_base), N, Cx, HW,
               _p(cond), Cc, next_inp.shape[-1] if next_inp is not None else 0, _p(next_inp), stream())
 
 

@@ -63,9 +63,6 @@ def _block_engine_cls():
             self.wc = WeightCache()
             self._tt = None
             self.gl, self.gl_slot = None, {}
-            self.side_stream_wgrad = False
-            self._side = None
-            self._side_keep = []
             self._head_bwd = None
             self.dims1 = False
 

@@ -30,9 +30,6 @@ class VAEEngine(UNetEngine):
         self.wc = WeightCache()
         self._tt = None
         self.gl, self.gl_slot = None, {}
-        self.side_stream_wgrad = False
-        self._side = None
-        self._side_keep = []
         self._fold = None
         self._fold_key = None
         self._head_bwd = None

@@ -119,6 +119,8 @@ def _fused_ok(model, scheduler, use_fused) -> bool:
     from ...models.unet.base import BaseUNetND
     from ...pipelines.schedulers import (DDIMScheduler, DDPMScheduler, DPMSolverMultistepScheduler,
                                          FlowMatchEulerDiscreteScheduler, UniPCMultistepScheduler)
+    if isinstance(scheduler, UniPCMultistepScheduler) and int(scheduler.config.solver_order) > 3:
+        return False   # the table step (fmd_sched_step) holds <= 3 history coefficients; the eager step any order
     return use_fused and isinstance(model, BaseUNetND) and isinstance(scheduler, (
         FlowMatchEulerDiscreteScheduler, DDPMScheduler, DDIMScheduler, DPMSolverMultistepScheduler,
         UniPCMultistepScheduler))

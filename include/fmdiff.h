@@ -362,9 +362,11 @@ int fmd_adamw_sched(float* p, const float* g, float* m, float* v, int64_t n, con
                     fmd_stream_t s);
 int fmd_flow_euler(float* x, const float* v, int32_t Kpad, const float* sigmas, const int32_t* index, int32_t N,
                    int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad, void* next, fmd_stream_t s);
+/* noise: DDPM variance noise, a per-step table whose row 0 belongs to step noise_base (row = index - noise_base),
+ * or, with noise_base < 0, one [N][Cx][HW] buffer refilled before every step; NULL for DDIM / the last step. */
 int fmd_ddpm_step(float* x, const float* eps, int32_t Kpad, const float* coef, const int32_t* index,
-                  const float* noise, int32_t N, int32_t Cx, int32_t HW, const float* cond, int32_t Cc, int32_t Cpad,
-                  void* next, fmd_stream_t s);
+                  const float* noise, int32_t noise_base, int32_t N, int32_t Cx, int32_t HW, const float* cond,
+                  int32_t Cc, int32_t Cpad, void* next, fmd_stream_t s);
 int fmd_fill_from_table(const float* table, const int32_t* index, float* out, int32_t N, fmd_stream_t s);
 /* out = sum_k c[k] * in[k] over n fp32 elements: the multistep scheduler updates (DPM-Solver / UniPC,
  * replaces diffusers' DPMSolverMultistepScheduler.step / UniPCMultistepScheduler.step tensor arithmetic,
@@ -409,6 +411,11 @@ int fmd_sched_step(const fmd_sched_step_desc* d, fmd_stream_t s);
  * sampling schedule) selected by a device-side step counter, so the step stays graph-replayable. */
 int fmd_gather_row(const float* table, const int32_t* index, int64_t n, float* out, fmd_stream_t s);
 int fmd_counter_add(int32_t* c, int32_t v, fmd_stream_t s);
+/* y = x (NHWC bf16, Cpad channels per pixel) with channels [0, C) mapped to scale * x + shift: the model
+ * input centring of UNetDiffusersND(center_input_sample=True), `x = 2 * x - 1.0`
+ * (src/models/unet/unet_diffusers_nd.py:156-157), applied to the packed input (one extra bf16 rounding). */
+int fmd_affine_channels(const void* x, int32_t C, int32_t Cpad, int64_t npix, float scale, float shift, void* y,
+                        fmd_stream_t s);
 
 #ifdef __cplusplus
 }

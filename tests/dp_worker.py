@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--rank", type=int, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--null-stream", action="store_true",
+                    help="stay on the legacy null stream (FusedTrainStep must refuse a multi-rank step there)")
     ap.add_argument("--mode", default="graph", choices=["graph", "graph_plain", "eager", "eager_plain"],
                     help="graph: capture + replay (the trainer's path); eager: step() with the overlapped exchange; "
                          "eager_plain: step() with one blocking all-reduce after the backward")
@@ -49,7 +51,8 @@ def main():
     torch.cuda.set_device(0)
     # as bench.py and the trainer loop do: all work on a created stream (graph replays and collectives on the
     # legacy null stream corrupted gradient buckets on this stack)
-    torch.cuda.set_stream(torch.cuda.Stream())
+    if not a.null_stream:
+        torch.cuda.set_stream(torch.cuda.Stream())
     if a.world > 1:
         dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
     meta = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["ldct_fm_test"]
@@ -76,6 +79,17 @@ def main():
         return tuple(v[sl].contiguous().to("cuda") for v in batches[i])
 
     c0, l0, n0, t0 = local(0)
+    if a.null_stream:
+        try:
+            step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0) if a.mode.startswith("graph") else \
+                step.step(c0, l0, noise=n0, t=t0)
+            refused = ""
+        except RuntimeError as e:
+            refused = str(e)
+        torch.save({"refused": refused, "world": a.world}, a.out)
+        if a.world > 1:
+            dist.destroy_process_group()
+        return
     if a.mode.startswith("graph"):
         step.capture(c0, l0, warmup_iters=2, noise=n0, t=t0)
     params, losses, gnorms = [], [], []

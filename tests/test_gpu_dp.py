@@ -35,7 +35,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, out_dir, timeout=240, mode="graph"):
+def _run(world, out_dir, timeout=240, mode="graph", extra=()):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
     procs, outs = [], []
@@ -43,7 +43,8 @@ def _run(world, out_dir, timeout=240, mode="graph"):
         out = os.path.join(out_dir, f"w{world}_r{r}_{mode}.pt")
         log = open(os.path.join(out_dir, f"w{world}_r{r}.log"), "w")
         procs.append((subprocess.Popen([sys.executable, WORKER, "--world", str(world), "--rank", str(r),
-                                        "--out", out, "--mode", mode, "--steps", os.environ.get("FMD_DP_STEPS", "2")], env=env, stdout=log, stderr=subprocess.STDOUT), log))
+                                        "--out", out, "--mode", mode, "--steps", os.environ.get("FMD_DP_STEPS", "2"),
+                                        *extra], env=env, stdout=log, stderr=subprocess.STDOUT), log))
         outs.append(out)
     try:
         for p, _ in procs:
@@ -110,3 +111,31 @@ def _initial_params():
     model = DiffusionUNetFactory().build(meta["unet"], tr["conditioning"], ch)
     model.load_state_dict(U.seeded_state_dict(S.derive_spec(meta["unet"], tr["conditioning"], ch), meta["seed"]))
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()]).double()
+
+
+def test_multi_rank_step_on_null_stream_is_refused(tmp_path):
+    """Graph replays + collectives with the process on the legacy null stream corrupted gradient buckets on this
+    stack (fused.py _own_stream); until that is explained the 2-rank step refuses to run there (RuntimeError at
+    capture and at an eager step), while world 1 on the null stream still runs."""
+    for mode in ("graph", "eager"):
+        for r in _run(2, str(tmp_path), mode=mode, extra=("--null-stream",)):
+            assert "null" in r["refused"], (mode, r)
+    (one,) = _run(1, str(tmp_path), mode="graph", extra=("--null-stream",))
+    assert one["refused"] == ""
+
+
+def test_bench_gpus_flag_launches_ranks(tmp_path):
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (torch.distributed.run) before touching the GPU;
+    rank 0 prints one JSON line with n_gpus 2 (gloo transport: the box has one GPU, both ranks share it)."""
+    import json
+    env = dict(os.environ, FMD_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "2", "--img", "64", "--no-sampler", "--no-cpu-baseline", "--no-roofline"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    print(r.stderr[-3000:])
+    assert r.returncode == 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 4 and res["value"] > 0

@@ -631,3 +631,48 @@ def test_fused_train_step_with_context_ca_matches_module_path():
     smp = FusedFlowSampler(model, 4)
     x = smp.sample(torch.randn(4, 1, 32, 32, device=DEV, generator=g), None, use_graph=True, context_ca=lat)
     assert x.shape == (4, 1, 32, 32) and torch.isfinite(x).all()
+
+
+def test_center_input_sample_vs_oracle(golden):
+    """UNetDiffusersND(center_input_sample=True): ``x = 2 * cat(x, context) - 1`` before conv_in
+    (reference unet_diffusers_nd.py:156-157; factory key diffusionfactory.py:113), on the HIP path as one
+    fmd_affine_channels pass over the packed input.  Forward and FM train-step parameter gradients vs the oracle's
+    fp32 UNet with the same flag (no shipped config sets it, so no reference fixture: pinned by the oracle,
+    whose non-centred forward is golden-pinned)."""
+    import torch.nn.functional as F
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from oracle import spec as S
+    from oracle import unet as U
+    T, M = golden
+    meta = M["mnist_ddpm_diffusers"]
+    unet = dict(meta["unet"], center_input_sample=True)
+    tr = meta["training"]
+    model = DiffusionUNetFactory().build(unet, tr["conditioning"], tr["channels"] or 1).to(DEV)
+    assert model.center_input_sample
+    spec = S.derive_spec(unet, tr["conditioning"], tr["channels"] or 1)
+    assert spec["center_input_sample"]
+    sd = U.seeded_state_dict(spec, meta["seed"])
+    model.load_state_dict(sd)
+    name = "mnist_ddpm_diffusers"
+    x, t, cond = T[f"{name}/x"], T[f"{name}/t"], T[f"{name}/cond"]
+    with torch.no_grad():
+        y = model(x.to(DEV), t.to(DEV), context=cond.to(DEV))
+    ref = U.unet_forward(sd, spec, x, t, context=cond)
+    plain = T[f"{name}/y"]
+    err = _rel(y, ref)
+    print(f"center_input_sample forward rel L2 {err:.3e} (centred vs plain reference differ by {_rel(ref, plain):.2f})")
+    assert err < 2e-2
+    assert _rel(ref, plain) > 0.1   # the flag changes the output: the check is not vacuous
+    # gradients
+    sdg = {k: v.clone().requires_grad_() for k, v in sd.items()}
+    tgt = torch.randn(x.shape, generator=torch.Generator().manual_seed(5))
+    F.mse_loss(U.unet_forward(sdg, spec, x, t, context=cond), tgt).backward()
+    F.mse_loss(model(x.to(DEV), t.to(DEV), context=cond.to(DEV)), tgt.to(DEV)).backward()
+    num = den = 0.0
+    for k, p in model.named_parameters():
+        g, r = p.grad.double().cpu(), sdg[k].grad.double()
+        num += (g - r).pow(2).sum().item()
+        den += r.pow(2).sum().item()
+    rel = math.sqrt(num / den)
+    print(f"center_input_sample grad rel L2 {rel:.3e}")
+    assert rel < 5e-2
