@@ -76,3 +76,15 @@ def golden_ddpm():
     tensors = torch.load(os.path.join(d, "golden_ddpm.pt"), weights_only=True)
     meta = json.load(open(os.path.join(d, "golden_ddpm.json")))
     return tensors, meta
+
+
+@pytest.fixture(scope="session")
+def golden_e():
+    """Config E at its own architecture (308 M 3-D EfficientUNetND; 64^3 forward, 32^3 FM step): make_golden_e.py."""
+    import json
+
+    import torch
+    d = os.path.join(REPO, "tests", "golden")
+    tensors = torch.load(os.path.join(d, "golden_e.pt"), weights_only=True)
+    meta = json.load(open(os.path.join(d, "golden_e.json")))
+    return tensors, meta

@@ -1,0 +1,93 @@
+"""Configs D and E at their OWN architectures against reference-generated fixtures (BASELINE.json configs[3], [4]).
+
+* Config D: the AutoencoderKL of ``configs/LDCT/LDCT_autoencoder_kl.json`` (82,599,141 parameters: 128/256/512/512
+  channels, 2 res blocks per level, mid attention 4 x 64 over the 8x8 latent grid of a 64x64 image), built by the
+  reference's own VAEFactory in tests/golden/make_vae_golden_d.py; weights regenerated here by the same
+  name-seeded rule (tests/golden/seeded_params.py).  Encode (mu, logvar, posterior.mode()) and decode through the
+  HIP VAE engine vs the reference (reference kl.py:118-130, encoder.py:136-158, decoder.py:137-160).
+* Config E: ``EfficientUNetND(spatial_dims=3)`` from ``configs/flow_matching/ldct_flow_matching.json`` (308,246,913
+  parameters; reference unet.py:70-96, convolution.py:36), tests/golden/make_golden_e.py: the 64^3 forward and the
+  graph-captured FusedTrainStep at 32^3 (loss, gradient statistics and order-sensitive fingerprints, AdamW deltas)
+  with the same checks and tolerances as config B's 256^2 step (test_gpu_unet._check_step_vs_golden).
+
+Tolerances as DESIGN.md section 4: forward / encode / decode relative L2 < 2e-2 (bf16 activations, fp32 accumulation).
+"""
+import json
+import os
+import sys
+import warnings
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def test_config_d_vae_vs_reference_fixture():
+    import seeded_params as SP
+    from fmdiff.models.vae import AutoencoderKL
+    G = torch.load(os.path.join(HERE, "golden", "vae_golden_d.pt"), weights_only=True)
+    model = json.loads(bytes(G["cfg_json"].tolist()).decode())
+    kw = {k: v for k, v in model.items() if k not in ("latent_type", "model_type", "norm_type", "act")}
+    kw["down_channels"] = tuple(kw["down_channels"])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**kw)
+    assert sum(p.numel() for p in vae.parameters()) == int(G["nparam"])
+    SP.fill_module(vae, 3131)
+    vae = vae.to(DEV).eval()
+    x = G["x"].to(DEV)
+    with torch.no_grad():
+        post = vae.encode(vae.image_to_model_range(x))
+        rec = vae.decode(G["z"].to(DEV))
+    errs = dict(mu=_rel(post.mu, G["mu"]), logvar=_rel(post.logvar, G["logvar"]), mode=_rel(post.mode(), G["mode"]),
+                rec=_rel(rec, G["rec"]))
+    print("config D VAE vs reference: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    assert all(v < 2e-2 for v in errs.values()), errs
+
+
+def _build_e(m):
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from oracle import spec as S
+    from oracle import unet as U
+    tr = m["training"]
+    model = DiffusionUNetFactory().build(m["unet"], tr["conditioning"], tr["channels"] or 1)
+    sd = U.seeded_state_dict(S.derive_spec(m["unet"], tr["conditioning"], tr["channels"] or 1), m["seed"])
+    model.load_state_dict(sd)
+    return model.to(DEV), sd
+
+
+def test_config_e_forward_vs_reference_golden(golden_e):
+    T, m = golden_e
+    model, _ = _build_e(m)
+    assert sum(p.numel() for p in model.parameters()) == 308246913
+    with torch.no_grad():
+        y = model(T["fwd/x"].to(DEV), T["fwd/t"].to(DEV), context=T["fwd/cond"].to(DEV))
+    err = _rel(y, T["fwd/y"])
+    print(f"config E 64^3 forward rel L2 {err:.3e}")
+    assert err < 2e-2
+
+
+def test_config_e_fused_train_step_vs_reference_golden(golden_e):
+    """FusedTrainStep (graph-captured, concatenate conditioning, injected eps / t) on config E's 3-D UNet at 32^3:
+    one replay vs the reference's loss, gradients and post-AdamW parameters (flow_matching_lib.py:150-182)."""
+    from fmdiff.pipelines.train.fused import FusedTrainStep
+    from test_gpu_unet import _check_step_vs_golden
+    T, m = golden_e
+    model, sd = _build_e(m)
+    tr = FusedTrainStep(model, lr=m["lr"], warmup=m["warmup"], total_steps=m["total"],
+                        num_train_timesteps=m["num_train_timesteps"], weight_decay=m["weight_decay"])
+    clean, ldct, noise, t = (T[f"step/{k}"].to(DEV) for k in ("clean", "ldct", "noise", "t"))
+    tr.capture(clean, ldct, warmup_iters=2, noise=noise, t=t)
+    loss = tr.replay()
+    torch.cuda.synchronize()
+    assert int(tr.step_ctr.item()) == 1
+    _check_step_vs_golden(model, T, m, "step", loss.item(), m["lr"], small=m["small_grads"], sd_before=sd)

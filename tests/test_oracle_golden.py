@@ -315,3 +315,52 @@ def test_pool_factor_unet_vs_reference(name):
     with torch.no_grad():
         y = U.unet_forward(sd, spec, T[f"{name}/x"], T[f"{name}/t"])
     assert torch.equal(y, T[f"{name}/y"])
+
+
+def test_vae_oracle_matches_config_d_fixture():
+    """oracle/vae.py at config D's own architecture (configs/LDCT/LDCT_autoencoder_kl.json, 82.6 M parameters,
+    reference VAEFactory; tests/golden/make_vae_golden_d.py) vs the reference's encode / decode outputs, with the
+    weights regenerated by the fixture's name-seeded rule."""
+    import json
+    import os
+    import sys
+    import warnings
+    from fmdiff.models.vae import AutoencoderKL
+    from oracle import vae as V
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import seeded_params as SP
+    G = torch.load(os.path.join(os.path.dirname(__file__), "golden", "vae_golden_d.pt"), weights_only=True)
+    model = json.loads(bytes(G["cfg_json"].tolist()).decode())
+    cfg = {k: v for k, v in model.items() if k not in ("latent_type", "model_type", "norm_type", "act")}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**cfg)
+    sd = SP.fill_module(vae, 3131)
+    assert sum(v.numel() for v in sd.values()) == int(G["nparam"])
+    torch.set_num_threads(max(1, min(8, torch.get_num_threads())))
+    with torch.no_grad():
+        m = V.encode_moments(sd, cfg, G["x"] * 2.0 - 1.0)
+        r = V.decode(sd, cfg, G["z"])
+    mu, logvar = m.chunk(2, 1)
+    torch.testing.assert_close(mu, G["mu"], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(logvar.clamp(-30.0, 20.0), G["logvar"], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(r, G["rec"], rtol=1e-4, atol=1e-4)
+
+
+def test_unet_oracle_matches_config_e_fixture():
+    """oracle/unet.py's 3-D EfficientUNetND at config E's own architecture (308 M parameters) reproduces the
+    reference module's 64^3 forward (tests/golden/make_golden_e.py)."""
+    import json
+    import os
+    from oracle import spec as S
+    from oracle import unet as U
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    T = torch.load(os.path.join(d, "golden_e.pt"), weights_only=True)
+    m = json.load(open(os.path.join(d, "golden_e.json")))
+    tr = m["training"]
+    spec = S.derive_spec(m["unet"], tr["conditioning"], tr["channels"] or 1)
+    sd = U.seeded_state_dict(spec, m["seed"])
+    assert sum(v.numel() for v in sd.values()) == 308246913
+    with torch.no_grad():
+        y = U.unet_forward(sd, spec, torch.cat([T["fwd/x"], T["fwd/cond"]], 1), T["fwd/t"])
+    torch.testing.assert_close(y, T["fwd/y"], rtol=1e-4, atol=1e-4)
