@@ -30,8 +30,7 @@
 // Same epilogue contract as csrc/conv.hip (bias, per-sample bias, residual,
 // second 1x1 GEMM over src2|src3, data-gradient SiLU' + GN-backward sums,
 // channel statistics).
-#include "common.h"
-#include "../../include/fmdiff.h"
+#include "halo_args.h"
 
 namespace {
 
@@ -45,25 +44,7 @@ constexpr int HBUF = KC * HPAD * 8;       // bf16 elements per halo buffer (21 K
 constexpr int WBUF = KC * BCO * 8;        // bf16 elements per weight tile (8 KiB = one 16 B DMA per thread)
 static_assert(2 * HBUF + 4 * WBUF >= TH * TW * BCO, "epilogue tile fits in the staging LDS");
 
-struct HArgs {
-  fmd_conv_desc d;
-  int C, C23;
-  int tiles_x, tiles_y, ntc;
-  int nchunk1, nchunk2;   // main / 1x1-segment chunks
-  int splits, cps;        // split-K over main chunks: split y owns chunks [y*cps, min(nchunk1, (y+1)*cps));
-                          // the 1x1 segment belongs to the last split; fp32 partials go to d.ws
-  int nsteps_slots;       // taps over the whole reduction (9 per 3x3 chunk + 1 per 1x1 chunk)
-  const bf16r* wt;        // pre-tiled main weights [ntc][nchunk1][9][KC][BCO][8]
-  const bf16r* wt2;       // pre-tiled 1x1 weights  [ntc][nchunk2][KC][BCO][8]
-  int depth, ncb, dsrc;   // 3-D (depth > 0): images are the N*depth output slices; main chunk = (depth tap
-                          // kz, 32-channel block cb) = kz*ncb + cb, reading logical input slice z + kz - 1
-                          // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
-                          // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
-  unsigned long long* tbuf;    // per-wave phase timestamps (compiled in only with -DFMD_HALO_TIME)
-  int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
-                               // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop,
-                               // 16 no SiLU' in the epilogue, 32 no statistics, 64 no side-tile loads
-};
+// HArgs: csrc/halo_args.h (shared with the v9 kernel, csrc/conv_halo9.hip)
 
 #ifdef FMD_HALO_DBG
 #define HDBG(bit) (A.dbg & (bit))
@@ -803,6 +784,10 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < g_halo_min_wg) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
+  {   // the v9 kernel (csrc/conv_halo9.hip) takes every problem it supports
+    const int rc9 = halo9_launch(A, pro, stream);
+    if (rc9 != 1) return rc9;
+  }
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);
   const dim3 blk(NT);
