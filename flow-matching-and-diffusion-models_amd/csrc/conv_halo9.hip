@@ -38,6 +38,10 @@ constexpr int NWSLOT = 3;              // weight ring slots (a tap reads slot t 
 constexpr int CMAX = 512;              // widest GN-prologue input of the affine table
 constexpr int OUT_TILE = TH * TW * BCO * 2;
 constexpr int ZFLAG = 1 << 30;         // staged-piece flag: store zeros (padding)
+#ifndef FMD_H9_SCHED
+#define FMD_H9_SCHED 1
+#endif
+constexpr bool H9_SCHED = FMD_H9_SCHED;   // v9b: pinned read/MFMA interleave of a tap (build flag for A/B)
 
 template <bool UP>
 struct G9 {
@@ -77,6 +81,14 @@ FMD_DEV void step_end(int keep) {
 
 FMD_DEV bf16x8 as_bf16x8(const u32x4& u) { return __builtin_bit_cast(bf16x8, u); }
 
+// debug ablations (A.dbg via fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG, tools/build_variant.sh):
+// 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop, 128 no step barrier, 256 no MFMA
+#ifdef FMD_HALO_DBG
+#define HDBG9(bit) (A.dbg & (bit))
+#else
+#define HDBG9(bit) false
+#endif
+
 // accumulator row pr (0..31) of pixel block pb of wave row-group wpx -> tile-local pixel index (y * 16 + x)
 FMD_DEV int pix_of(int wpx, int pb, int pr) {
   const int q = pr >> 4;
@@ -84,7 +96,9 @@ FMD_DEV int pix_of(int wpx, int pb, int pr) {
   return (8 * wpx + 2 * pb + q) * TW + cl;
 }
 
-template <bool UP, int PRO>
+// V: 1 = per-tap fragment reads (round-4 first version); 2 = software-pipelined step (A fragments of the next tap
+// prefetched under the current tap's MFMAs, branch-free staging interleaved with the MFMAs)
+template <bool UP, int PRO, int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9(const HArgs A) {
   using G = G9<UP>;
@@ -302,6 +316,61 @@ void conv3x3_halo9(const HArgs A) {
   };
   auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
 
+  // ---- V2 pieces: A fragments of one k-step of a tap, the B fragments of a ring slot, branch-free staging
+  constexpr int DUMMY = (G::HPOS + 2) * 16;   // plane-0 padding slot no fragment read touches: unstaged lanes' store
+  auto readA = [&](bf16x8 (&af)[4], int tap, int hb, int s) {
+    const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      const int off = UP ? hb + abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
+                         : hb + abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
+      af[pb] = *(const bf16x8*)(smem + off);
+    }
+  };
+  auto readB = [&](bf16x8 (&bw)[2][2], int ring) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) bw[s][cb] = *(const bf16x8*)(smem + bbase + ring * WTILE + s * 4096 + cb * 512);
+  };
+  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bw)[2]) {
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) acc[pb][cb] = mfma32(af[pb], bw[cb], acc[pb][cb]);
+  };
+  auto load_round2 = [&](int q) {
+    const int sp = q < NR ? spix[q] : -2;
+    const bool act = sseg2 ? q < 4 : sp != -2;
+    const bool valid = act && sok && (sseg2 || sp >= 0);
+    const int pix = sseg2 ? s2pix0 + 4 * q * d.Wo : simg + sp;
+    const int dst = sseg2 ? s2dst0 + q * 72 * 16 : sdst0 + q * 1024;
+    const bf16r* src = valid ? sbase + (size_t)pix * scs : s0;
+    rh[q & 1] = HDBG9(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
+    roff[q & 1] = !act ? DUMMY : (dst | (valid ? 0 : ZFLAG));
+  };
+  auto transform2 = [&](int q) -> u32x4 {   // the GN affine re-read from LDS (4 ds_read_b128): 16 VGPRs freed
+    const u32x4 raw = rh[q & 1];
+    u32x4 v = raw;
+    if (PRO != 0 && !HDBG9(2)) {
+      const f32x4 a0 = *(const f32x4*)(coef + scch), a1 = *(const f32x4*)(coef + scch + 4);
+      const f32x4 b0 = *(const f32x4*)(coef + A.C + scch), b1 = *(const f32x4*)(coef + A.C + scch + 4);
+      const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float qb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
+        float hi = bf_hi(raw[e]) * qa[2 * e + 1] + qb[2 * e + 1];
+        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
+        v[e] = sseg2 ? raw[e] : pack2(lo, hi);
+      }
+    }
+    const bool z = (roff[q & 1] & ZFLAG) != 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
+    return v;
+  };
+
   // ---- prologue: weights of steps 0 and 1, the whole first chunk staged
   __syncthreads();   // affine + epilogue tables
   dma(0, 0);
@@ -327,6 +396,40 @@ void conv3x3_halo9(const HArgs A) {
   step_end(0);
 
   // ---- 3x3 chunks: 9 unrolled taps; next chunk staged in rounds (load at tap q, transform + store at tap q + 2)
+  if constexpr (V == 2) {
+    bf16x8 af0[4];   // A fragments (k-step 0) of the current tap, prefetched during the previous tap
+    readA(af0, 0, (c_lo & 1) * HBUF, 0);
+    for (int chunk = c_lo; chunk < c_hi; ++chunk) {
+      const int nx = next_chunk(chunk);
+      setup(nx);
+      const int hb = (chunk & 1) * HBUF, nb = ((chunk + 1) & 1) * HBUF;
+      const int gc = (chunk - c_lo) * 9;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        bf16x8 bw[2][2], af1[4];
+        readB(bw, t % NWSLOT);
+        readA(af1, t, hb, 1);
+        const bool st = t >= 2 && t < NR + 2;
+        u32x4 sv;
+        int so = DUMMY;
+        if (st) {
+          sv = transform2(t - 2);
+          so = roff[t & 1] & ~ZFLAG;
+        }
+        if (!HDBG9(256)) mma(af0, bw[0]);
+        // next tap's k-step-0 fragments: this chunk's buffer, or at the last tap the next chunk's (its staging
+        // finished at tap NR + 1 < 8, before that step's barrier)
+        if (t < 8) readA(af0, t + 1, hb, 0);
+        else readA(af0, 0, nb, 0);
+        if (!HDBG9(256)) mma(af1, bw[1]);
+        if (st) *(u32x4*)(smem + nb + so) = sv;
+        if (!HDBG9(8)) dma(gc + t + 2, (t + 2) % NWSLOT);
+        if (t < NR) load_round2(t);
+        if (HDBG9(128)) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else step_end((t >= 1 && t - 1 < NR ? 1 : 0) + 2 + (t < NR ? 1 : 0));
+      }
+    }
+  } else
   for (int chunk = c_lo; chunk < c_hi; ++chunk) {
     const int nx = next_chunk(chunk);
     setup(nx);
@@ -370,6 +473,7 @@ void conv3x3_halo9(const HArgs A) {
     step_end(2);
   }
   step_end(0);   // every DMA landed (the tail re-fetches too) before the LDS is reused
+  if (HDBG9(4)) return;
 
   // ------------------------------------------------------------ epilogue
   const int K = d.K, Ho = d.Ho, Wo = d.Wo;
@@ -513,14 +617,428 @@ void conv3x3_halo9(const HArgs A) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// v9b: the same tile, staging and epilogue, with the weights taken straight from L2 into registers.
+//
+// Each wave owns one 32-cout quarter of the tile over all 256 pixels (8 pixel blocks of 2 rows = 8 accumulators);
+// its B fragments (32 couts x 32 channels of one tap, 2 KiB) are two 16-byte global loads per lane, issued one tap
+// ahead.  No LDS weight ring means no per-tap DMA and no per-tap barrier: the only workgroup barrier is at the chunk
+// boundary (the staged halo of the next chunk complete, the previous buffer free), so the four waves and the two
+// workgroups of a CU run their 9 taps independently.  Every load is an ordinary one, so hipcc counts all waits.
+template <bool UP, int PRO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void conv3x3_halo9b(const HArgs A) {
+  using G = G9<UP>;
+  constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
+  constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
+  constexpr int SM_EPI = SM_COEF + 2 * CMAX * 4;
+  constexpr int SM_BYTES = SM_EPI + 3 * BCO * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+  float* const coef = (float*)(smem + SM_COEF);
+  float* const epi = (float*)(smem + SM_EPI);
+
+  const fmd_conv_desc& d = A.d;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;   // wave = 32-cout quarter of the tile
+  const int r = lane & 31, hh = lane >> 5, rr = r >> 4;
+  const int col = rr ? ((r - 18) & 15) : r;
+
+  const int per_img = A.tiles_x * A.tiles_y;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tco = b % A.ntc;
+  const int tile = b / A.ntc;
+  const int n = tile / per_img;
+  const int tin = tile - n * per_img;
+  const int smp = A.depth ? n / A.depth : n;
+  const int zz = A.depth ? n - smp * A.depth : 0;
+  const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
+  const int co0 = tco * BCO;
+  const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;
+  const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
+  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
+  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
+  const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
+  const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
+
+  if (PRO != 0) {
+    for (int i = tid; i < 2 * A.C; i += NT9)
+      coef[i] = i < A.C ? d.pro_a[(size_t)smp * A.C + i] : d.pro_b[(size_t)smp * A.C + (i - A.C)];
+  }
+  if (tid < BCO) {
+    const int co = co0 + tid;
+    const bool ok = co < d.K;
+    float bsum = 0.f;
+    if (ok && d.bias) bsum += d.bias[co];
+    if (ok && d.bias2) bsum += d.bias2[co];
+    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)smp * d.K + co];
+    epi[tid] = bsum;
+    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)smp * d.K + co] : 0.f;
+    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)smp * d.K + co] : 0.f;
+  }
+
+  const int split = blockIdx.y;
+  const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
+  const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
+  const int T1 = A.nchunk1 * 9;
+
+  // ---- B fragments from global: slot sl (tap of the whole reduction) -> [plane 4][cout 128][8] bf16 tile
+  const unsigned char* const wt1 = (const unsigned char*)(A.wt + (size_t)tco * T1 * (WTILE / 2));
+  const unsigned char* const wt2b = (const unsigned char*)(A.wt2 + (size_t)tco * A.nchunk2 * (WTILE / 2));
+  const int boff = (hh * BCO + 32 * wid + r) * 16;   // this lane's 16 bytes of k-step 0 (k-step 1: + 4096)
+  auto loadB = [&](bf16x8 (&bq)[2], int sl) {
+    const unsigned char* base = sl < T1 ? wt1 + (size_t)sl * WTILE : wt2b + (size_t)(sl - T1) * WTILE;
+    bq[0] = *(const bf16x8*)(base + boff);
+    bq[1] = *(const bf16x8*)(base + boff + 4096);
+  };
+
+  // ---- halo staging (as v9)
+  const int kc = (tid >> 3) & (KC - 1);
+  const int p0 = (tid >> 5) * 8 + (tid & 7);
+  int spix[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    const int pos = q * 64 + p0;
+    const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
+    const int y = hy0 + py, x = hx0 + px;
+    spix[q] = pos >= G::HPOS ? -2 : (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? y * d.Ws + x : -1;
+  }
+  const int sdst0 = (kc * HPAD + p0) * 16;
+  const int s2pix0 = (n * d.Ho + ty0 + (p0 >> 4)) * d.Wo + tx0 + (p0 & 15);
+  const int s2dst0 = (kc * HPAD + ((p0 >> 4) + 1) * (TW + 2) + (p0 & 15) + 1) * 16;
+  const int HWs = d.Hs * d.Ws;
+  constexpr int DUMMY = (G::HPOS + 2) * 16;
+  const bf16r* sbase = s0;
+  int scs = 0, simg = 0, scch = 0;
+  bool sok = false, sseg2 = false;
+  auto setup = [&](int chunk) {
+    sseg2 = chunk >= A.nchunk1;
+    if (chunk < 0) {
+      sok = false; sbase = s0; scs = 0; simg = 0; scch = 0;
+    } else if (!sseg2) {
+      int cb = chunk;
+      bool zok = true;
+      int sl = n;
+      if (A.depth) {
+        const int kz = chunk / A.ncb;
+        cb = chunk - kz * A.ncb;
+        const int zl = zz + kz - 1;
+        zok = zl >= 0 && zl < A.depth;
+        sl = smp * A.dsrc + (UP ? zl >> 1 : zl);
+      }
+      const int c = cb * BK + kc * 8;
+      sok = c < A.C && zok;
+      sbase = !sok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
+      scs = (c < d.C0) ? d.C0 : d.C1;
+      simg = sl * HWs;
+      scch = sok ? c : 0;
+    } else {
+      const int c = (chunk - A.nchunk1) * BK + kc * 8;
+      sok = c < A.C23;
+      sbase = !sok ? s2 : (c < d.C2) ? s2 + c : s3 + (c - d.C2);
+      scs = (c < d.C2) ? d.C2 : d.C3;
+      simg = 0;
+      scch = 0;
+    }
+  };
+  u32x4 rh[2];
+  int roff[2];
+  auto load_round = [&](int q) {
+    const int sp = q < NR ? spix[q] : -2;
+    const bool act = sseg2 ? q < 4 : sp != -2;
+    const bool valid = act && sok && (sseg2 || sp >= 0);
+    const int pix = sseg2 ? s2pix0 + 4 * q * d.Wo : simg + sp;
+    const int dst = sseg2 ? s2dst0 + q * 72 * 16 : sdst0 + q * 1024;
+    const bf16r* src = valid ? sbase + (size_t)pix * scs : s0;
+    rh[q & 1] = *(const u32x4*)src;
+    roff[q & 1] = !act ? DUMMY : (dst | (valid ? 0 : ZFLAG));
+  };
+  auto transform = [&](int q) -> u32x4 {
+    const u32x4 raw = rh[q & 1];
+    u32x4 v = raw;
+    if (PRO != 0) {
+      const f32x4 a0 = *(const f32x4*)(coef + scch), a1 = *(const f32x4*)(coef + scch + 4);
+      const f32x4 b0 = *(const f32x4*)(coef + A.C + scch), b1 = *(const f32x4*)(coef + A.C + scch + 4);
+      const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const float qb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
+        float hi = bf_hi(raw[e]) * qa[2 * e + 1] + qb[2 * e + 1];
+        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
+        v[e] = sseg2 ? raw[e] : pack2(lo, hi);
+      }
+    }
+    const bool z = (roff[q & 1] & ZFLAG) != 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
+    return v;
+  };
+
+  // ---- A fragments: 8 pixel blocks of the wave (rows 2pb, 2pb+1), one k-step of a tap
+  int abase;
+  int uo[9];
+  if constexpr (UP) {
+    abase = (hh * HPAD + HROW + 1) * 16;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t % 3;
+      uo[t] = (((rr + ky - 1) >> 1) * HROW + ((col + kx - 1) >> 1)) * 16;
+    }
+  } else {
+    abase = (hh * HPAD + rr * HROW + col) * 16;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) uo[t] = 0;
+  }
+  auto aoff = [&](int tap, int s, int pb) {
+    const int ky = tap / 3, kx = tap % 3;
+    return UP ? abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
+              : abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int pb = 0; pb < 8; ++pb)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[pb][e] = 0.f;
+
+  // one tap: 8 pixel blocks x 2 k-steps = 16 MFMAs.  The 16 A-fragment reads are software-pipelined four
+  // groups ahead of their MFMAs (sched_group_barrier: 8 reads, then 4 MFMAs + 4 reads per group), so each group's
+  // LDS latency hides under the previous group's 4 x 32 MFMA cycles instead of every MFMA waiting on its read
+  auto tap_mma = [&](int tap, int hb, const bf16x8 (&bq)[2]) {
+    bf16x8 af[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[4 * g + i] = *(const bf16x8*)(smem + hb + aoff(tap, g >> 1, 4 * (g & 1) + i));
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[4 * (g & 1) + i] = mfma32(af[4 * g + i], bq[g >> 1], acc[4 * (g & 1) + i]);
+    if constexpr (H9_SCHED) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+  };
+  auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
+
+  // ---- prologue: first chunk staged whole; B of its tap 0 in flight
+  __syncthreads();   // affine + epilogue tables
+  bf16x8 bq[2][2];
+  loadB(bq[0], c_lo * 9);
+  setup(c_lo);
+  {
+    u32x4 pv[NR];
+    int po[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      load_round(q);
+      pv[q] = rh[q & 1];
+      po[q] = roff[q & 1];
+    }
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      rh[q & 1] = pv[q];
+      roff[q & 1] = po[q];
+      const u32x4 v = transform(q);
+      *(u32x4*)(smem + (c_lo & 1) * HBUF + (roff[q & 1] & ~ZFLAG)) = v;
+    }
+  }
+  __syncthreads();
+
+  for (int chunk = c_lo; chunk < c_hi; ++chunk) {
+    const int nx = next_chunk(chunk);
+    setup(nx);
+    const int hb = (chunk & 1) * HBUF, nb = ((chunk + 1) & 1) * HBUF;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // B of the next tap (next chunk's tap 0 / first 1x1 slot at the last tap; a re-load past the end)
+      const int nsl = t < 8 ? chunk * 9 + t + 1 : (nx < 0 ? chunk * 9 + t : nx < A.nchunk1 ? nx * 9 : T1);
+      loadB(bq[(t + 1) & 1], nsl);
+      if (t < NR) load_round(t);
+      if (t >= 2 && t < NR + 2) {
+        const u32x4 v = transform(t - 2);
+        *(u32x4*)(smem + nb + (roff[t & 1] & ~ZFLAG)) = v;
+      }
+      tap_mma(t, hb, bq[t & 1]);
+    }
+    // chunk boundary: the next chunk's halo complete, this chunk's buffer free
+    __syncthreads();
+    // bq parity: 9 taps per chunk flip it; keep tap 0 of the next chunk in bq[0]
+    bq[0][0] = bq[1][0];
+    bq[0][1] = bq[1][1];
+  }
+
+  // ---- 1x1 chunks: one tap each; the next chunk loaded whole; B of the next slot one step ahead
+  for (int i = 0; i < n_seg2; ++i) {
+    const int ch = A.nchunk1 + i;
+    const bool more = i + 1 < n_seg2;
+    setup(more ? ch + 1 : -1);
+    loadB(bq[1], T1 + (more ? i + 1 : i));
+    u32x4 sv[4];
+    int so[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool valid = more && sok;
+      const bf16r* src = valid ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2;
+      sv[q] = *(const u32x4*)src;
+      so[q] = !more ? DUMMY : (s2dst0 + q * 72 * 16) | (valid ? 0 : ZFLAG);
+    }
+    tap_mma(4, (ch & 1) * HBUF, bq[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      u32x4 v = sv[q];
+      if (so[q] & ZFLAG) v = u32x4{0u, 0u, 0u, 0u};
+      *(u32x4*)(smem + ((ch + 1) & 1) * HBUF + (so[q] & ~ZFLAG)) = v;
+    }
+    __syncthreads();
+    bq[0][0] = bq[1][0];
+    bq[0][1] = bq[1][1];
+  }
+
+  // ------------------------------------------------------------ epilogue (layout of v9; wave = cout quarter)
+  const int K = d.K, Ho = d.Ho, Wo = d.Wo;
+  auto pixl = [&](int pb, int pr) {
+    const int q = pr >> 4;
+    const int cl = q ? ((pr - 18) & 15) : pr;
+    return (2 * pb + q) * TW + cl;
+  };
+  if (A.splits > 1) {
+    float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
+    const int co = co0 + 32 * wid + r;
+    if (co < K) {
+#pragma unroll
+      for (int pb = 0; pb < 8; ++pb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int pi = pixl(pb, (e & 3) + 8 * (e >> 2) + 4 * hh);
+          const size_t p = ((size_t)n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+          ws[p * K + co] = acc[pb][e];
+        }
+    }
+    return;
+  }
+  unsigned char* const tileb = smem;
+  const bool hasx = d.ep_x0 != nullptr;
+  const bool dep = d.ep_a != nullptr;
+  const bool side = d.resid != nullptr || hasx;
+  const bool stats = d.stats != nullptr;
+  if (side) {
+    constexpr int SK = TH * TW * BCO / 8 / NT9;
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
+      const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+      const int c = co0 + c16 * 8;
+      const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
+                         : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
+                                         : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
+      *(u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16)) = *(const u32x4*)src;
+    }
+    __syncthreads();
+  }
+  bf16x8 inat[2], iperm[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      inat[s][j] = (__bf16)((16 * s + 8 * hh + j) == r ? 1.0f : 0.0f);
+      iperm[s][j] = (__bf16)((16 * s + 8 * (j >> 2) + 4 * hh + (j & 3)) == r ? 1.0f : 0.0f);
+    }
+  const int cl = 32 * wid;
+  const float bias = epi[cl + r];
+  const float ea = epi[BCO + cl + r], eb = epi[2 * BCO + cl + r];
+  float st1 = 0.f, st2 = 0.f;
+#pragma unroll
+  for (int pb = 0; pb < 8; ++pb) {
+    const int pi_l = pixl(pb, r);
+    f32x16 v = acc[pb];
+    f32x16 xc;
+    if (side) {
+      bf16x8 fr[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int c = cl + 16 * s + 8 * hh;
+        fr[s] = *(const bf16x8*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16));
+      }
+      if (d.resid) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) v = mfma32(fr[s], inat[s], v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) xc[e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) xc = mfma32(fr[s], inat[s], xc);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] += bias;
+    if (hasx && dep) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] *= silu_grad(ea * xc[e] + eb);
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = pack2(v[8 * s + 2 * e], v[8 * s + 2 * e + 1]);
+      pf[s] = as_bf16x8(u);
+      if (stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float w0 = bf_lo(u[e]), w1 = bf_hi(u[e]);
+          st1 += w0 + w1;
+          st2 += hasx ? w0 * xc[8 * s + 2 * e] + w1 * xc[8 * s + 2 * e + 1] : w0 * w0 + w1 * w1;
+        }
+      }
+    }
+    f32x16 z;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) z[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) z = mfma32(pf[s], iperm[s], z);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = cl + 8 * g + 4 * hh;
+      u32x2 o;
+      o[0] = pack2(z[4 * g], z[4 * g + 1]);
+      o[1] = pack2(z[4 * g + 2], z[4 * g + 3]);
+      *(u32x2*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16) + (c & 7) * 2) = o;
+    }
+    if (stats && (pb & 1)) {   // one statistics row per 64 pixels (= pixel blocks 2k, 2k+1: 4 tile rows)
+      const int srow = tile * 4 + (pb >> 1);
+      const float a = st1 + __shfl_xor(st1, 32, 64);
+      const float q = st2 + __shfl_xor(st2, 32, 64);
+      if (hh == 0) {
+        float* sp = d.stats + ((size_t)srow * K + co0 + cl + r) * 2;
+        sp[0] = a;
+        sp[1] = q;
+      }
+      st1 = 0.f;
+      st2 = 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < TH * TW * BCO / 8 / NT9; ++k) {
+    const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
+    const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+    *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) = *(const u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16));
+  }
+}
+
 }  // namespace
 
-static int g_halo9 = -1;   // FMD_HALO9=0 keeps every problem on the round-3 kernel (A/B runs)
+static int g_halo9 = -1;   // FMD_HALO9: 0 = round-3 kernel for every problem, 1 = v9, 2 = v9 pipelined, else v9b
 
 int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   if (g_halo9 < 0) {
     const char* e = getenv("FMD_HALO9");
-    g_halo9 = (e && *e == '0') ? 0 : 1;
+    g_halo9 = (e && *e) ? atoi(e) : 3;
   }
   const fmd_conv_desc* d = &A.d;
   if (!g_halo9 || d->gout) return 1;
@@ -531,14 +1049,29 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const dim3 g(nwg, A.splits);
   const dim3 blk(NT9);
   hipStream_t st = (hipStream_t)stream;
-  if (d->upsample) {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<true, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<true, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo9<true, 0>), g, blk, 0, st, A);
+#define H9_LAUNCH(V)                                                                        \
+  do {                                                                                      \
+    if (d->upsample) {                                                                      \
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<true, 2, V>), g, blk, 0, st, A);      \
+      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<true, 1, V>), g, blk, 0, st, A); \
+      else hipLaunchKernelGGL((conv3x3_halo9<true, 0, V>), g, blk, 0, st, A);               \
+    } else {                                                                                \
+      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<false, 2, V>), g, blk, 0, st, A);     \
+      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<false, 1, V>), g, blk, 0, st, A);\
+      else hipLaunchKernelGGL((conv3x3_halo9<false, 0, V>), g, blk, 0, st, A);              \
+    }                                                                                       \
+  } while (0)
+  if (g_halo9 == 1) H9_LAUNCH(1);
+  else if (g_halo9 == 2) H9_LAUNCH(2);
+  else if (d->upsample) {
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<true, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<true, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo9b<true, 0>), g, blk, 0, st, A);
   } else {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<false, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<false, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo9<false, 0>), g, blk, 0, st, A);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo9b<false, 0>), g, blk, 0, st, A);
   }
+#undef H9_LAUNCH
   return (int)hipGetLastError();
 }

@@ -457,6 +457,10 @@ WGRAD_CU_MULT = int(os.environ.get("FMD_WGRAD_CU_MULT", "4"))
 # workgroups the halo weight gradient aims for (one per CU); fewer means fewer pixel splits, i.e. smaller
 # split-K slabs (their write + reduce read) at the small levels (FMD_WGRAD_HALO_WG: A/B override)
 WGRAD_HALO_WG = int(os.environ.get("FMD_WGRAD_HALO_WG", "0") or 0) or NUM_CU
+# split-K slab caps (MB): the partial slabs' write + reduce read bound the small levels (A/B: FMD_WGRAD_SLAB_MB,
+# FMD_WGRAD_GEN_SLAB_MB)
+WGRAD_SLAB_MB = int(os.environ.get("FMD_WGRAD_SLAB_MB", "96") or 96)
+WGRAD_GEN_SLAB_MB = int(os.environ.get("FMD_WGRAD_GEN_SLAB_MB", "48") or 48)
 
 
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
@@ -512,7 +516,7 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             zt = 3 if d3 else 1
             tiles = N * max(Do, 1) * (Ho // 8) * (Wo // 16)
             base = (K // 128) * (Ct // 64) * zt
-            splits = max(1, min(tiles, -(-WGRAD_HALO_WG // base), (96 << 20) // (K * Ct * 36 * zt)))
+            splits = max(1, min(tiles, -(-WGRAD_HALO_WG // base), (WGRAD_SLAB_MB << 20) // (K * Ct * 36 * zt)))
         else:
             # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
             T = ks * ks * (ks if d3 else 1)
@@ -520,7 +524,7 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             steps = -(-M // 32)
             # up to WGRAD_CU_MULT workgroups per CU (the kernel is latency-bound at one), >= WGRAD_MIN_STEPS
             # 32-pixel steps per split, partial slabs <= 48 MB
-            cap = max(256, min(1024, (48 << 20) // (K * Ct * T * 4)))
+            cap = max(256, min(1024, (WGRAD_GEN_SLAB_MB << 20) // (K * Ct * T * 4)))
             splits = max(1, min(steps // WGRAD_MIN_STEPS, -(-WGRAD_CU_MULT * NUM_CU // tiles), cap))
     d.splits = splits
     ws = torch.empty((int(_lib.lib().fmd_wgrad_workspace(C.byref(d))),), device=dy.device, dtype=F32)
