@@ -858,11 +858,12 @@ void conv3x3_halo9b(const HArgs A) {
       // B of the next tap (next chunk's tap 0 / first 1x1 slot at the last tap; a re-load past the end)
       const int nsl = t < 8 ? chunk * 9 + t + 1 : (nx < 0 ? chunk * 9 + t : nx < A.nchunk1 ? nx * 9 : T1);
       loadB(bq[(t + 1) & 1], nsl);
-      if (t < NR) load_round(t);
+      // round t - 2 leaves its register slot before round t lands in it
       if (t >= 2 && t < NR + 2) {
         const u32x4 v = transform(t - 2);
         *(u32x4*)(smem + nb + (roff[t & 1] & ~ZFLAG)) = v;
       }
+      if (t < NR) load_round(t);
       tap_mma(t, hb, bq[t & 1]);
     }
     // chunk boundary: the next chunk's halo complete, this chunk's buffer free

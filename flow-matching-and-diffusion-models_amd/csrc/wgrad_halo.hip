@@ -506,10 +506,10 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int nwg = A.ntc * A.nci * A.splits;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
-  static int w9 = -1;   // FMD_WGRAD9=0: the round-3 kernel (A/B runs)
+  static int w9 = -1;   // FMD_WGRAD9=1: the 32x32x16 kernel (measured slower than the round-3 one: off by default)
   if (w9 < 0) {
     const char* e = getenv("FMD_WGRAD9");
-    w9 = (e && *e == '0') ? 0 : 1;
+    w9 = (e && *e) ? atoi(e) : 0;
   }
   if (w9) {
     if (pro == 2) hipLaunchKernelGGL(wgrad_halo9_kernel<2>, dim3(nwg), dim3(W9NT), 0, st, A);

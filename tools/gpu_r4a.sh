@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "halo or conv or wgrad" > gpurun_out/r4a_kernels.log 2>&1
 rc=$?; echo "kernel tests rc=$rc"; tail -2 gpurun_out/r4a_kernels.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
-  for arm in "FMD_HALO9=0 FMD_WGRAD9=0" "FMD_HALO9=2 FMD_WGRAD9=1" "FMD_HALO9=3 FMD_WGRAD9=1"; do
+  for arm in "FMD_HALO9=1 FMD_WGRAD9=0" "FMD_HALO9=3 FMD_WGRAD9=1"; do
     env $arm timeout -k 10 120 python -u tools/conv_micro.py --only fwd,dgrad,cat,wgrad --iters 50 > gpurun_out/r4a_micro.txt 2>&1
     rc=$?; echo "micro [$arm] rc=$rc"; grep -v amdgpu.ids gpurun_out/r4a_micro.txt; [ $rc -eq 0 ] || exit $rc
   done
