@@ -632,7 +632,8 @@ void conv3x3_halo9b(const HArgs A) {
   using G = G9<UP>;
   constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
   constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
-  constexpr int SM_EPI = SM_COEF + 2 * CMAX * 4;
+  constexpr int ZCOEF = 2 * CMAX;   // 8 zero coefficients: the affine of a chunk's invalid channels (-> SiLU(0) = 0)
+  constexpr int SM_EPI = SM_COEF + (2 * CMAX + 8) * 4;
   constexpr int SM_BYTES = SM_EPI + 3 * BCO * 4;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
   float* const coef = (float*)(smem + SM_COEF);
@@ -663,6 +664,7 @@ void conv3x3_halo9b(const HArgs A) {
   if (PRO != 0) {
     for (int i = tid; i < 2 * A.C; i += NT9)
       coef[i] = i < A.C ? d.pro_a[(size_t)smp * A.C + i] : d.pro_b[(size_t)smp * A.C + (i - A.C)];
+    if (tid < 8) coef[ZCOEF + tid] = 0.f;
   }
   if (tid < BCO) {
     const int co = co0 + tid;
@@ -708,12 +710,12 @@ void conv3x3_halo9b(const HArgs A) {
   const int HWs = d.Hs * d.Ws;
   constexpr int DUMMY = (G::HPOS + 2) * 16;
   const bf16r* sbase = s0;
-  int scs = 0, simg = 0, scch = 0;
+  int scs = 0, simg = 0, sca = 0, scb = 0;
   bool sok = false, sseg2 = false;
   auto setup = [&](int chunk) {
     sseg2 = chunk >= A.nchunk1;
     if (chunk < 0) {
-      sok = false; sbase = s0; scs = 0; simg = 0; scch = 0;
+      sok = false; sbase = s0; scs = 0; simg = 0; sca = ZCOEF; scb = ZCOEF;
     } else if (!sseg2) {
       int cb = chunk;
       bool zok = true;
@@ -730,34 +732,37 @@ void conv3x3_halo9b(const HArgs A) {
       sbase = !sok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
       scs = (c < d.C0) ? d.C0 : d.C1;
       simg = sl * HWs;
-      scch = sok ? c : 0;
+      sca = sok ? c : ZCOEF;
+      scb = sok ? A.C + c : ZCOEF;
     } else {
       const int c = (chunk - A.nchunk1) * BK + kc * 8;
       sok = c < A.C23;
       sbase = !sok ? s2 : (c < d.C2) ? s2 + c : s3 + (c - d.C2);
       scs = (c < d.C2) ? d.C2 : d.C3;
       simg = 0;
-      scch = 0;
+      sca = ZCOEF;
+      scb = ZCOEF;
     }
   };
   u32x4 rh[2];
   int roff[2];
+  // staging round q of a 3x3 chunk (1x1 chunks: stage_seg2)
   auto load_round = [&](int q) {
-    const int sp = q < NR ? spix[q] : -2;
-    const bool act = sseg2 ? q < 4 : sp != -2;
-    const bool valid = act && sok && (sseg2 || sp >= 0);
-    const int pix = sseg2 ? s2pix0 + 4 * q * d.Wo : simg + sp;
-    const int dst = sseg2 ? s2dst0 + q * 72 * 16 : sdst0 + q * 1024;
-    const bf16r* src = valid ? sbase + (size_t)pix * scs : s0;
+    const int sp = spix[q];
+    const bool valid = sok && sp >= 0;
+    const bf16r* src = valid ? sbase + (size_t)(simg + sp) * scs : s0;
     rh[q & 1] = *(const u32x4*)src;
-    roff[q & 1] = !act ? DUMMY : (dst | (valid ? 0 : ZFLAG));
+    // GN prologue: padding positions were zeroed once (their store goes to the dummy slot) and invalid channels /
+    // depth slices meet zero coefficients, so the transform needs no select
+    const int dst = sdst0 + q * 1024;
+    roff[q & 1] = sp == -2 ? DUMMY : PRO != 0 ? (sp >= 0 ? dst : DUMMY) : (dst | (valid ? 0 : ZFLAG));
   };
   auto transform = [&](int q) -> u32x4 {
     const u32x4 raw = rh[q & 1];
     u32x4 v = raw;
     if (PRO != 0) {
-      const f32x4 a0 = *(const f32x4*)(coef + scch), a1 = *(const f32x4*)(coef + scch + 4);
-      const f32x4 b0 = *(const f32x4*)(coef + A.C + scch), b1 = *(const f32x4*)(coef + A.C + scch + 4);
+      const f32x4 a0 = *(const f32x4*)(coef + sca), a1 = *(const f32x4*)(coef + sca + 4);
+      const f32x4 b0 = *(const f32x4*)(coef + scb), b1 = *(const f32x4*)(coef + scb + 4);
       const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       const float qb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 #pragma unroll
@@ -765,12 +770,13 @@ void conv3x3_halo9b(const HArgs A) {
         float lo = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
         float hi = bf_hi(raw[e]) * qa[2 * e + 1] + qb[2 * e + 1];
         if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-        v[e] = sseg2 ? raw[e] : pack2(lo, hi);
+        v[e] = pack2(lo, hi);
       }
-    }
-    const bool z = (roff[q & 1] & ZFLAG) != 0;
+    } else {
+      const bool z = (roff[q & 1] & ZFLAG) != 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
+      for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
+    }
     return v;
   };
 
@@ -824,13 +830,39 @@ void conv3x3_halo9b(const HArgs A) {
     }
   };
   auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
+  // a 1x1 chunk (raw src2 | src3 at the tile's own pixels) staged whole into buffer byte offset buf
+  auto stage_seg2 = [&](int ch, int buf) {
+    setup(ch);
+    u32x4 sv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sv[q] = *(const u32x4*)(sok ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *(u32x4*)(smem + buf + s2dst0 + q * 72 * 16) = sok ? sv[q] : u32x4{0u, 0u, 0u, 0u};
+  };
 
-  // ---- prologue: first chunk staged whole; B of its tap 0 in flight
+  // ---- prologue: padding positions of both halo buffers zeroed (fixed for the tile); first chunk staged whole;
+  // B of its tap 0 in flight
+#pragma unroll
+  for (int q = 0; q < NR; ++q)
+    if (spix[q] == -1) {
+      *(u32x4*)(smem + sdst0 + q * 1024) = u32x4{0u, 0u, 0u, 0u};
+      *(u32x4*)(smem + HBUF + sdst0 + q * 1024) = u32x4{0u, 0u, 0u, 0u};
+    }
   __syncthreads();   // affine + epilogue tables
+  if (A.splits <= 1) {   // the summed bias is the accumulators' start value
+    const float bv = epi[32 * wid + r];
+#pragma unroll
+    for (int pb = 0; pb < 8; ++pb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[pb][e] = bv;
+  }
   bf16x8 bq[2][2];
-  loadB(bq[0], c_lo * 9);
-  setup(c_lo);
-  {
+  loadB(bq[0], c_lo < c_hi ? c_lo * 9 : T1);
+  if (c_lo >= c_hi) {
+    if (n_seg2) stage_seg2(A.nchunk1, (A.nchunk1 & 1) * HBUF);
+  } else {
+    setup(c_lo);
     u32x4 pv[NR];
     int po[NR];
 #pragma unroll
@@ -851,19 +883,20 @@ void conv3x3_halo9b(const HArgs A) {
 
   for (int chunk = c_lo; chunk < c_hi; ++chunk) {
     const int nx = next_chunk(chunk);
-    setup(nx);
     const int hb = (chunk & 1) * HBUF, nb = ((chunk + 1) & 1) * HBUF;
+    // next chunk a 3x3 one: staged in rounds under this chunk's taps (the 1x1 segment's first chunk is staged
+    // whole after the loop); B of the next chunk's tap 0 / the first 1x1 slot at the last tap
+    const bool stg = nx >= 0 && nx < A.nchunk1;
+    if (stg) setup(nx);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      // B of the next tap (next chunk's tap 0 / first 1x1 slot at the last tap; a re-load past the end)
-      const int nsl = t < 8 ? chunk * 9 + t + 1 : (nx < 0 ? chunk * 9 + t : nx < A.nchunk1 ? nx * 9 : T1);
-      loadB(bq[(t + 1) & 1], nsl);
+      loadB(bq[(t + 1) & 1], t < 8 ? chunk * 9 + t + 1 : stg ? nx * 9 : nx < 0 ? chunk * 9 + t : T1);
       // round t - 2 leaves its register slot before round t lands in it
-      if (t >= 2 && t < NR + 2) {
+      if (stg && t >= 2 && t < NR + 2) {
         const u32x4 v = transform(t - 2);
         *(u32x4*)(smem + nb + (roff[t & 1] & ~ZFLAG)) = v;
       }
-      if (t < NR) load_round(t);
+      if (stg && t < NR) load_round(t);
       tap_mma(t, hb, bq[t & 1]);
     }
     // chunk boundary: the next chunk's halo complete, this chunk's buffer free
@@ -871,6 +904,10 @@ void conv3x3_halo9b(const HArgs A) {
     // bq parity: 9 taps per chunk flip it; keep tap 0 of the next chunk in bq[0]
     bq[0][0] = bq[1][0];
     bq[0][1] = bq[1][1];
+  }
+  if (c_lo < c_hi && n_seg2) {   // first 1x1 chunk, staged whole after the 3x3 chunks (its buffer is free)
+    stage_seg2(A.nchunk1, (A.nchunk1 & 1) * HBUF);
+    __syncthreads();
   }
 
   // ---- 1x1 chunks: one tap each; the next chunk loaded whole; B of the next slot one step ahead
@@ -950,7 +987,6 @@ void conv3x3_halo9b(const HArgs A) {
       iperm[s][j] = (__bf16)((16 * s + 8 * (j >> 2) + 4 * hh + (j & 3)) == r ? 1.0f : 0.0f);
     }
   const int cl = 32 * wid;
-  const float bias = epi[cl + r];
   const float ea = epi[BCO + cl + r], eb = epi[2 * BCO + cl + r];
   float st1 = 0.f, st2 = 0.f;
 #pragma unroll
@@ -975,8 +1011,6 @@ void conv3x3_halo9b(const HArgs A) {
         for (int s = 0; s < 2; ++s) xc = mfma32(fr[s], inat[s], xc);
       }
     }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) v[e] += bias;
     if (hasx && dep) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] *= silu_grad(ea * xc[e] + eb);

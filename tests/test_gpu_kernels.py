@@ -1098,8 +1098,8 @@ def test_adamw_sched_matches_torch_with_cosine_warmup(n, offset):
 @pytest.mark.parametrize("case", ["plain", "concat", "upsample", "split", "affine", "d3", "d3_up"])
 def test_halo_conv_gout_side_output(case):
     """fmd_conv_desc.gout: the halo kernel copies its prologue's output G = SiLU(a*x+b) (or the affine alone)
-    for the tile's own pixels out of each staged halo image.  Checks: (1) the conv output is bit-identical
-    with and without the side output; (2) every element of G is written (NaN-filled beforehand) and equals
+    for the tile's own pixels out of each staged halo image.  Checks: (1) the conv output agrees with the
+    plain call's (another kernel generation: within a bf16 step); (2) every element of G is written (NaN-filled beforehand) and equals
     the fp32 torch transform rounded to bf16 within one bf16 ulp (the kernel's SiLU uses v_exp / v_rcp);
     (3) the weight gradient from G (no prologue) is bit-identical to the one that recomputes GN + SiLU."""
     O = ops()
@@ -1136,7 +1136,9 @@ def test_halo_conv_gout_side_output(case):
     gout = torch.full((*x0.shape[:-1], Ct), float("nan"), device=DEV, dtype=torch.bfloat16)
     y0, _ = O.conv(x0, K, None, **kw)
     y1, _ = O.conv(x0, K, None, gout=gout, **kw)
-    assert torch.equal(y0, y1), "the side output changed the conv result"
+    # a gout call runs the round-3 halo kernel, a plain one the v9 kernel (bias as the accumulators' start value):
+    # equal up to fp32 summation order, i.e. within a bf16 step
+    torch.testing.assert_close(y1.float(), y0.float(), rtol=1e-2, atol=1e-2 * y0.float().abs().max().item())
     xf = torch.cat([x0, x1], -1).float() if x1 is not None else x0.float()
     shp = (N,) + (1,) * (xf.dim() - 2) + (Ct,)
     z = xf * a.view(shp) + b.view(shp)
