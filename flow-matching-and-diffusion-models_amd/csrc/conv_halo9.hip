@@ -751,7 +751,7 @@ void conv3x3_halo9b(const HArgs A) {
     const int sp = spix[q];
     const bool valid = sok && sp >= 0;
     const bf16r* src = valid ? sbase + (size_t)(simg + sp) * scs : s0;
-    rh[q & 1] = *(const u32x4*)src;
+    rh[q & 1] = HDBG9(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
     // GN prologue: padding positions were zeroed once (their store goes to the dummy slot) and invalid channels /
     // depth slices meet zero coefficients, so the transform needs no select
     const int dst = sdst0 + q * 1024;
@@ -760,7 +760,7 @@ void conv3x3_halo9b(const HArgs A) {
   auto transform = [&](int q) -> u32x4 {
     const u32x4 raw = rh[q & 1];
     u32x4 v = raw;
-    if (PRO != 0) {
+    if (PRO != 0 && !HDBG9(2)) {
       const f32x4 a0 = *(const f32x4*)(coef + sca), a1 = *(const f32x4*)(coef + sca + 4);
       const f32x4 b0 = *(const f32x4*)(coef + scb), b1 = *(const f32x4*)(coef + scb + 4);
       const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
@@ -857,8 +857,17 @@ void conv3x3_halo9b(const HArgs A) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[pb][e] = bv;
   }
-  bf16x8 bq[2][2];
-  loadB(bq[0], c_lo < c_hi ? c_lo * 9 : T1);
+  // B fragments three slots deep: the load of slot g + 2 is issued at slot g, two taps (about 2,000 cycles with
+  // the partner wave) ahead of its MFMAs -- one tap did not cover an L2 hit under load
+  bf16x8 bq[3][2];
+  const int last2 = T1 + n_seg2 - 1;   // last 1x1 slot of this split (when n_seg2 > 0)
+  if (c_lo < c_hi) {
+    loadB(bq[0], c_lo * 9);
+    loadB(bq[1], c_lo * 9 + 1);
+  } else {
+    loadB(bq[0], T1);
+    loadB(bq[1], min(T1 + 1, last2));
+  }
   if (c_lo >= c_hi) {
     if (n_seg2) stage_seg2(A.nchunk1, (A.nchunk1 & 1) * HBUF);
   } else {
@@ -890,20 +899,20 @@ void conv3x3_halo9b(const HArgs A) {
     if (stg) setup(nx);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      loadB(bq[(t + 1) & 1], t < 8 ? chunk * 9 + t + 1 : stg ? nx * 9 : nx < 0 ? chunk * 9 + t : T1);
+      // slot of tap t + 2: this chunk, the next 3x3 chunk's taps 0 / 1, the first 1x1 slots, or a re-load
+      const int s2 = t < 7 ? chunk * 9 + t + 2 : stg ? nx * 9 + t - 7 : nx < 0 ? chunk * 9 + t : min(T1 + t - 7, last2);
+      if (!HDBG9(8)) loadB(bq[(t + 2) % 3], s2);
       // round t - 2 leaves its register slot before round t lands in it
       if (stg && t >= 2 && t < NR + 2) {
         const u32x4 v = transform(t - 2);
         *(u32x4*)(smem + nb + (roff[t & 1] & ~ZFLAG)) = v;
       }
       if (stg && t < NR) load_round(t);
-      tap_mma(t, hb, bq[t & 1]);
+      if (!HDBG9(256)) tap_mma(t, hb, bq[t % 3]);
     }
-    // chunk boundary: the next chunk's halo complete, this chunk's buffer free
+    // chunk boundary: the next chunk's halo complete, this chunk's buffer free (9 taps: the B ring's phase is
+    // the same at every chunk start)
     __syncthreads();
-    // bq parity: 9 taps per chunk flip it; keep tap 0 of the next chunk in bq[0]
-    bq[0][0] = bq[1][0];
-    bq[0][1] = bq[1][1];
   }
   if (c_lo < c_hi && n_seg2) {   // first 1x1 chunk, staged whole after the 3x3 chunks (its buffer is free)
     stage_seg2(A.nchunk1, (A.nchunk1 & 1) * HBUF);
@@ -915,7 +924,7 @@ void conv3x3_halo9b(const HArgs A) {
     const int ch = A.nchunk1 + i;
     const bool more = i + 1 < n_seg2;
     setup(more ? ch + 1 : -1);
-    loadB(bq[1], T1 + (more ? i + 1 : i));
+    loadB(bq[2], min(T1 + i + 2, last2));
     u32x4 sv[4];
     int so[4];
 #pragma unroll
@@ -933,10 +942,14 @@ void conv3x3_halo9b(const HArgs A) {
       *(u32x4*)(smem + ((ch + 1) & 1) * HBUF + (so[q] & ~ZFLAG)) = v;
     }
     __syncthreads();
-    bq[0][0] = bq[1][0];
-    bq[0][1] = bq[1][1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bq[0][h] = bq[1][h];
+      bq[1][h] = bq[2][h];
+    }
   }
 
+  if (HDBG9(4)) return;
   // ------------------------------------------------------------ epilogue (layout of v9; wave = cout quarter)
   const int K = d.K, Ho = d.Ho, Wo = d.Wo;
   auto pixl = [&](int pb, int pr) {
@@ -964,19 +977,20 @@ void conv3x3_halo9b(const HArgs A) {
   const bool dep = d.ep_a != nullptr;
   const bool side = d.resid != nullptr || hasx;
   const bool stats = d.stats != nullptr;
+  // side input (residual / the data gradient's x) of pixel block pb = tile rows 2pb, 2pb+1: two 16-byte pieces per
+  // thread, loaded two pixel blocks ahead of their use and staged into the block's rows of the output tile
+  auto side_piece = [&](int k) -> const bf16r* {
+    const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
+    const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+    const int c = co0 + c16 * 8;
+    return d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
+                   : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
+                                   : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
+  };
+  u32x4 sv[2][2];
   if (side) {
-    constexpr int SK = TH * TW * BCO / 8 / NT9;
 #pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
-      const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-      const int c = co0 + c16 * 8;
-      const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
-                         : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
-                                         : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-      *(u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16)) = *(const u32x4*)src;
-    }
-    __syncthreads();
+    for (int k = 0; k < 4; ++k) sv[k >> 1][k & 1] = *(const u32x4*)side_piece(k);
   }
   bf16x8 inat[2], iperm[2];
 #pragma unroll
@@ -995,6 +1009,16 @@ void conv3x3_halo9b(const HArgs A) {
     f32x16 v = acc[pb];
     f32x16 xc;
     if (side) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = tid + NT9 * (2 * pb + j), pi = q >> 4, c16 = q & 15;
+        *(u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16)) = sv[pb & 1][j];
+      }
+      __syncthreads();
+      if (pb + 2 < 8) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sv[pb & 1][j] = *(const u32x4*)side_piece(2 * pb + 4 + j);
+      }
       bf16x8 fr[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
