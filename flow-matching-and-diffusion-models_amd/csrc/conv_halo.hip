@@ -32,6 +32,10 @@
 // channel statistics).
 #include "halo_args.h"
 
+// ablation flags of the next launches (fmd_debug_halo_flags); also read by the halo weight gradient
+// (csrc/wgrad_halo.hip) in FMD_HALO_DBG builds
+int g_dbg = 0;
+
 namespace {
 
 constexpr int TH = 16, TW = 16;           // output tile
@@ -52,7 +56,6 @@ static_assert(2 * HBUF + 4 * WBUF >= TH * TW * BCO, "epilogue tile fits in the s
 #define HDBG(bit) false
 #endif
 
-static int g_dbg = 0;
 static unsigned long long* g_tbuf = nullptr;
 
 // Phase timeline instrumentation (-DFMD_HALO_TIME; tools/halo_timeline.py): lane 0 of waves 0 and 4 of every

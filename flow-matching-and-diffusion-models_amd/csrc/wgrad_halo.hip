@@ -25,6 +25,13 @@
 #include "common.h"
 #include "../../include/fmdiff.h"
 
+#ifdef FMD_HALO_DBG
+extern int g_dbg;
+#define WDBG(bit) (A.dbg & (bit))
+#else
+#define WDBG(bit) false
+#endif
+
 namespace {
 
 constexpr int WTH = 8, WTW = 16;                 // pixel tile
@@ -45,6 +52,8 @@ struct HWArgs {
   int C, ldy;
   int tiles_x, tiles_y, ntiles;    // pixel tiles over N x Ho x Wo
   int ntc, nci, splits, per_split;
+  int dbg;                         // ablation flags (FMD_HALO_DBG builds): 1 no G loads, 2 no transform, 4 no dY DMA,
+                                   // 8 no MFMA, 16 no per-tile wait + barrier, 32 no slab write
   int depth, ncc, dsrc;            // 3-D (depth > 0): tiles over the N*depth output slices; input chunk
                                    // tci = (depth tap kz, 64-channel block) = kz*ncc + cb reading logical
                                    // slice z + kz - 1 (stored slice >> 1 under nearest-x2; dsrc = stored depth)
@@ -97,7 +106,6 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   u32x4 rx[XLD];
   int xo[XLD];                  // LDS offset, -1 none, bit 30 zero padding
   int cur_n = -1;
-  float dbs[4] = {0.f, 0.f, 0.f, 0.f};   // bias partials of this lane's 4 couts (from the A fragments)
 
   auto load_tile = [&](int t) {
     int n, ty0, tx0;
@@ -125,7 +133,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       const bool valid = act && zok && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
       const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
       const int pix = valid ? (srcsl * d.Hs + sy) * d.Ws + sx : 0;
-      rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
+      rx[k] = WDBG(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)(xsrc + (size_t)pix * xcs);
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
     }
   };
@@ -141,14 +149,14 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       const int pos = half * 64 + lane;
       const int pix = (n * d.Ho + ty0 + (pos >> 4)) * d.Wo + tx0 + (pos & 15);
       const unsigned dst = db_base + (unsigned)(buf * DBUF + (plane * DPAD + half * 64) * 8) * 2;
-      glds16(dy + (size_t)pix * A.ldy + co0 + plane * 8, __builtin_amdgcn_readfirstlane(dst));
+      if (!WDBG(4)) glds16(dy + (size_t)pix * A.ldy + co0 + plane * 8, __builtin_amdgcn_readfirstlane(dst));
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int k = 0; k < XLD; ++k) {
       u32x4 v = rx[k];
-      if (PRO != 0) {
+      if (PRO != 0 && !WDBG(2)) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float lo = bf_lo(v[e]) * pa[2 * e] + pb[2 * e];
@@ -169,39 +177,53 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};   // bias partials of this lane's 4 couts (from the A fragments)
+
+  // one pixel tile: 4 k-steps (32 pixels each) x 9 taps x 4 cout blocks = 144 MFMAs.  Fully unrolled and
+  // software-pipelined: the B fragment (G at the tap's shifted pixels) of tap slot s + 2 is read at slot s (a
+  // 3-deep ring) and the next k-step's A fragments (dY^T) half-way through a k-step, so no MFMA waits on the LDS
+  // read it consumes (round 3: read -> wait -> 4 MFMAs per tap)
+  const bf16r* const abase = db_ + ((wco * 8 + (rp >> 1)) * DPAD + (lq >> 1) * WTW + 8 * (lq & 1) + rq) * 8 + (rp & 1) * 4;
+  const bf16r* const bbase = xb + ((wci * 2 + (rp >> 1)) * XPAD + (lq >> 1) * HR + 8 * (lq & 1) + rq) * 8 + (rp & 1) * 4;
+  auto readA = [&](int buf, int ks, bf16x8 (&a)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16r* p = abase + buf * DBUF + (ks * 2 * WTW + 2 * i * DPAD) * 8;
+      const s16x4 lo = ds_read_tr16(p), hi = ds_read_tr16(p + 4 * 8);
+      a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  };
   auto compute = [&](int buf) {
-    const bf16r* xbb = xb + buf * XBUF;
-    const bf16r* dbb = db_ + buf * DBUF;
-#pragma unroll 1
-    for (int ks = 0; ks < WPIX / 32; ++ks) {
-      const int r0 = 2 * ks + (lq >> 1);          // tile row of this lane group's 8 pixels
-      const int px0 = 8 * (lq & 1);
-      bf16x8 af[4];
+    bf16x8 af[2][4], bq[3];
+    auto readB = [&](int sl) {
+      const int ks = sl / 9, tap = sl % 9, ky = tap / 3, kx = tap % 3;
+      const bf16r* p = bbase + buf * XBUF + ((2 * ks + ky) * HR + kx) * 8;
+      const s16x4 lo = ds_read_tr16(p), hi = ds_read_tr16(p + 4 * 8);
+      bq[sl % 3] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    readA(buf, 0, af[0]);
+    readB(0);
+    readB(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int plane = wco * 8 + 2 * i + (rp >> 1);
-        const bf16r* base = dbb + (plane * DPAD + r0 * WTW + px0 + rq) * 8 + (rp & 1) * 4;
-        const s16x4 lo = ds_read_tr16(base);
-        const s16x4 hi = ds_read_tr16(base + 4 * 8);
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        if (do_bias && ks == wci) {   // each wave sums one k-step's pixels: sum over waves = all pixels
-          float sacc = 0.f;
+    for (int sl = 0; sl < 36; ++sl) {
+      const int ks = sl / 9, tap = sl % 9;
+      if (tap == 4 && ks < 3) readA(buf, ks + 1, af[(ks + 1) & 1]);
+      if (sl + 2 < 36) readB(sl + 2);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sacc += bf2f((unsigned short)lo[e]) + bf2f((unsigned short)hi[e]);
-          dbs[i] += sacc;
-        }
-      }
+      for (int i = 0; i < 4; ++i) acc[i][tap] = mfma16(af[ks & 1][i], bq[sl % 3], acc[i][tap]);
+    }
+  };
+  // bias partials (workgroups of the first cin block): each wave sums k-step wci's 32 pixels of its 64 couts, so
+  // the four cin waves of a cout half cover the tile
+  auto bias_sums = [&](int buf) {
+    bf16x8 a[4];
+    readA(buf, wci, a);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap % 3;
-        const int plane = wci * 2 + (rp >> 1);
-        const bf16r* base = xbb + (plane * XPAD + (r0 + ky) * HR + px0 + kx + rq) * 8 + (rp & 1) * 4;
-        const s16x4 lo = ds_read_tr16(base);
-        const s16x4 hi = ds_read_tr16(base + 4 * 8);
-        const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    for (int i = 0; i < 4; ++i) {
+      float sacc = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][tap] = mfma16(af[i], bv, acc[i][tap]);
-      }
+      for (int e = 0; e < 8; ++e) sacc += (float)a[i][e];
+      dbs[i] += sacc;
     }
   };
 
@@ -218,14 +240,18 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
         load_tile(t + 1);
         dma_dy(t + 1, buf ^ 1);
       }
-      compute(buf);
+      if (!WDBG(8)) compute(buf);
+      if (do_bias) bias_sums(buf);
       if (more) store_tile(buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's dY DMA landed before the barrier
-      __syncthreads();
+      if (!WDBG(16)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile's dY DMA landed before the barrier
+        __syncthreads();
+      }
       buf ^= 1;
     }
   }
 
+  if (WDBG(32)) return;
   // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout; 3-D tap = kz*9 + ky*3 + kx)
   const size_t per = (size_t)d.K * T * A.C;
   float* ws = d.ws + (size_t)split * per;
@@ -503,6 +529,11 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   A.nci = d3 ? 3 * A.ncc : A.ncc;
   A.splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.ntiles + A.splits - 1) / A.splits;
+#ifdef FMD_HALO_DBG
+  A.dbg = g_dbg;
+#else
+  A.dbg = 0;
+#endif
   const int nwg = A.ntc * A.nci * A.splits;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
