@@ -287,218 +287,6 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 }
 
 
-// ---------------------------------------------------------------------------------------------------------------
-// Round-4 form (wgrad_halo9_kernel): the same workgroup tile (128 couts x 64 cins x 9 taps, 8x16-pixel tiles, one
-// barrier per tile) on v_mfma_f32_32x32x16_bf16: each wave owns 32 couts x 32 cins x 9 taps (9 accumulators of
-// 32x32 = 144 VGPRs), A = dY^T (32 couts x 16 pixels), B = G (16 pixels x 32 cins, one per tap).  An MFMA of this
-// shape holds the SIMD's vector issue for 8 of its 32 cycles instead of 8 of 16, and the LDS images are swizzled
-// so both transposing reads are bank-conflict-free (round 3: 22.6 % conflict cycles):
-//   dY tile [pixel][128 couts]: 64-byte cout block index ^ (pixel & 3)  (4 pixel rows of one read: 4 blocks);
-//   G halo [position][64 cins]: 64-byte cin block index ^ ((position >> 1) & 1)  (4 consecutive positions).
-constexpr int W9NT = 512;
-constexpr int W9DY = WPIX * WCO * 2;            // dY tile bytes (32 KiB)
-constexpr int W9G = HPOSW * WCI * 2;            // G halo bytes (22.5 KiB)
-constexpr int W9BUF = W9DY + W9G;
-constexpr int W9XLD = (HPOSW * (WCI / 8) + W9NT - 1) / W9NT;   // G pieces per thread per tile (3)
-
-typedef __attribute__((ext_vector_type(16))) float f32x16w;
-
-template <int PRO>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void wgrad_halo9_kernel(const HWArgs A) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * W9BUF];
-  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  const fmd_wgrad_desc& d = A.d;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid >> 1, wci = wid & 1;       // 32-cout quarter, 32-cin half
-  const int r = lane & 31, hh = lane >> 5;
-
-  int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int tci = b % A.nci; b /= A.nci;
-  const int tco = b % A.ntc; b /= A.ntc;
-  const int split = b;
-  const int kz = A.depth ? tci / A.ncc : 0;
-  const int zsh = A.depth ? kz - 1 : 0;
-  const int co0 = tco * WCO, ci0 = (A.depth ? tci - kz * A.ncc : tci) * WCI;
-  const int T = A.depth ? 27 : 9;
-  const int t0 = split * A.per_split, t1 = min(A.ntiles, t0 + A.per_split);
-  const bool do_bias = d.db != nullptr && tci == 0;
-  const bf16r* __restrict__ dy = (const bf16r*)d.dy;
-  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
-  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
-
-  // G staging: 8 consecutive lanes = the 8 channel groups (16 B) of one halo position
-  const int c8 = tid & 7;
-  const int c = ci0 + c8 * 8;
-  const bf16r* xsrc = (c < d.C0) ? s0 + c : s1 + (c - d.C0);
-  const int xcs = (c < d.C0) ? d.C0 : d.C1;
-  float pa[8], pb[8];
-  int cur_n = -1;
-  auto tile_org = [&](int t, int& n, int& ty0, int& tx0) {
-    const int per_img = A.tiles_x * A.tiles_y;
-    n = t / per_img;
-    const int rr = t - n * per_img;
-    ty0 = (rr / A.tiles_x) * WTH;
-    tx0 = (rr - (rr / A.tiles_x) * A.tiles_x) * WTW;
-  };
-  u32x4 rx[W9XLD];
-  int xo[W9XLD];
-  auto load_tile = [&](int t) {
-    int n, ty0, tx0;
-    tile_org(t, n, ty0, tx0);
-    const int smp = A.depth ? n / A.depth : n;
-    if (PRO != 0 && smp != cur_n) {
-      const f32x4* a4 = (const f32x4*)(d.pro_a + (size_t)smp * A.C + c);
-      const f32x4* b4 = (const f32x4*)(d.pro_b + (size_t)smp * A.C + c);
-      const f32x4 a0 = a4[0], a1 = a4[1], b0 = b4[0], b1 = b4[1];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { pa[e] = a0[e]; pa[4 + e] = a1[e]; pb[e] = b0[e]; pb[4 + e] = b1[e]; }
-      cur_n = smp;
-    }
-    const int zl = A.depth ? n - smp * A.depth + zsh : 0;
-    const bool zok = !A.depth || (zl >= 0 && zl < A.depth);
-    const int srcsl = A.depth ? smp * A.dsrc + (d.upsample ? zl >> 1 : zl) : n;
-#pragma unroll
-    for (int k = 0; k < W9XLD; ++k) {
-      const int pos = (tid >> 3) + (W9NT / 8) * k;
-      const bool act = pos < HPOSW;
-      const int hy = act ? pos / HR : 0, hx = act ? pos - (pos / HR) * HR : 0;
-      const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-      const bool valid = act && zok && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
-      const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
-      const int pix = valid ? (srcsl * d.Hs + sy) * d.Ws + sx : 0;
-      rx[k] = *(const u32x4*)(xsrc + (size_t)pix * xcs);
-      const int blk = (c8 >> 2) ^ ((pos >> 1) & 1);
-      xo[k] = !act ? -1 : (W9DY + pos * 128 + blk * 64 + (c8 & 3) * 16) | (valid ? 0 : (1 << 30));
-    }
-  };
-  // dY tile by DMA: wave w fills pixels [16w, 16w + 16) (4 x 1 KiB = 4 pixel rows per instruction); lane L of
-  // instruction j lands at pixel 16w + 4j + L/16, chunk position L%16, which holds cout chunk
-  // ((cp >> 2) ^ (pixel & 3)) * 4 + (cp & 3) of that pixel
-  auto dma_dy = [&](int t, int buf) {
-    int n, ty0, tx0;
-    tile_org(t, n, ty0, tx0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int px = 16 * wid + 4 * j + (lane >> 4), cp = lane & 15;
-      const int c16 = (((cp >> 2) ^ (px & 3)) << 2) | (cp & 3);
-      const int pix = (n * d.Ho + ty0 + (px >> 4)) * d.Wo + tx0 + (px & 15);
-      const unsigned dst = lds_base + (unsigned)(buf * W9BUF + (16 * wid + 4 * j) * 256);
-      glds16(dy + (size_t)pix * A.ldy + co0 + c16 * 8, __builtin_amdgcn_readfirstlane(dst));
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int k = 0; k < W9XLD; ++k) {
-      u32x4 v = rx[k];
-      if (PRO != 0) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float lo = bf_lo(v[e]) * pa[2 * e] + pb[2 * e];
-          float hi = bf_hi(v[e]) * pa[2 * e + 1] + pb[2 * e + 1];
-          if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-          v[e] = pack2(lo, hi);
-        }
-      }
-      const int o = xo[k];
-      if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
-      if (o >= 0) *(u32x4*)(smem + buf * W9BUF + (o & ~(1 << 30))) = v;
-    }
-  };
-
-  f32x16w acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-  float dbs = 0.f;   // bias partial of this lane's cout (waves wci == 0)
-
-  // transposing reads (ds_read_b64_tr_b16): lane 4q+p of a 16-lane group supplies row q, columns 4p..4p+3 of a
-  // 4 x 16 block; lane i of the group receives column i.  Group g = lane >> 4: columns = couts / cins
-  // 16 (g & 1) .. +15 of the wave's 32, rows = pixels / positions 8 (g >> 1) + {0..3 | 4..7} of the k-step.
-  const int gq = (lane & 15) >> 2, gp = lane & 3, g = lane >> 4;
-  const int acol = 32 * wco + 16 * (g & 1) + 4 * gp;          // cout of this lane's A address (tile-local)
-  const int bcol = 32 * wci + 16 * (g & 1) + 4 * gp;          // cin of this lane's B address
-  auto compute = [&](int buf) {
-    const unsigned char* dyb = smem + buf * W9BUF;
-    const unsigned char* gb = smem + buf * W9BUF + W9DY;
-#pragma unroll 2
-    for (int ks = 0; ks < WTH; ++ks) {   // k-step = one 16-pixel row of the tile
-      bf16x8 af;
-      {
-        s16x4 part[2];
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const int px = ks * WTW + 8 * (g >> 1) + 4 * hf + gq;
-          const int blk = (acol >> 5) ^ (px & 3);
-          part[hf] = ds_read_tr16(dyb + px * 256 + blk * 64 + (acol & 31) * 2);
-        }
-        af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(part[0], part[1], 0, 1, 2, 3, 4, 5, 6, 7));
-        if (do_bias && wci == 0) {
-          float sacc = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sacc += bf2f((unsigned short)part[0][e]) + bf2f((unsigned short)part[1][e]);
-          dbs += sacc;
-        }
-      }
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap % 3;
-        s16x4 part[2];
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const int pos = (ks + ky) * HR + kx + 8 * (g >> 1) + 4 * hf + gq;
-          const int blk = (bcol >> 5) ^ ((pos >> 1) & 1);
-          part[hf] = ds_read_tr16(gb + pos * 128 + blk * 64 + (bcol & 31) * 2);
-        }
-        const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(part[0], part[1], 0, 1, 2, 3, 4, 5, 6, 7));
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bv, acc[tap], 0, 0, 0);
-      }
-    }
-  };
-
-  if (t0 < t1) {
-    dma_dy(t0, 0);
-    load_tile(t0);
-    store_tile(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int buf = 0;
-    for (int t = t0; t < t1; ++t) {
-      const bool more = t + 1 < t1;
-      if (more) {
-        load_tile(t + 1);
-        dma_dy(t + 1, buf ^ 1);
-      }
-      compute(buf);
-      if (more) store_tile(buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      buf ^= 1;
-    }
-  }
-
-  // ---- partial slab ws[split][co][tap][ci]: accumulator register e = cout row (e&3) + 8(e>>2) + 4hh, lane = cin
-  const size_t per = (size_t)d.K * T * A.C;
-  float* ws = d.ws + (size_t)split * per;
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int co = co0 + 32 * wco + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      const int ci = ci0 + 32 * wci + r;
-      ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[tap][e];
-    }
-  if (do_bias) {
-    // A-fragment lanes: cout = 32 wco + 16 (g & 1) + (lane & 15); groups g and g ^ 2 hold the two pixel halves
-    dbs += __shfl_xor(dbs, 32, 64);
-    float* red = (float*)smem;   // tiles done (last barrier above)
-    if (wci == 0 && lane < 32) red[32 * wco + lane] = dbs;
-    __syncthreads();
-    if (tid < WCO) d.ws[(size_t)A.splits * per + (size_t)split * d.K + co0 + tid] = red[tid];
-  }
-}
-
 }  // namespace
 
 // 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
@@ -537,17 +325,6 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int nwg = A.ntc * A.nci * A.splits;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
-  static int w9 = -1;   // FMD_WGRAD9=1: the 32x32x16 kernel (measured slower than the round-3 one: off by default)
-  if (w9 < 0) {
-    const char* e = getenv("FMD_WGRAD9");
-    w9 = (e && *e) ? atoi(e) : 0;
-  }
-  if (w9) {
-    if (pro == 2) hipLaunchKernelGGL(wgrad_halo9_kernel<2>, dim3(nwg), dim3(W9NT), 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL(wgrad_halo9_kernel<1>, dim3(nwg), dim3(W9NT), 0, st, A);
-    else hipLaunchKernelGGL(wgrad_halo9_kernel<0>, dim3(nwg), dim3(W9NT), 0, st, A);
-    return (int)hipGetLastError();
-  }
   if (pro == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(nwg), dim3(NT), 0, st, A);
   else if (pro == 1) hipLaunchKernelGGL(wgrad_halo_kernel<1>, dim3(nwg), dim3(NT), 0, st, A);
   else hipLaunchKernelGGL(wgrad_halo_kernel<0>, dim3(nwg), dim3(NT), 0, st, A);
