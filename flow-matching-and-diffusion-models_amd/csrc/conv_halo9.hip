@@ -626,11 +626,24 @@ void conv3x3_halo9(const HArgs A) {
 // ahead.  No LDS weight ring means no per-tap DMA and no per-tap barrier: the only workgroup barrier is at the chunk
 // boundary (the staged halo of the next chunk complete, the previous buffer free), so the four waves and the two
 // workgroups of a CU run their 9 taps independently.  Every load is an ordinary one, so hipcc counts all waits.
-template <bool UP, int PRO>
+//
+// S2D: a stride-2 pad-1 conv (3x3, or the 4x4 that folds a nearest-x2 upsample into its data gradient) as a stride-1
+// 2x2 conv over the space-to-depth view of its input: plane (a, b) = the pixels (2y + a, 2x + b) at the output's
+// resolution, staged straight from the full-resolution NHWC tensor (chunk = plane-major 32-channel block); each
+// plane meets the taps u = 1 + 2i (a = 0) or 2i (a = 1), i.e. halo rows {0, +1} or {-1, 0} around the output row
+// (columns alike), 4 taps per chunk.  For the 3x3 the a = 0 row / b = 0 column taps at +1 carry zero weights
+// (16 tap-planes for 9 taps).  Weights pre-tiled as a 2x2 conv over 4C channels (fmd_s2d_tile_weights).
+template <bool UP, int PRO, bool S2D = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
   using G = G9<UP>;
   constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
+  static_assert(!(S2D && UP), "space-to-depth convs read full-resolution input");
+  constexpr int NTAP = S2D ? 4 : 9;          // taps per chunk
+  constexpr int RPT = S2D ? 2 : 1;           // staging rounds loaded per tap
+  constexpr int LAG = S2D ? 1 : 2;           // taps between a round's load and its transform + store
+  constexpr int RB = S2D ? 4 : 3;            // B-fragment ring (a multiple of... NTAP % RB == 0 keeps its phase per chunk)
+  static_assert(NTAP % RB == 0 && (NR + RPT - 1) / RPT + LAG <= NTAP, "chunk pipeline");
   constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
   constexpr int ZCOEF = 2 * CMAX;   // 8 zero coefficients: the affine of a chunk's invalid channels (-> SiLU(0) = 0)
   constexpr int SM_EPI = SM_COEF + (2 * CMAX + 8) * 4;
@@ -681,7 +694,7 @@ void conv3x3_halo9b(const HArgs A) {
   const int split = blockIdx.y;
   const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
   const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
-  const int T1 = A.nchunk1 * 9;
+  const int T1 = A.nchunk1 * NTAP;
 
   // ---- B fragments from global: slot sl (tap of the whole reduction) -> [plane 4][cout 128][8] bf16 tile
   const unsigned char* const wt1 = (const unsigned char*)(A.wt + (size_t)tco * T1 * (WTILE / 2));
@@ -702,7 +715,10 @@ void conv3x3_halo9b(const HArgs A) {
     const int pos = q * 64 + p0;
     const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
     const int y = hy0 + py, x = hx0 + px;
-    spix[q] = pos >= G::HPOS ? -2 : (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? y * d.Ws + x : -1;
+    if (S2D)   // full-resolution pixel (2y, 2x) of the output-resolution halo position; + the plane's (a, b) per chunk
+      spix[q] = pos >= G::HPOS ? -2 : (y >= 0 && y < d.Ho && x >= 0 && x < d.Wo) ? 2 * y * d.Ws + 2 * x : -1;
+    else
+      spix[q] = pos >= G::HPOS ? -2 : (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? y * d.Ws + x : -1;
   }
   const int sdst0 = (kc * HPAD + p0) * 16;
   const int s2pix0 = (n * d.Ho + ty0 + (p0 >> 4)) * d.Wo + tx0 + (p0 & 15);
@@ -720,7 +736,12 @@ void conv3x3_halo9b(const HArgs A) {
       int cb = chunk;
       bool zok = true;
       int sl = n;
-      if (A.depth) {
+      int poff = 0;
+      if (S2D) {
+        const int pl = chunk / A.ncb;   // plane (a, b) = (pl >> 1, pl & 1)
+        cb = chunk - pl * A.ncb;
+        poff = (pl >> 1) * d.Ws + (pl & 1);
+      } else if (A.depth) {
         const int kz = chunk / A.ncb;
         cb = chunk - kz * A.ncb;
         const int zl = zz + kz - 1;
@@ -731,7 +752,7 @@ void conv3x3_halo9b(const HArgs A) {
       sok = c < A.C && zok;
       sbase = !sok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
       scs = (c < d.C0) ? d.C0 : d.C1;
-      simg = sl * HWs;
+      simg = sl * HWs + poff;
       sca = sok ? c : ZCOEF;
       scb = sok ? A.C + c : ZCOEF;
     } else {
@@ -796,7 +817,7 @@ void conv3x3_halo9b(const HArgs A) {
     for (int t = 0; t < 9; ++t) uo[t] = 0;
   }
   auto aoff = [&](int tap, int s, int pb) {
-    const int ky = tap / 3, kx = tap % 3;
+    const int ky = S2D ? tap >> 1 : tap / 3, kx = S2D ? tap & 1 : tap % 3;
     return UP ? abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
               : abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
   };
@@ -859,11 +880,11 @@ void conv3x3_halo9b(const HArgs A) {
   }
   // B fragments three slots deep: the load of slot g + 2 is issued at slot g, two taps (about 2,000 cycles with
   // the partner wave) ahead of its MFMAs -- one tap did not cover an L2 hit under load
-  bf16x8 bq[3][2];
+  bf16x8 bq[RB][2];
   const int last2 = T1 + n_seg2 - 1;   // last 1x1 slot of this split (when n_seg2 > 0)
   if (c_lo < c_hi) {
-    loadB(bq[0], c_lo * 9);
-    loadB(bq[1], c_lo * 9 + 1);
+    loadB(bq[0], c_lo * NTAP);
+    loadB(bq[1], c_lo * NTAP + 1);
   } else {
     loadB(bq[0], T1);
     loadB(bq[1], min(T1 + 1, last2));
@@ -897,21 +918,35 @@ void conv3x3_halo9b(const HArgs A) {
     // whole after the loop); B of the next chunk's tap 0 / the first 1x1 slot at the last tap
     const bool stg = nx >= 0 && nx < A.nchunk1;
     if (stg) setup(nx);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      // slot of tap t + 2: this chunk, the next 3x3 chunk's taps 0 / 1, the first 1x1 slots, or a re-load
-      const int s2 = t < 7 ? chunk * 9 + t + 2 : stg ? nx * 9 + t - 7 : nx < 0 ? chunk * 9 + t : min(T1 + t - 7, last2);
-      if (!HDBG9(8)) loadB(bq[(t + 2) % 3], s2);
-      // round t - 2 leaves its register slot before round t lands in it
-      if (stg && t >= 2 && t < NR + 2) {
-        const u32x4 v = transform(t - 2);
-        *(u32x4*)(smem + nb + (roff[t & 1] & ~ZFLAG)) = v;
-      }
-      if (stg && t < NR) load_round(t);
-      if (!HDBG9(256)) tap_mma(t, hb, bq[t % 3]);
+    int hadj = 0;   // S2D: this chunk's plane (a, b) reads halo rows / columns {0, +1} where a / b = 0
+    if (S2D) {
+      const int pl = chunk / A.ncb;
+      hadj = ((pl >> 1) ? 0 : HROW * 16) + ((pl & 1) ? 0 : 16);
     }
-    // chunk boundary: the next chunk's halo complete, this chunk's buffer free (9 taps: the B ring's phase is
-    // the same at every chunk start)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) {
+      // slot of tap t + 2: this chunk, the next 3x3 chunk's taps 0 / 1, the first 1x1 slots, or a re-load
+      const int s2 = t < NTAP - 2 ? chunk * NTAP + t + 2
+                     : stg ? nx * NTAP + t - (NTAP - 2) : nx < 0 ? chunk * NTAP + t : min(T1 + t - (NTAP - 2), last2);
+      if (!HDBG9(8)) loadB(bq[(t + 2) % RB], s2);
+      if (stg) {
+        // rounds loaded LAG taps ago leave their register slots before this tap's rounds land in them
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          const int q = (t - LAG) * RPT + j;
+          if (t >= LAG && q < NR) {
+            const u32x4 v = transform(q);
+            *(u32x4*)(smem + nb + (roff[q & 1] & ~ZFLAG)) = v;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < RPT; ++j)
+          if (t * RPT + j < NR) load_round(t * RPT + j);
+      }
+      if (!HDBG9(256)) tap_mma(t, hb + hadj, bq[t % RB]);
+    }
+    // chunk boundary: the next chunk's halo complete, this chunk's buffer free (NTAP % RB == 0: the B ring's phase
+    // is the same at every chunk start)
     __syncthreads();
   }
   if (c_lo < c_hi && n_seg2) {   // first 1x1 chunk, staged whole after the 3x3 chunks (its buffer is free)
@@ -1132,5 +1167,111 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
     else hipLaunchKernelGGL((conv3x3_halo9b<false, 0>), g, blk, 0, st, A);
   }
 #undef H9_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Stride-2 pad-1 convs on the space-to-depth halo kernel (conv3x3_halo9b<false, PRO, true>).
+
+namespace {
+
+// tap index u of the ks-tap stride-2 kernel that plane parity a meets at its i-th halo offset (i = 0, 1):
+// a = 0 -> offsets {0, +1} = taps 1, 3; a = 1 -> offsets {-1, 0} = taps 0, 2
+FMD_DEV int s2d_tap(int a, int i) { return a ? 2 * i : 1 + 2 * i; }
+
+// out[tco][chunk][tap][kc][co 128][8] bf16 (the halo tiling of a 2x2 conv over 4*Ci plane-major channels)
+//   mode 0 (forward, ks = 3 or 4): rows = K couts, inner = C; value w[co][c][u][v] (0 where u or v >= ks)
+//   mode 1 (data gradient of conv3x3(nearest_x2(x))): rows = C, inner = K; the 4x4 kernel the nearest-x2 copy
+//            folds the 3x3 into, W4[c][k][u][v] = sum_{ky in S(u), kx in S(v)} w[k][c][ky][kx],
+//            S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1}, S(3) = {0}
+__global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode,
+                                        bf16r* __restrict__ out, long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int R = mode ? C : K, Ci = mode ? K : C;
+  const int nch = 4 * Ci / BK;
+  long long t = e;
+  const int j = (int)(t % 8); t /= 8;
+  const int co = (int)(t % BCO); t /= BCO;
+  const int kc = (int)(t % KC); t /= KC;
+  const int tap = (int)(t % 4); t /= 4;
+  const int chunk = (int)(t % nch); t /= nch;
+  const int tco = (int)t;
+  const int row = tco * BCO + co;
+  const int ch = chunk * BK + kc * 8 + j;   // plane-major channel of the 4*Ci view
+  const int pl = ch / Ci, ci = ch - pl * Ci;
+  const int u = s2d_tap(pl >> 1, tap >> 1), v = s2d_tap(pl & 1, tap & 1);
+  float val = 0.f;
+  if (row < R) {
+    if (!mode) {
+      if (u < ks && v < ks) val = w[(((size_t)row * C + ci) * ks + u) * ks + v];
+    } else {
+      const int ylo = u == 0 ? 2 : u == 3 ? 0 : 2 - u, yhi = u == 0 ? 2 : u == 3 ? 0 : 3 - u;
+      const int xlo = v == 0 ? 2 : v == 3 ? 0 : 2 - v, xhi = v == 0 ? 2 : v == 3 ? 0 : 3 - v;
+      for (int ky = ylo; ky <= yhi; ++ky)
+        for (int kx = xlo; kx <= xhi; ++kx) val += w[(((size_t)ci * C + row) * 3 + ky) * 3 + kx];
+    }
+  }
+  out[e] = (bf16r)f2bf(val);
+}
+
+}  // namespace
+
+extern "C" int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode) {
+  const int64_t R = mode ? C : K, Ci = mode ? K : C;
+  return ((R + BCO - 1) / BCO) * (4 * Ci / BK) * 4 * KC * BCO * 8;
+}
+
+extern "C" int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out,
+                                    fmd_stream_t stream) {
+  const int Ci = mode ? K : C;
+  if ((mode != 0 && mode != 1) || (mode == 0 && ks != 3 && ks != 4) || (mode == 1 && ks != 3) || Ci % BK) return -1;
+  const long long total = fmd_s2d_tiled_size(K, C, mode);
+  hipLaunchKernelGGL(s2d_tile_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, w, K, C, ks, mode, (bf16r*)out, total);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
+  if (d->stride != 2 || d->pad != 1 || (d->ks != 3 && d->ks != 4) || d->transposed || d->upsample) return 1;
+  if (d->Do > 0 || d->Ds > 0 || d->src2 || d->gout || d->out_f32 || d->splits > 1) return 1;
+  if (d->Hs != 2 * d->Ho || d->Ws != 2 * d->Wo || d->Ho % TH || d->Wo % TW) return 1;
+  const int C = d->C0 + d->C1;
+  if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;
+  if (d->pro_a && C > CMAX) return 1;
+  if (d->accumulate && (d->resid || d->ep_x0)) return 1;
+  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      (long long)d->N * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
+  HArgs A;
+  A.d = *d;
+  if (d->accumulate) {   // out += conv: the old output enters as the residual side input of the same tile
+    A.d.resid = d->out;
+    A.d.accumulate = 0;
+  }
+  A.C = C;
+  A.C23 = 0;
+  A.tiles_x = d->Wo / TW;
+  A.tiles_y = d->Ho / TH;
+  A.ntc = d->K / BCO;
+  A.depth = 0;
+  A.dsrc = 0;
+  A.ncb = C / BK;            // chunks per plane
+  A.nchunk1 = 4 * A.ncb;     // plane-major
+  A.nchunk2 = 0;
+  A.nsteps_slots = A.nchunk1 * 4;
+  A.splits = 1;
+  A.cps = A.nchunk1;
+  A.wt = (const bf16r*)d->wgt_tiled;
+  A.wt2 = nullptr;
+  A.tbuf = nullptr;
+  A.dbg = 0;
+  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  if (nwg < 128) return 1;
+  const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
+  const dim3 g(nwg), blk(NT9);
+  hipStream_t st = (hipStream_t)stream;
+  if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, true>), g, blk, 0, st, A);
+  else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, true>), g, blk, 0, st, A);
+  else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, true>), g, blk, 0, st, A);
   return (int)hipGetLastError();
 }

@@ -47,6 +47,9 @@ HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdif
 MAT3D = os.environ.get("FMD_MAT3D", "1") == "1"
 # 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
 DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
+# stride-2 3x3 forwards and nearest-x2 data gradients on the space-to-depth halo kernel (fmd_conv_s2d); 0: the
+# implicit GEMM (A/B runs)
+S2D_HALO = os.environ.get("FMD_S2D_HALO", "1") == "1"
 # ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); FMD_POINT_1X1=0 for A/B runs
 POINT_1X1 = os.environ.get("FMD_POINT_1X1", "1") == "1"
 # training, 3-D fused-prologue halo convs (FMD_MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
@@ -132,6 +135,8 @@ class WeightCache:
                 for w in e["src"]:
                     e["buf"][o:o + w.shape[0]].copy_(w.detach())
                     o += w.shape[0]
+            elif e["kind"] == "s2d":
+                ops.s2d_tile_weights(e["src"].detach(), e["mode"], out=e["buf"])
         for cubic in (False, True):   # square (<= 9 taps) and cubic (27 taps) masters: one launch each
             jobs = [(key, e) for key, e in self._c.items()
                     if e["kind"] in ("prep", "tiled") and (e["job"][7] == 27) == cubic]
@@ -271,6 +276,17 @@ class WeightCache:
             self._force.discard(key)
         return self._c[key]["buf"]
 
+    def s2d(self, w: torch.Tensor, mode: int):
+        """Space-to-depth halo tiles of a 2-D 3x3 weight (fmd_s2d_tile_weights): mode 0 the stride-2 forward,
+        1 the data gradient of the conv on a nearest-x2 input; re-derived by one launch per optimizer step."""
+        key = (id(w), "s2d", mode)
+        if not self._fresh(key, self._ver(w)):
+            e = self._c.get(key)
+            buf = ops.s2d_tile_weights(w.detach(), mode, out=None if e is None else e["buf"])
+            self._c[key] = dict(kind="s2d", src=w, buf=buf, ver=self._ver(w), mode=mode)
+            self._force.discard(key)
+        return self._c[key]["buf"]
+
     def padded(self, v: torch.Tensor, n: int):
         key = (id(v), "pad", n)
         if not self._fresh(key, self._ver(v)):
@@ -373,9 +389,15 @@ class UNetEngine:
             halo = DEPTH_HALO and stride == 1 and ops.halo_eligible(
                 N_ * Do_, sp[1], ops.out_hw(sp[1], 3, 1, 1, upsample), ops.out_hw(sp[2], 3, 1, 1, upsample),
                 conv.out_channels, upsample=upsample, Cin=Cin, ztaps=3)
-        w, wt = self._wts(conv.weight, 0, halo, None, Cin)
-        out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
-                           bias=conv.bias, want_stats="free", wgt_tiled=wt)
+        s2d = (S2D_HALO and stride == 2 and len(sp) == 2 and conv.weight.shape[1] == Cin and
+               ops.s2d_eligible(N_, sp[0], sp[1], sp[0] // 2, sp[1] // 2, conv.out_channels, Cin, 3))
+        if s2d:   # DownsampleND's conv on the space-to-depth halo kernel
+            out, st = ops.conv(x.t, conv.out_channels, None, ks=3, stride=2, pad=1, bias=conv.bias, want_stats="free",
+                               s2d_tiled=self.wc.s2d(conv.weight, 0))
+        else:
+            w, wt = self._wts(conv.weight, 0, halo, None, Cin)
+            out, st = ops.conv(x.t, conv.out_channels, w, ks=3, stride=stride, pad=1, upsample=upsample,
+                               bias=conv.bias, want_stats="free", wgt_tiled=wt)
         o = Act(out, st)
         if ctx.tape is not None:
             def bwd():
@@ -390,7 +412,12 @@ class UNetEngine:
                 if not x.need_grad:
                     return
                 g, acc = _gdest(x)
-                if upsample and len(sp) == 2:
+                if upsample and len(sp) == 2 and S2D_HALO and conv.weight.shape[1] == Cin and ops.s2d_eligible(
+                        N_, 2 * sp[0], 2 * sp[1], sp[0], sp[1], Cin, dy.shape[-1], 4):
+                    # nearest-x2 folded into a 4x4 stride-2 gather, on the space-to-depth halo kernel
+                    ops.conv(dy, Cin, None, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc),
+                             s2d_tiled=self.wc.s2d(conv.weight, 1))
+                elif upsample and len(sp) == 2:
                     # nearest-x2 folded into the weights: a 4x4 stride-2 transposed gather (mode 2)
                     wd = self.wc.get(conv.weight, 2)
                     ops.conv(dy, Cin, wd, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc))

@@ -259,18 +259,39 @@ def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, trans
             and halo_splits(N, Ho, Wo, K, Cin, ztaps) > 0)
 
 
+def s2d_eligible(N, Hs, Ws, Ho, Wo, K, C, ks) -> bool:
+    """Mirror of fmd_conv_s2d's applicability test (csrc/conv_halo9.hip): a 2-D stride-2 pad-1 3x3 / 4x4 forward
+    gather onto 16x16 output tiles, C % 32 == 0, K % 128 == 0, >= 128 workgroups."""
+    return (ks in (3, 4) and Hs == 2 * Ho and Ws == 2 * Wo and Ho % 16 == 0 and Wo % 16 == 0 and C % 32 == 0
+            and K % 128 == 0 and N * (Ho // 16) * (Wo // 16) * (K // 128) >= 128
+            and N * Hs * Ws * C < (1 << 31) and N * Ho * Wo * K < (1 << 31))
+
+
+def s2d_tile_weights(w: torch.Tensor, mode: int, out=None) -> torch.Tensor:
+    """fp32 [K][C][ks][ks] -> fmd_conv_s2d's tiles (mode 0 stride-2 forward, 1 data gradient of a 3x3 conv on a
+    nearest-x2 input)."""
+    K, Cc, ks = w.shape[0], w.shape[1], w.shape[2]
+    n = int(_lib.lib().fmd_s2d_tiled_size(K, Cc, mode))
+    if out is None:
+        out = torch.empty((n,), device=w.device, dtype=BF16)
+    _lib.call("fmd_s2d_tile_weights", _p(w.contiguous()), K, Cc, ks, mode, _p(out), stream())
+    return out
+
+
 def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, transposed=False, out_hw_=None,
          pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
          out_f32=False,
          accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
-         wgt2_tiled=None, gout=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+         wgt2_tiled=None, gout=None, s2d_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
     """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``.
     ``want_stats``: True = per-channel statistics of the output (a separate fmd_channel_stats pass when the
     kernel cannot emit them); "free" = only when the kernel emits them (else None: Act statistics are then
     derived on demand, and a small-level consumer that computes its own GroupNorm never pays for them).
     ``gout``: bf16 tensor shaped like the (concatenated) input; the halo path writes the prologue's output
     G = SiLU(a*x+b) into it (the weight gradient's operand).  Requires ``pro``, (C0+C1) % 32 == 0 and a
-    halo-eligible problem (:func:`halo_eligible`); raises otherwise."""
+    halo-eligible problem (:func:`halo_eligible`); raises otherwise.
+    ``s2d_tiled``: :func:`s2d_tile_weights` of the stride-2 conv's weight -- the problem runs on the space-to-depth
+    halo kernel (fmd_conv_s2d; the caller checks :func:`s2d_eligible`), ``wgt`` unused."""
     _need_cuda(src0, "conv")
     # 3-D (spatial_dims = 3): NDHWC tensors, cubic kernels; ``out_hw_`` is then (Do, Ho, Wo)
     d3 = src0.dim() == 5
@@ -332,6 +353,20 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
                                                    C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
+    if s2d_tiled is not None:   # space-to-depth halo kernel: one launch, statistics in its epilogue
+        if not s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks) or d3 or stride != 2 or pad != 1 or transposed \
+                or upsample or src2 is not None or out_f32 or gout is not None:
+            raise ValueError("conv: s2d_tiled given for a problem fmd_conv_s2d does not take")
+        d.wgt_tiled, d.splits = _p(s2d_tiled), 1
+        st = None
+        if want_stats and (Ho * Wo) % 64 == 0:
+            slab = torch.empty((M // 64, K, 2), device=dev, dtype=F32)
+            d.stats = _p(slab)
+            st = Stats(slab, 64)
+        _lib.call("fmd_conv_s2d", C.byref(d), stream())
+        if want_stats is True and st is None:
+            st = channel_stats(out)
+        return out, st
     if gout is not None:
         want = (N, Ds, Hs, Ws, C0 + C1) if d3 else (N, Hs, Ws, C0 + C1)
         if pro is None or not halo or (C0 + C1) % HALO_BK or tuple(gout.shape) != want or gout.dtype != BF16:

@@ -120,6 +120,18 @@ int fmd_halo_set_min_workgroups(int32_t n);
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);
 int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* out, fmd_stream_t s);
+/* Stride-2 pad-1 convs (3x3, or the 4x4 data gradient of conv3x3(nearest_x2(x))) as a 2x2 conv over the
+ * space-to-depth view of the input (plane (a, b) = pixels (2y + a, 2x + b), staged from the full-resolution NHWC
+ * tensor) on the halo kernel (csrc/conv_halo9.hip).  Replaces the implicit GEMM of DownsampleND's conv
+ * (src/nn/ops/upsampling.py:49-56) and the data gradient of UpsampleND's conv (upsampling.py:27-29).  Needs
+ * d->wgt_tiled from fmd_s2d_tile_weights, Hs = 2 Ho, Ws = 2 Wo, Ho and Wo multiples of 16, (C0 + C1) % 32 == 0,
+ * K % 128 == 0, >= 128 output tiles; d->accumulate adds into d->out.  Returns 1 when the problem does not qualify. */
+int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t s);
+/* fp32 reference-layout conv weight [K][C][ks][ks] -> the space-to-depth halo tiles of fmd_conv_s2d.  mode 0: the
+ * stride-2 forward (rows K, ks 3 or 4); mode 1: the 4x4 data gradient of a 3x3 conv on a nearest-x2 input
+ * (rows C, inner channels K, ks 3).  The inner channel count must be a multiple of 32. */
+int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode);
+int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out, fmd_stream_t s);
 
 /* UNet output head: out = conv3x3(SiLU(a*h + b)) to K <= 8 channels, fp32 NHWC [N][H][W][8]
  * (channels >= K zero), replacing the final GroupNorm -> SiLU -> ConvND of

@@ -1220,3 +1220,50 @@ def test_conv3d_s2_dgrad_parity_classes_with_fused_stats():
     rel = ((t1 - t2).norm() / t2.norm()).item()
     print(f"3-D parity-class statistics vs split-K reduce rel L2 {rel:.3e}")
     assert rel < 1e-2
+
+
+@pytest.mark.parametrize("case", ["down", "down_pro_stats", "updgrad", "updgrad_acc"])
+def test_s2d_halo_conv_vs_torch(case):
+    """fmd_conv_s2d (csrc/conv_halo9.hip): stride-2 convs as 2x2 convs over the space-to-depth view on the halo
+    kernel, vs fp32 torch on the bf16-rounded operands.  down: DownsampleND's 3x3 stride-2 conv (+ bias; the
+    _pro_stats case with a GroupNorm-affine + SiLU prologue and fused statistics); updgrad: the data gradient of
+    conv3x3(nearest_x2(x)) through the 4x4 stride-2 gather the copy folds into (the _acc case adds into the
+    existing gradient)."""
+    O = ops()
+    g = torch.Generator().manual_seed(50)
+    if case.startswith("down"):
+        N, H, W, C, K = 8, 128, 128, 64, 128
+        x = _rand_nhwc(N, H, W, C, 51)
+        w = _w(K, C, 3, 52)
+        b = torch.randn(K, generator=g) * 0.1
+        pro = None
+        xin = x.float()
+        if case == "down_pro_stats":
+            pa, pb = torch.rand(N, C, generator=g) + 0.5, torch.randn(N, C, generator=g) * 0.2
+            pro = (pa.to(DEV), pb.to(DEV), True)
+            xin = F.silu(pa[:, None, None, :] * xin + pb[:, None, None, :]).to(torch.bfloat16).float()
+        got, st = O.conv(x.to(DEV), K, None, ks=3, stride=2, pad=1, bias=b.to(DEV), pro=pro,
+                         want_stats=case == "down_pro_stats", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 0))
+        ref = F.conv2d(_to_nchw(xin), _bfw(w), b, stride=2, padding=1).permute(0, 2, 3, 1)
+        _close(got, ref)
+        if st is not None:
+            gf = got.float().cpu()
+            sums = st.slab.view(N, -1, K, 2).sum(1).cpu()
+            torch.testing.assert_close(sums[..., 0], gf.sum((1, 2)), rtol=5e-3, atol=3e-2)
+            torch.testing.assert_close(sums[..., 1], (gf * gf).sum((1, 2)), rtol=5e-3, atol=3e-2)
+    else:
+        N, Hl, Wl, Cin, K = 8, 64, 64, 128, 128
+        w = _w(K, Cin, 3, 53)
+        dy = _rand_nhwc(N, 2 * Hl, 2 * Wl, K, 54)
+        xl = torch.zeros(N, Cin, Hl, Wl, requires_grad=True)
+        y = F.conv2d(F.interpolate(xl, scale_factor=2, mode="nearest"), _bfw(w), padding=1)
+        y.backward(_to_nchw(dy))
+        ref = xl.grad.permute(0, 2, 3, 1)
+        out = None
+        if case == "updgrad_acc":
+            prev = _rand_nhwc(N, Hl, Wl, Cin, 55)
+            out = prev.to(DEV).clone()
+            ref = ref + prev.float()
+        got, _ = O.conv(dy.to(DEV), Cin, None, ks=4, stride=2, pad=1, out_hw_=(Hl, Wl), out=out,
+                        accumulate=case == "updgrad_acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 1))
+        _close(got, ref)
