@@ -633,16 +633,23 @@ void conv3x3_halo9(const HArgs A) {
 // plane meets the taps u = 1 + 2i (a = 0) or 2i (a = 1), i.e. halo rows {0, +1} or {-1, 0} around the output row
 // (columns alike), 4 taps per chunk.  For the 3x3 the a = 0 row / b = 0 column taps at +1 carry zero weights
 // (16 tap-planes for 9 taps).  Weights pre-tiled as a 2x2 conv over 4C channels (fmd_s2d_tile_weights).
-template <bool UP, int PRO, bool S2D = false>
+//
+// D2S: the data gradient of a stride-2 3x3 conv (transposed gather) as a stride-1 2x2 conv from the low-resolution
+// gradient onto the depth-to-space view of the output: output class (a, b) = the pixels (2i + a, 2j + b), each a
+// block of 4 x cout "channels" (class-major, one class per 128-cout tile), meeting dy at offsets {0, +1} (taps
+// 1 | 2, 0 per dimension; 9 of the 16 tap-classes non-zero); the epilogue writes the class's pixels.
+// MODE: 0 plain 3x3, 1 S2D, 2 D2S.
+template <bool UP, int PRO, int MODE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
   using G = G9<UP>;
   constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
-  static_assert(!(S2D && UP), "space-to-depth convs read full-resolution input");
-  constexpr int NTAP = S2D ? 4 : 9;          // taps per chunk
-  constexpr int RPT = S2D ? 2 : 1;           // staging rounds loaded per tap
-  constexpr int LAG = S2D ? 1 : 2;           // taps between a round's load and its transform + store
-  constexpr int RB = S2D ? 4 : 3;            // B-fragment ring (a multiple of... NTAP % RB == 0 keeps its phase per chunk)
+  constexpr bool S2D = MODE == 1, D2S = MODE == 2;
+  static_assert(!(MODE && UP), "stride-2 modes are not nearest-x2 gathers");
+  constexpr int NTAP = MODE ? 4 : 9;         // taps per chunk
+  constexpr int RPT = MODE ? 2 : 1;          // staging rounds loaded per tap
+  constexpr int LAG = MODE ? 1 : 2;          // taps between a round's load and its transform + store
+  constexpr int RB = MODE ? 4 : 3;           // B-fragment ring (NTAP % RB == 0 keeps its phase per chunk)
   static_assert(NTAP % RB == 0 && (NR + RPT - 1) / RPT + LAG <= NTAP, "chunk pipeline");
   constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
   constexpr int ZCOEF = 2 * CMAX;   // 8 zero coefficients: the affine of a chunk's invalid channels (-> SiLU(0) = 0)
@@ -666,7 +673,15 @@ void conv3x3_halo9b(const HArgs A) {
   const int smp = A.depth ? n / A.depth : n;
   const int zz = A.depth ? n - smp * A.depth : 0;
   const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
-  const int co0 = tco * BCO;
+  // D2S: cout tile tco = (output class, 128-cout block), class-major
+  const int ncob = D2S ? d.K / BCO : 1;
+  const int ocls = D2S ? tco / ncob : 0;
+  const int co0 = (D2S ? tco - ocls * ncob : tco) * BCO;
+  // output pixel of tile-local pixel pi (y * 16 + x); D2S: the class's full-resolution pixel
+  auto opix = [&](int pi) -> int {
+    const int y = ty0 + (pi >> 4), x = tx0 + (pi & 15);
+    return D2S ? (n * d.Ho + 2 * y + (ocls >> 1)) * d.Wo + 2 * x + (ocls & 1) : (n * d.Ho + y) * d.Wo + x;
+  };
   const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;
   const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
   const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
@@ -817,7 +832,7 @@ void conv3x3_halo9b(const HArgs A) {
     for (int t = 0; t < 9; ++t) uo[t] = 0;
   }
   auto aoff = [&](int tap, int s, int pb) {
-    const int ky = S2D ? tap >> 1 : tap / 3, kx = S2D ? tap & 1 : tap % 3;
+    const int ky = MODE ? tap >> 1 : tap / 3, kx = MODE ? tap & 1 : tap % 3;
     return UP ? abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
               : abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
   };
@@ -918,7 +933,8 @@ void conv3x3_halo9b(const HArgs A) {
     // whole after the loop); B of the next chunk's tap 0 / the first 1x1 slot at the last tap
     const bool stg = nx >= 0 && nx < A.nchunk1;
     if (stg) setup(nx);
-    int hadj = 0;   // S2D: this chunk's plane (a, b) reads halo rows / columns {0, +1} where a / b = 0
+    // S2D: this chunk's plane (a, b) reads halo rows / columns {0, +1} where a / b = 0; D2S: always {0, +1}
+    int hadj = D2S ? HROW * 16 + 16 : 0;
     if (S2D) {
       const int pl = chunk / A.ncb;
       hadj = ((pl >> 1) ? 0 : HROW * 16) + ((pl & 1) ? 0 : 16);
@@ -1001,8 +1017,7 @@ void conv3x3_halo9b(const HArgs A) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int pi = pixl(pb, (e & 3) + 8 * (e >> 2) + 4 * hh);
-          const size_t p = ((size_t)n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-          ws[p * K + co] = acc[pb][e];
+          ws[(size_t)opix(pi) * K + co] = acc[pb][e];
         }
     }
     return;
@@ -1016,7 +1031,7 @@ void conv3x3_halo9b(const HArgs A) {
   // thread, loaded two pixel blocks ahead of their use and staged into the block's rows of the output tile
   auto side_piece = [&](int k) -> const bf16r* {
     const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
-    const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
+    const int p = opix(pi);
     const int c = co0 + c16 * 8;
     return d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
                    : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
@@ -1104,7 +1119,7 @@ void conv3x3_halo9b(const HArgs A) {
       *(u32x2*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16) + (c & 7) * 2) = o;
     }
     if (stats && (pb & 1)) {   // one statistics row per 64 pixels (= pixel blocks 2k, 2k+1: 4 tile rows)
-      const int srow = tile * 4 + (pb >> 1);
+      const int srow = (D2S ? tile * 4 + ocls : tile) * 4 + (pb >> 1);
       const float a = st1 + __shfl_xor(st1, 32, 64);
       const float q = st2 + __shfl_xor(st2, 32, 64);
       if (hh == 0) {
@@ -1120,8 +1135,8 @@ void conv3x3_halo9b(const HArgs A) {
 #pragma unroll
   for (int k = 0; k < TH * TW * BCO / 8 / NT9; ++k) {
     const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
-    const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-    *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) = *(const u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16));
+    *(u32x4*)((bf16r*)d.out + (size_t)opix(pi) * K + co0 + c16 * 8) =
+        *(const u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16));
   }
 }
 
@@ -1179,17 +1194,19 @@ namespace {
 // a = 0 -> offsets {0, +1} = taps 1, 3; a = 1 -> offsets {-1, 0} = taps 0, 2
 FMD_DEV int s2d_tap(int a, int i) { return a ? 2 * i : 1 + 2 * i; }
 
-// out[tco][chunk][tap][kc][co 128][8] bf16 (the halo tiling of a 2x2 conv over 4*Ci plane-major channels)
-//   mode 0 (forward, ks = 3 or 4): rows = K couts, inner = C; value w[co][c][u][v] (0 where u or v >= ks)
-//   mode 1 (data gradient of conv3x3(nearest_x2(x))): rows = C, inner = K; the 4x4 kernel the nearest-x2 copy
+// out[tco][chunk][tap][kc][co 128][8] bf16 (the halo tiling of a 2x2 conv)
+//   mode 0 (forward, ks = 3 or 4): rows = K couts, inner = 4C plane-major; value w[co][c][u][v] (0 where u or v >= ks)
+//   mode 1 (data gradient of conv3x3(nearest_x2(x))): rows = C, inner = 4K; the 4x4 kernel the nearest-x2 copy
 //            folds the 3x3 into, W4[c][k][u][v] = sum_{ky in S(u), kx in S(v)} w[k][c][ky][kx],
 //            S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1}, S(3) = {0}
+//   mode 2 (data gradient of a stride-2 3x3, D2S): rows = 4C class-major, inner = K; class a meets dy offset u with
+//            tap ky = (a ? (u ? 0 : 2) : (u ? none : 1)), columns alike
 __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode,
                                         bf16r* __restrict__ out, long long total) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
-  const int R = mode ? C : K, Ci = mode ? K : C;
-  const int nch = 4 * Ci / BK;
+  const int R = mode == 0 ? K : mode == 1 ? C : 4 * C, Ci = mode == 0 ? C : K;
+  const int nch = (mode == 2 ? Ci : 4 * Ci) / BK;
   long long t = e;
   const int j = (int)(t % 8); t /= 8;
   const int co = (int)(t % BCO); t /= BCO;
@@ -1198,10 +1215,18 @@ __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int 
   const int chunk = (int)(t % nch); t /= nch;
   const int tco = (int)t;
   const int row = tco * BCO + co;
-  const int ch = chunk * BK + kc * 8 + j;   // plane-major channel of the 4*Ci view
+  const int ch = chunk * BK + kc * 8 + j;   // inner channel (modes 0, 1: plane-major over 4*Ci)
+  float val = 0.f;
+  if (mode == 2) {
+    const int cls = row / C, c = row - cls * C;
+    const int a = cls >> 1, b = cls & 1, uu = tap >> 1, vv = tap & 1;
+    const int ky = a ? (uu ? 0 : 2) : (uu ? -1 : 1), kx = b ? (vv ? 0 : 2) : (vv ? -1 : 1);
+    if (row < R && ky >= 0 && kx >= 0) val = w[(((size_t)ch * C + c) * 3 + ky) * 3 + kx];
+    out[e] = (bf16r)f2bf(val);
+    return;
+  }
   const int pl = ch / Ci, ci = ch - pl * Ci;
   const int u = s2d_tap(pl >> 1, tap >> 1), v = s2d_tap(pl & 1, tap & 1);
-  float val = 0.f;
   if (row < R) {
     if (!mode) {
       if (u < ks && v < ks) val = w[(((size_t)row * C + ci) * ks + u) * ks + v];
@@ -1218,14 +1243,15 @@ __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int 
 }  // namespace
 
 extern "C" int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode) {
-  const int64_t R = mode ? C : K, Ci = mode ? K : C;
-  return ((R + BCO - 1) / BCO) * (4 * Ci / BK) * 4 * KC * BCO * 8;
+  const int64_t R = mode == 0 ? K : mode == 1 ? C : 4LL * C, Ci = mode == 0 ? C : K;
+  return ((R + BCO - 1) / BCO) * ((mode == 2 ? Ci : 4 * Ci) / BK) * 4 * KC * BCO * 8;
 }
 
 extern "C" int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out,
                                     fmd_stream_t stream) {
   const int Ci = mode ? K : C;
-  if ((mode != 0 && mode != 1) || (mode == 0 && ks != 3 && ks != 4) || (mode == 1 && ks != 3) || Ci % BK) return -1;
+  if (mode < 0 || mode > 2 || (mode == 0 && ks != 3 && ks != 4) || (mode != 0 && ks != 3) || Ci % BK) return -1;
+  if (mode == 2 && C % BCO) return -1;   // one output class per 128-row tile
   const long long total = fmd_s2d_tiled_size(K, C, mode);
   hipLaunchKernelGGL(s2d_tile_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, w, K, C, ks, mode, (bf16r*)out, total);
@@ -1270,8 +1296,46 @@ extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   const dim3 g(nwg), blk(NT9);
   hipStream_t st = (hipStream_t)stream;
-  if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, true>), g, blk, 0, st, A);
-  else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, true>), g, blk, 0, st, A);
-  else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, true>), g, blk, 0, st, A);
+  if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, 1>), g, blk, 0, st, A);
+  else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, 1>), g, blk, 0, st, A);
+  else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 1>), g, blk, 0, st, A);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t stream) {
+  if (!d->transposed || d->stride != 2 || d->pad != 1 || d->ks != 3 || d->upsample) return 1;
+  if (d->Do > 0 || d->Ds > 0 || d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->pro_a) return 1;
+  if (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws || d->Hs % TH || d->Ws % TW) return 1;
+  const int C = d->C0 + d->C1;
+  if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;
+  if (d->accumulate && (d->resid || d->ep_x0)) return 1;
+  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      (long long)d->N * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
+  HArgs A;
+  A.d = *d;
+  if (d->accumulate) {
+    A.d.resid = d->out;
+    A.d.accumulate = 0;
+  }
+  A.C = C;
+  A.C23 = 0;
+  A.tiles_x = d->Ws / TW;    // tiles over the low-resolution input grid; 4 output classes per tile
+  A.tiles_y = d->Hs / TH;
+  A.ntc = 4 * (d->K / BCO);
+  A.depth = 0;
+  A.dsrc = 0;
+  A.ncb = C / BK;
+  A.nchunk1 = A.ncb;
+  A.nchunk2 = 0;
+  A.nsteps_slots = A.nchunk1 * 4;
+  A.splits = 1;
+  A.cps = A.nchunk1;
+  A.wt = (const bf16r*)d->wgt_tiled;
+  A.wt2 = nullptr;
+  A.tbuf = nullptr;
+  A.dbg = 0;
+  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  if (nwg < 128) return 1;
+  hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 2>), dim3(nwg), dim3(NT9), 0, (hipStream_t)stream, A);
   return (int)hipGetLastError();
 }

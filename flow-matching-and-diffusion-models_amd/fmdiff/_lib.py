@@ -86,6 +86,7 @@ SIGNATURES = {
     "fmd_halo_tiled_size": [i32, i32, i32],
     "fmd_tile_weights_halo": [p, i32, i32, i32, p, p],
     "fmd_conv_s2d": [C.POINTER(ConvDesc), p],
+    "fmd_conv_d2s": [C.POINTER(ConvDesc), p],
     "fmd_s2d_tiled_size": [i32, i32, i32],
     "fmd_s2d_tile_weights": [p, i32, i32, i32, i32, p, p],
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],

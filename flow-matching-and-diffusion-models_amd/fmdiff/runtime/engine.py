@@ -277,8 +277,9 @@ class WeightCache:
         return self._c[key]["buf"]
 
     def s2d(self, w: torch.Tensor, mode: int):
-        """Space-to-depth halo tiles of a 2-D 3x3 weight (fmd_s2d_tile_weights): mode 0 the stride-2 forward,
-        1 the data gradient of the conv on a nearest-x2 input; re-derived by one launch per optimizer step."""
+        """Stride-2 halo tiles of a 2-D 3x3 weight (fmd_s2d_tile_weights): mode 0 the stride-2 forward, 1 the data
+        gradient of the conv on a nearest-x2 input, 2 the stride-2 data gradient; re-derived by one launch per
+        optimizer step."""
         key = (id(w), "s2d", mode)
         if not self._fresh(key, self._ver(w)):
             e = self._c.get(key)
@@ -532,6 +533,12 @@ class UNetEngine:
             halo = self._halo_ok(dy.shape[0], sp, Cin, dy.shape[-1])
             base, tiled = self._wts(w, 3, halo, Kpad, None)
             return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=sp, wgt_tiled=tiled, **kw)
+        if (S2D_HALO and len(sp) == 2 and Kpad is None and w.dim() == 4 and w.shape[1] == Cin and
+                not kw.get("pro") and ops.d2s_eligible(dy.shape[0], dy.shape[1], dy.shape[2], sp[0], sp[1], Cin,
+                                                       dy.shape[-1])):
+            # transposed stride-2 gather onto the depth-to-space view, on the halo kernel
+            return ops.conv(dy, Cin, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=sp,
+                            s2d_tiled=self.wc.s2d(w, 2), **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,
                         out_hw_=sp, **kw)
 

@@ -267,9 +267,17 @@ def s2d_eligible(N, Hs, Ws, Ho, Wo, K, C, ks) -> bool:
             and N * Hs * Ws * C < (1 << 31) and N * Ho * Wo * K < (1 << 31))
 
 
+def d2s_eligible(N, Hs, Ws, Ho, Wo, K, C) -> bool:
+    """Mirror of fmd_conv_d2s's applicability test: the transposed gather of a 2-D stride-2 pad-1 3x3 conv from an
+    Hs x Ws gradient (multiples of 16) onto Ho = 2 Hs, Wo = 2 Ws, C % 32 == 0, K % 128 == 0, >= 128 workgroups."""
+    return (Ho == 2 * Hs and Wo == 2 * Ws and Hs % 16 == 0 and Ws % 16 == 0 and C % 32 == 0 and K % 128 == 0
+            and N * (Hs // 16) * (Ws // 16) * 4 * (K // 128) >= 128
+            and N * Hs * Ws * C < (1 << 31) and N * Ho * Wo * K < (1 << 31))
+
+
 def s2d_tile_weights(w: torch.Tensor, mode: int, out=None) -> torch.Tensor:
-    """fp32 [K][C][ks][ks] -> fmd_conv_s2d's tiles (mode 0 stride-2 forward, 1 data gradient of a 3x3 conv on a
-    nearest-x2 input)."""
+    """fp32 [K][C][ks][ks] -> fmd_conv_s2d / fmd_conv_d2s tiles (mode 0 stride-2 forward, 1 data gradient of a 3x3
+    conv on a nearest-x2 input, 2 stride-2 3x3 data gradient)."""
     K, Cc, ks = w.shape[0], w.shape[1], w.shape[2]
     n = int(_lib.lib().fmd_s2d_tiled_size(K, Cc, mode))
     if out is None:
@@ -353,17 +361,18 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
                                                    C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
-    if s2d_tiled is not None:   # space-to-depth halo kernel: one launch, statistics in its epilogue
-        if not s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks) or d3 or stride != 2 or pad != 1 or transposed \
-                or upsample or src2 is not None or out_f32 or gout is not None:
-            raise ValueError("conv: s2d_tiled given for a problem fmd_conv_s2d does not take")
+    if s2d_tiled is not None:   # stride-2 on the halo kernel: one launch, statistics in its epilogue
+        ok = (s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks) if not transposed else
+              (ks == 3 and pro is None and d2s_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1)))
+        if not ok or d3 or stride != 2 or pad != 1 or upsample or src2 is not None or out_f32 or gout is not None:
+            raise ValueError("conv: s2d_tiled given for a problem fmd_conv_s2d / fmd_conv_d2s does not take")
         d.wgt_tiled, d.splits = _p(s2d_tiled), 1
         st = None
         if want_stats and (Ho * Wo) % 64 == 0:
             slab = torch.empty((M // 64, K, 2), device=dev, dtype=F32)
             d.stats = _p(slab)
             st = Stats(slab, 64)
-        _lib.call("fmd_conv_s2d", C.byref(d), stream())
+        _lib.call("fmd_conv_d2s" if transposed else "fmd_conv_s2d", C.byref(d), stream())
         if want_stats is True and st is None:
             st = channel_stats(out)
         return out, st

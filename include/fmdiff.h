@@ -127,9 +127,17 @@ int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* 
  * d->wgt_tiled from fmd_s2d_tile_weights, Hs = 2 Ho, Ws = 2 Wo, Ho and Wo multiples of 16, (C0 + C1) % 32 == 0,
  * K % 128 == 0, >= 128 output tiles; d->accumulate adds into d->out.  Returns 1 when the problem does not qualify. */
 int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t s);
-/* fp32 reference-layout conv weight [K][C][ks][ks] -> the space-to-depth halo tiles of fmd_conv_s2d.  mode 0: the
+/* The data gradient of a stride-2 pad-1 3x3 conv (the transposed gather of DownsampleND's conv,
+ * src/nn/ops/upsampling.py:49-56) as a stride-1 2x2 conv from the low-resolution gradient onto the depth-to-space
+ * view of the output (4 pixel classes x K channels, one class per 128-channel tile) on the halo kernel.  d as for
+ * fmd_conv with transposed = 1: Ho = 2 Hs, Wo = 2 Ws, Hs and Ws multiples of 16, (C0 + C1) % 32 == 0, K % 128 == 0,
+ * no prologue; d->wgt_tiled from fmd_s2d_tile_weights mode 2; d->accumulate adds into d->out.  Returns 1 when the
+ * problem does not qualify. */
+int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t s);
+/* fp32 reference-layout conv weight [K][C][ks][ks] -> the halo tiles of fmd_conv_s2d / fmd_conv_d2s.  mode 0: the
  * stride-2 forward (rows K, ks 3 or 4); mode 1: the 4x4 data gradient of a 3x3 conv on a nearest-x2 input
- * (rows C, inner channels K, ks 3).  The inner channel count must be a multiple of 32. */
+ * (rows C, inner channels K, ks 3); mode 2: the stride-2 3x3 data gradient (rows 4C class-major, C % 128 == 0,
+ * inner K).  The inner channel count must be a multiple of 32. */
 int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode);
 int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out, fmd_stream_t s);
 

@@ -1267,3 +1267,26 @@ def test_s2d_halo_conv_vs_torch(case):
         got, _ = O.conv(dy.to(DEV), Cin, None, ks=4, stride=2, pad=1, out_hw_=(Hl, Wl), out=out,
                         accumulate=case == "updgrad_acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 1))
         _close(got, ref)
+
+
+@pytest.mark.parametrize("case", ["plain", "acc"])
+def test_d2s_halo_dgrad_vs_torch(case):
+    """fmd_conv_d2s (csrc/conv_halo9.hip): the data gradient of DownsampleND's stride-2 3x3 conv as a 2x2 conv onto
+    the depth-to-space view of the output, vs torch autograd of F.conv2d(stride=2) on the bf16-rounded operands (the
+    acc case adds into the existing gradient)."""
+    O = ops()
+    N, H, W, C, K = 8, 128, 128, 128, 256   # input x [N, H, W, C] -> y [N, H/2, W/2, K]
+    w = _w(K, C, 3, 61)
+    dy = _rand_nhwc(N, H // 2, W // 2, K, 62)
+    x = torch.zeros(N, C, H, W, requires_grad=True)
+    F.conv2d(x, _bfw(w), stride=2, padding=1).backward(_to_nchw(dy))
+    ref = x.grad.permute(0, 2, 3, 1)
+    out = None
+    if case == "acc":
+        prev = _rand_nhwc(N, H, W, C, 63)
+        out = prev.to(DEV).clone()
+        ref = ref + prev.float()
+    assert O.d2s_eligible(N, H // 2, W // 2, H, W, C, K)
+    got, _ = O.conv(dy.to(DEV), C, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=(H, W), out=out,
+                    accumulate=case == "acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 2))
+    _close(got, ref)

@@ -38,7 +38,8 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     # (kind, N, full-resolution H, C in, K out)
     for kind, N, H, C, K in (("down", 8, 256, 128, 128), ("down", 8, 128, 256, 256), ("down", 8, 64, 256, 256),
-                             ("updgrad", 8, 256, 256, 256), ("updgrad", 8, 128, 256, 256), ("updgrad", 8, 64, 512, 512)):
+                             ("updgrad", 8, 256, 256, 256), ("updgrad", 8, 128, 256, 256), ("updgrad", 8, 64, 512, 512),
+                             ("s2dgrad", 8, 256, 128, 128), ("s2dgrad", 8, 128, 256, 256), ("s2dgrad", 8, 64, 256, 256)):
         h = H // 2
         if kind == "down":
             x = torch.randn(N, H, H, C, device=dev, generator=g).to(torch.bfloat16)
@@ -48,6 +49,14 @@ def main():
             gen = lambda: O.conv(x, K, wg, ks=3, stride=2, pad=1)
             s2d = (lambda: O.conv(x, K, None, ks=3, stride=2, pad=1, s2d_tiled=ws)) \
                 if O.s2d_eligible(N, H, H, h, h, K, C, 3) else None
+        elif kind == "s2dgrad":   # data gradient of the stride-2 conv x [N, H, H, C] -> y [N, h, h, K]
+            dy = torch.randn(N, h, h, K, device=dev, generator=g).to(torch.bfloat16)
+            w = torch.randn(K, C, 3, 3, device=dev, generator=g) / math.sqrt(9 * C)
+            wg, ws = O.prep_weights(w, 1), O.s2d_tile_weights(w, 2)
+            flops = 2 * N * h * h * K * C * 9
+            gen = lambda: O.conv(dy, C, wg, ks=3, stride=2, pad=1, transposed=True, out_hw_=(H, H))
+            s2d = (lambda: O.conv(dy, C, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=(H, H), s2d_tiled=ws)) \
+                if O.d2s_eligible(N, h, h, H, H, C, K) else None
         else:   # data gradient of conv3x3(nearest_x2(x)): x [N, h, h, C] -> conv output K channels at H
             dy = torch.randn(N, H, H, K, device=dev, generator=g).to(torch.bfloat16)
             w = torch.randn(K, C, 3, 3, device=dev, generator=g) / math.sqrt(9 * C)
