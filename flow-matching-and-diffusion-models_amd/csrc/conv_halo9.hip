@@ -42,6 +42,9 @@ constexpr int ZFLAG = 1 << 30;         // staged-piece flag: store zeros (paddin
 #define FMD_H9_SCHED 1
 #endif
 constexpr bool H9_SCHED = FMD_H9_SCHED;   // v9b: pinned read/MFMA interleave of a tap (build flag for A/B)
+#ifndef FMD_H9_LAG
+#define FMD_H9_LAG 3   // taps between a staging round's load and its transform (2: 22.94 / 23.00 vs 3: 22.89 / 22.89 ms per train step)
+#endif
 
 template <bool UP>
 struct G9 {
@@ -648,7 +651,8 @@ void conv3x3_halo9b(const HArgs A) {
   static_assert(!(MODE && UP), "stride-2 modes are not nearest-x2 gathers");
   constexpr int NTAP = MODE ? 4 : 9;         // taps per chunk
   constexpr int RPT = MODE ? 2 : 1;          // staging rounds loaded per tap
-  constexpr int LAG = MODE ? 1 : 2;          // taps between a round's load and its transform + store
+  constexpr int LAG = MODE ? 1 : FMD_H9_LAG;  // taps between a round's load and its transform + store
+  constexpr int SL = RPT * LAG;              // staging register slots (rounds in flight)
   constexpr int RB = MODE ? 4 : 3;           // B-fragment ring (NTAP % RB == 0 keeps its phase per chunk)
   static_assert(NTAP % RB == 0 && (NR + RPT - 1) / RPT + LAG <= NTAP, "chunk pipeline");
   constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
@@ -780,21 +784,21 @@ void conv3x3_halo9b(const HArgs A) {
       scb = ZCOEF;
     }
   };
-  u32x4 rh[2];
-  int roff[2];
+  u32x4 rh[SL];
+  int roff[SL];
   // staging round q of a 3x3 chunk (1x1 chunks: stage_seg2)
   auto load_round = [&](int q) {
     const int sp = spix[q];
     const bool valid = sok && sp >= 0;
     const bf16r* src = valid ? sbase + (size_t)(simg + sp) * scs : s0;
-    rh[q & 1] = HDBG9(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
+    rh[q % SL] = HDBG9(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
     // GN prologue: padding positions were zeroed once (their store goes to the dummy slot) and invalid channels /
     // depth slices meet zero coefficients, so the transform needs no select
     const int dst = sdst0 + q * 1024;
-    roff[q & 1] = sp == -2 ? DUMMY : PRO != 0 ? (sp >= 0 ? dst : DUMMY) : (dst | (valid ? 0 : ZFLAG));
+    roff[q % SL] = sp == -2 ? DUMMY : PRO != 0 ? (sp >= 0 ? dst : DUMMY) : (dst | (valid ? 0 : ZFLAG));
   };
   auto transform = [&](int q) -> u32x4 {
-    const u32x4 raw = rh[q & 1];
+    const u32x4 raw = rh[q % SL];
     u32x4 v = raw;
     if (PRO != 0 && !HDBG9(2)) {
       const f32x4 a0 = *(const f32x4*)(coef + sca), a1 = *(const f32x4*)(coef + sca + 4);
@@ -809,7 +813,7 @@ void conv3x3_halo9b(const HArgs A) {
         v[e] = pack2(lo, hi);
       }
     } else {
-      const bool z = (roff[q & 1] & ZFLAG) != 0;
+      const bool z = (roff[q % SL] & ZFLAG) != 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
     }
@@ -913,15 +917,15 @@ void conv3x3_halo9b(const HArgs A) {
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
       load_round(q);
-      pv[q] = rh[q & 1];
-      po[q] = roff[q & 1];
+      pv[q] = rh[q % SL];
+      po[q] = roff[q % SL];
     }
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
-      rh[q & 1] = pv[q];
-      roff[q & 1] = po[q];
+      rh[q % SL] = pv[q];
+      roff[q % SL] = po[q];
       const u32x4 v = transform(q);
-      *(u32x4*)(smem + (c_lo & 1) * HBUF + (roff[q & 1] & ~ZFLAG)) = v;
+      *(u32x4*)(smem + (c_lo & 1) * HBUF + (roff[q % SL] & ~ZFLAG)) = v;
     }
   }
   __syncthreads();
@@ -952,7 +956,7 @@ void conv3x3_halo9b(const HArgs A) {
           const int q = (t - LAG) * RPT + j;
           if (t >= LAG && q < NR) {
             const u32x4 v = transform(q);
-            *(u32x4*)(smem + nb + (roff[q & 1] & ~ZFLAG)) = v;
+            *(u32x4*)(smem + nb + (roff[q % SL] & ~ZFLAG)) = v;
           }
         }
 #pragma unroll
