@@ -309,6 +309,57 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const WArgs A, int splits, i
   }
 }
 
+// Combine with all T taps of (k, 64 channels) per block and the slabs spread over SL slab lanes, so every form
+// of the problem keeps the block busy: items (tap, 4-channel quad) x SL lanes <= 512 threads, each lane summing
+// slabs sl, sl + SL, ... (of the nsl slabs at stride sstride) as 16-byte loads in four chains; the lanes are then
+// combined in fixed order through LDS and written transposed to the reference dW[k][c][tap] layout.
+// Deterministic.  T <= 27, C % 4 == 0, blockDim 512.
+__global__ __launch_bounds__(512) void wgrad_reduce2(const WArgs A, int splits, int nsl, int sstride, int SL) {
+  const fmd_wgrad_desc& d = A.d;
+  __shared__ __attribute__((aligned(16))) float part[512 * 4];   // [sl][tap][64 c]
+  const size_t per = (size_t)d.K * A.T * A.C;
+  const int k = blockIdx.x, c0 = blockIdx.y * RC;
+  const int items = 16 * A.T;
+  const int t = threadIdx.x;
+  if (t < items * SL) {
+    const int sl = t / items, it = t - sl * items;
+    const int tap = it >> 4, cq = it & 15;
+    const int c = c0 + cq * 4;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (c < A.C) {
+      const float* src = d.ws + ((size_t)k * A.T + tap) * A.C + c;
+      const size_t st = (size_t)SL * sstride * per;
+      const float* p = src + (size_t)sl * sstride * per;
+      int s = sl;
+      for (; s + 3 * SL < nsl; s += 4 * SL, p += 4 * st) {
+        a0 += *(const f32x4*)p;
+        a1 += *(const f32x4*)(p + st);
+        a2 += *(const f32x4*)(p + 2 * st);
+        a3 += *(const f32x4*)(p + 3 * st);
+      }
+      for (; s < nsl; s += SL, p += st) a0 += *(const f32x4*)p;
+    }
+    *(f32x4*)&part[((size_t)sl * A.T + tap) * 64 + cq * 4] = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
+  const int nc = min(RC, A.C - c0);
+  float* out = d.dw + ((size_t)k * A.C + c0) * A.T;
+  for (int e = t; e < nc * A.T; e += blockDim.x) {
+    const int cl = e / A.T, tap = e - cl * A.T;
+    float v = part[tap * 64 + cl];
+    for (int sl = 1; sl < SL; ++sl) v += part[((size_t)sl * A.T + tap) * 64 + cl];
+    out[e] = d.accumulate ? out[e] + v : v;
+  }
+  if (d.db && blockIdx.y == 0 && t < 64) {
+    const float* wb = d.ws + (size_t)splits * per;
+    float v = 0.f;
+    for (int s = t; s < nsl; s += 64) v += wb[(size_t)s * sstride * d.K + k];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    if (t == 0) d.db[k] = d.accumulate ? d.db[k] + v : v;
+  }
+}
+
 WArgs make_args(const fmd_wgrad_desc* d) {
   WArgs A;
   A.d = *d;
@@ -350,6 +401,23 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   }
   if (rc) return rc;
   const size_t per = (size_t)d->K * A.T * A.C;
+  // FMD_WGRAD_REDUCE (A/B runs): 1 (default) = wgrad_reduce2 in one pass (train step 22.61 -> 22.20 ms),
+  // 0 = stage 1 (> 8 splits) + wgrad_reduce (round 3), 2 = stage 1 + wgrad_reduce2
+  static const int red_mode = [] {
+    const char* e = getenv("FMD_WGRAD_REDUCE");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (A.T > 27) return -4;
+  auto final_pass = [&](int nsl_, int sstride_) {
+    if (red_mode && A.C % 4 == 0) {
+      const int sl = max(1, min(nsl_, 512 / (16 * A.T)));
+      hipLaunchKernelGGL(wgrad_reduce2, dim3(d->K, (A.C + RC - 1) / RC), dim3(512), 0, s, A, splits, nsl_, sstride_, sl);
+    } else {
+      hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl_, sstride_);
+    }
+    return (int)hipGetLastError();
+  };
+  if (red_mode == 1 && A.C % 4 == 0) return final_pass(splits, 1);
   const int vblocks = (int)((per / 4 + 255) / 256);
   int nsl = splits, sstride = 1;
   if (splits > 8) {   // two stages: enough threads in flight for a wide split
@@ -361,7 +429,5 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
     if (rc) return rc;
   }
-  if (A.T > 27) return -4;
-  hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl, sstride);
-  return (int)hipGetLastError();
+  return final_pass(nsl, sstride);
 }

@@ -134,6 +134,41 @@ def test_conv_splitk_fused_stats(ep):
     torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("shape", ["tiny32", "small64", "big128", "k64", "k192_ep", "acc_f32"])
+def test_conv_splitk_last_arriver(shape, monkeypatch):
+    """The in-launch last-arriver split-K combine (conv_igemm + d.splitk_ctr) sums the slabs in the same fixed
+    order as the separate splitk_reduce_rows kernel: outputs and statistics must be bit-identical, and the
+    tile counters must be left zeroed (a second launch gives the same result)."""
+    O = ops()
+    N, H, W, C, K = {"tiny32": (2, 4, 4, 256, 256), "small64": (2, 16, 16, 256, 256), "big128": (4, 32, 32, 128, 256),
+                     "k64": (2, 8, 8, 256, 64), "k192_ep": (2, 16, 16, 256, 192), "acc_f32": (2, 8, 8, 256, 128)}[shape]
+    x = _rand_nhwc(N, H, W, C, 51).to(DEV)
+    wp = O.prep_weights(_w(K, C, 3, 52).to(DEV), 0)
+    g = torch.Generator().manual_seed(53)
+    kw = dict(bias=(torch.randn(K, generator=g) * 0.1).to(DEV), force_generic=True, splits=5)
+    if shape == "acc_f32":
+        kw.update(out_f32=True, accumulate=True)
+    else:
+        kw.update(bias_nc=(torch.randn(N, K, generator=g) * 0.1).to(DEV), want_stats=True)
+    if shape == "k192_ep":
+        kw.update(ep=(_rand_nhwc(N, H, W, K, 54).to(DEV), None, (torch.rand(N, K, generator=g) + 0.5).to(DEV),
+                      (torch.randn(N, K, generator=g) * 0.2).to(DEV)))
+    init = torch.randn(N, H, W, K, generator=g).to(DEV)
+    res = []
+    for fuse in (False, True, True):
+        monkeypatch.setattr(O, "SPLITK_FUSE", fuse)
+        out = init.clone() if shape == "acc_f32" else None
+        y, st = O.conv(x, K, wp, out=out, **kw)
+        torch.cuda.synchronize()
+        res.append((y, st))
+    for y, st in res[1:]:
+        assert torch.equal(y, res[0][0])
+        if st is not None:
+            assert torch.equal(st.slab, res[0][1].slab)
+    for ctr in O._SPLITK_CTR.values():
+        assert int(ctr.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "s2_split"])
 def test_conv_data_gradient(mode):
     """Data gradients through the generic implicit GEMM; s2 runs the parity-class decomposition of the
@@ -193,6 +228,31 @@ def test_wgrad(mode):
             pad=pad, upsample=up, pro=pro, db=db, force_generic=generic)
     torch.testing.assert_close(dw.cpu(), w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
     torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("splits,generic", [(3, False), (20, False), (64, False), (37, True)])
+def test_wgrad_split_combine(splits, generic):
+    """The weight-gradient split-K combine (wgrad_reduce / wgrad_reduce2, FMD_WGRAD_REDUCE): wide splits (more than 16 slab lanes), accumulate into
+    dW/db, vs torch; repeated runs are bit-identical (fixed summation order)."""
+    O = ops()
+    N, H, W, C, K = 4, 32, 32, 64, 128
+    xb = _rand_nhwc(N, H, W, C, 61)
+    w = _w(K, C, 3, 62).requires_grad_()
+    bias = torch.zeros(K, requires_grad=True)
+    y = F.conv2d(_to_nchw(xb), w, bias, padding=1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+    g = torch.Generator().manual_seed(63)
+    dw0, db0 = torch.randn(K, C, 3, 3, generator=g), torch.randn(K, generator=g)
+    outs = []
+    for _ in range(2):
+        dw, db = dw0.clone().to(DEV), db0.clone().to(DEV)
+        O.wgrad(xb.to(DEV), dyn, dw, db=db, accumulate=True, splits=splits, force_generic=generic)
+        outs.append((dw.cpu(), db.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[0][0] - dw0, w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
+    torch.testing.assert_close(outs[0][1] - db0, bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
 
 
 @pytest.mark.parametrize("case", ["concat_pro", "wide_dy_offset", "many_tiles"])
