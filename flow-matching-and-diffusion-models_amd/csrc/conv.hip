@@ -35,16 +35,11 @@ struct KArgs {
                   // decomposition: only the 1/2/2/4 taps that hit a class are iterated, not all 9; in 3-D
                   // 8 classes of 1..8 of the 27 taps)
   int Mfull;      // N*Ho*Wo (== M unless par)
-  int fuse;       // split-K: the last-arriving split of a tile combines it (combine_row16) -- d.splitk_ctr
-  float* fstats;  // statistics slab of the fused combine (d.stats is cleared for the main loop)
   int pack;       // 1: the input has exactly 8 (padded) channels -- one 16-byte chunk per tap -- and a K-iteration
                   // covers BK/8 consecutive TAPS (chunk j = tap kk*BK/8 + j, channels 0..7) instead of BK
                   // channels of one tap: the UNet's input conv and the 1-channel head's data gradient (K = 9
                   // or 27 taps x 8) run in ceil(T/(BK/8)) K-iterations, not T (7/8 of each was zero padding)
 };
-
-__device__ __forceinline__ void combine_row16(const fmd_conv_desc& d, float* stats, int M, int row, int cblk,
-                                              float (*red)[64][2], bool tail_sync);
 
 template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
 __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
@@ -330,31 +325,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
         }
       }
     }
-    if (BCO % 64 || !A.fuse) return;
-    // last-arriver combine: the split that completes a tile sums all slabs of the tile in fixed split order
-    // (the same arithmetic as splitk_reduce_rows, so results do not depend on arrival order) and runs the
-    // epilogue.  Counters are vector atomics on d.splitk_ctr[tile]; the last arriver re-zeroes its counter.
-    __threadfence();   // release this split's slab rows
-    __syncthreads();
-    int* flag = (int*)(lds + 2048);   // past red[] below (the main loop's tiles are done)
-    if (tid == 0) {
-      const int old = atomicAdd(d.splitk_ctr + blockIdx.x, 1);
-      const int last = old == (int)gridDim.y - 1;
-      if (last) atomicExch(d.splitk_ctr + blockIdx.x, 0);
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    __threadfence();   // acquire the other splits' rows
-    float(*red)[64][2] = (float(*)[64][2])lds;
-    const int rows = min(BPX, A.M - px0) / FMD_SPLIT_STATS_ROWS;
-#pragma unroll 1
-    for (int cb = 0; cb < BCO / 64; ++cb) {
-      if (co0 + cb * 64 >= K) break;
-#pragma unroll 1
-      for (int r = 0; r < rows; ++r)
-        combine_row16(d, A.fstats, A.Mfull, px0 / FMD_SPLIT_STATS_ROWS + r, co0 / 64 + cb, red, true);
-    }
     return;
   }
 
@@ -610,18 +580,15 @@ __global__ void splitk_reduce(const fmd_conv_desc d, int M) {
 // rounded output (sum v, sum v^2 -- or sum v*x with the data-gradient epilogue) written as slab row p/16
 // (FMD_SPLIT_STATS_ROWS), so no separate statistics pass is needed.  Split-K only runs on the small
 // levels: 16-pixel rows give enough blocks there.  Needs K % 4 == 0 and M % 16 == 0.
-// One (16-pixel row, 64-channel block) of the combine; red = 4*64*2 floats of LDS.  Block-uniform
-// arguments (it holds a barrier when stats are written); tail_sync: a trailing barrier so the caller may
-// reuse red at once.
-__device__ __forceinline__ void combine_row16(const fmd_conv_desc& d, float* stats, int M, int row, int cblk,
-                                              float (*red)[64][2], bool tail_sync) {
+__global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d, int M) {
   const int K = d.K;
   const int HWo = (d.Do > 0 ? d.Do : 1) * d.Ho * d.Wo;
   const size_t total = (size_t)M * K;
   constexpr int RP = FMD_SPLIT_STATS_ROWS;
+  const int row = blockIdx.x;
   const int tq = threadIdx.x & 15, pl = threadIdx.x >> 4;
   static_assert(RP == 16, "one pixel per 16-lane group");
-  const int c = cblk * 64 + tq * 4;
+  const int c = blockIdx.y * 64 + tq * 4;
   const bool cok = c < K;
   const bool hasx = d.ep_x0 != nullptr;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
@@ -685,8 +652,9 @@ __device__ __forceinline__ void combine_row16(const fmd_conv_desc& d, float* sta
       }
     }
   }
-  if (!stats) return;
+  if (!d.stats) return;
   // lanes tq, tq+16, tq+32, tq+48 of a wave hold the same channels (4 pixels); then the 4 waves via LDS
+  __shared__ float red[4][64][2];
 #pragma unroll
   for (int r2 = 0; r2 < 4; ++r2) {
     s1[r2] += __shfl_xor(s1[r2], 16, 64);
@@ -702,25 +670,16 @@ __device__ __forceinline__ void combine_row16(const fmd_conv_desc& d, float* sta
   __syncthreads();
   if (threadIdx.x < 128) {
     const int cl = threadIdx.x >> 1, k = threadIdx.x & 1;
-    const int cc = cblk * 64 + cl;
+    const int cc = blockIdx.y * 64 + cl;
     if (cc < K)
-      stats[((size_t)row * K + cc) * 2 + k] = (red[0][cl][k] + red[1][cl][k]) + (red[2][cl][k] + red[3][cl][k]);
+      d.stats[((size_t)row * K + cc) * 2 + k] = (red[0][cl][k] + red[1][cl][k]) + (red[2][cl][k] + red[3][cl][k]);
   }
-  if (tail_sync) __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d, int M) {
-  __shared__ float red[4][64][2];
-  combine_row16(d, d.stats, M, blockIdx.x, blockIdx.y, red, false);
 }
 
 template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
-int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = nullptr, float* fstats = nullptr,
-           bool* fused = nullptr) {
+int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = nullptr) {
   KArgs A;
   A.d = *d;
-  A.fuse = 0;
-  A.fstats = fstats;
   if (g) A.g = *g;
   const int Dz = d->Do > 0 ? d->Do : 1;
   A.M = d->N * Dz * d->Ho * d->Wo;
@@ -747,9 +706,6 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
       return -11;
   }
   dim3 grid(A.ntp * A.ntc, splits, A.par ? (d->Do > 0 ? 8 : 4) : 1);
-  // fused split-K combine: whole 16-pixel rows per tile (BPX % 16, M % 16 checked by the caller), no parity classes
-  A.fuse = fused && d->splitk_ctr && splits > 1 && !A.par && BCO % 64 == 0 && !GNA && (int)grid.x <= FMD_SPLITK_CTR_MAX;
-  if (fused) *fused = A.fuse;
   hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);
   return (int)hipGetLastError();
 }
@@ -782,8 +738,6 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
   (void)C;
   fmd_conv_desc dm = *d;
   if (d->splits > 1) dm.stats = nullptr;
-  bool fused = false;
-  bool* fz = d->splits > 1 && rows_ok ? &fused : nullptr;   // the fused combine needs the 16-pixel-row layout
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
     rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
@@ -793,16 +747,16 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
     if (d->K <= 16)
       rc = launch<16, 256, 1, 4, 64>(&dm, s);
     else if (d->K <= 64)
-      rc = launch<64, 128, 2, 2, 64>(&dm, s, nullptr, d->stats, fz);
+      rc = launch<64, 128, 2, 2, 64>(&dm, s);
     else if (M <= tiny_m && d->splits > 1)    // tinier: 32-pixel tiles
-      rc = launch<128, 32, 2, 2, 64>(&dm, s, nullptr, d->stats, fz);
+      rc = launch<128, 32, 2, 2, 64>(&dm, s);
     else if (M <= small_m && d->splits > 1)   // tiny levels: 64-pixel tiles, half the split-K slabs
-      rc = launch<128, 64, 2, 2, 64>(&dm, s, nullptr, d->stats, fz);
+      rc = launch<128, 64, 2, 2, 64>(&dm, s);
     else
-      rc = launch<128, 128, 2, 2, 64>(&dm, s, nullptr, d->stats, fz);
+      rc = launch<128, 128, 2, 2, 64>(&dm, s);
   }
   if (rc) return rc;
-  if (d->splits > 1 && !fused) {
+  if (d->splits > 1) {
     if (rows_ok) {
       hipLaunchKernelGGL(splitk_reduce_rows, dim3(M / FMD_SPLIT_STATS_ROWS, (d->K + 63) / 64), dim3(256), 0, s, *d, M);
     } else {

@@ -28,7 +28,7 @@ class ConvDesc(C.Structure):
         ("bias", p), ("bias2", p), ("bias_nc", p), ("resid", p), ("out", p), ("out_f32", i32), ("accumulate", i32),
         ("stats", p), ("ep_x0", p), ("ep_x1", p), ("ep_C0", i32), ("ep_a", p), ("ep_b", p),
         ("ws", p), ("splits", i32), ("force_generic", i32), ("wgt_tiled", p), ("wgt2_tiled", p),
-        ("Ds", i32), ("Do", i32), ("gout", p), ("splitk_ctr", p),
+        ("Ds", i32), ("Do", i32), ("gout", p),
     ]
 
 
@@ -51,7 +51,6 @@ class GnApplyDesc(C.Structure):
 
 
 LINCOMB_MAX = 6   # FMD_LINCOMB_MAX
-SPLITK_CTR_MAX = 16384   # FMD_SPLITK_CTR_MAX
 
 
 class LincombDesc(C.Structure):

@@ -206,22 +206,6 @@ BPX64_M = int(os.environ.get("FMD_BPX64_M", "2048") or 0)
 BPX32_M = int(os.environ.get("FMD_BPX32_M", "128") or 0)
 
 
-# split-K tile counters of the fused last-arriver combine (csrc/conv.hip conv_igemm): one zeroed int32 set per
-# (device, stream), left zeroed by every launch.  FMD_SPLITK_FUSE=0: the separate combine kernel (A/B runs)
-SPLITK_FUSE = os.environ.get("FMD_SPLITK_FUSE", "1") == "1"
-_SPLITK_CTR = {}
-
-
-def _splitk_ctr(dev):
-    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
-    buf = _SPLITK_CTR.get(key)
-    if buf is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None   # not allocated inside a graph capture: that launch uses the separate combine
-        buf = _SPLITK_CTR[key] = torch.zeros(_lib.SPLITK_CTR_MAX, device=dev, dtype=torch.int32)
-    return buf
-
-
 def _choose_splits(M, K, nk, bpx=128, bco=128):
     tiles = -(-M // bpx) * -(-K // bco)
     if tiles >= NUM_CU or nk < 8:
@@ -413,8 +397,6 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     if splits > 1:
         ws = torch.empty((splits, M, K), device=dev, dtype=F32)
         d.ws, d.splits = _p(ws), splits
-        if SPLITK_FUSE:
-            d.splitk_ctr = _p(_splitk_ctr(dev))
     else:
         d.splits = 1
     st = None

@@ -79,10 +79,6 @@ typedef struct fmd_conv_desc {
                                halo path -- the weight gradient's operand, so the backward does not recompute
                                the GroupNorm+SiLU.  Requires pro_a, (C0+C1) % 32 == 0 and the halo path (fmd_conv
                                returns -9 otherwise); NULL = off */
-  int32_t* splitk_ctr;      /* optional zeroed int32 [FMD_SPLITK_CTR_MAX] tile counters (one set per stream): with
-                               splits > 1 on the implicit-GEMM path the last-arriving split of each tile combines
-                               the slabs in fixed split order and runs the epilogue in the same launch (no
-                               split-K combine kernel); counters are left zeroed.  NULL = separate combine */
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the
@@ -116,7 +112,6 @@ int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_st
 
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
-#define FMD_SPLITK_CTR_MAX 16384  /* tiles covered by fmd_conv_desc.splitk_ctr */
 /* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv
  * (default 128; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
  * halo_splits mirror reads the same variable. */

@@ -134,41 +134,6 @@ def test_conv_splitk_fused_stats(ep):
     torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("shape", ["tiny32", "small64", "big128", "k64", "k192_ep", "acc_f32"])
-def test_conv_splitk_last_arriver(shape, monkeypatch):
-    """The in-launch last-arriver split-K combine (conv_igemm + d.splitk_ctr) sums the slabs in the same fixed
-    order as the separate splitk_reduce_rows kernel: outputs and statistics must be bit-identical, and the
-    tile counters must be left zeroed (a second launch gives the same result)."""
-    O = ops()
-    N, H, W, C, K = {"tiny32": (2, 4, 4, 256, 256), "small64": (2, 16, 16, 256, 256), "big128": (4, 32, 32, 128, 256),
-                     "k64": (2, 8, 8, 256, 64), "k192_ep": (2, 16, 16, 256, 192), "acc_f32": (2, 8, 8, 256, 128)}[shape]
-    x = _rand_nhwc(N, H, W, C, 51).to(DEV)
-    wp = O.prep_weights(_w(K, C, 3, 52).to(DEV), 0)
-    g = torch.Generator().manual_seed(53)
-    kw = dict(bias=(torch.randn(K, generator=g) * 0.1).to(DEV), force_generic=True, splits=5)
-    if shape == "acc_f32":
-        kw.update(out_f32=True, accumulate=True)
-    else:
-        kw.update(bias_nc=(torch.randn(N, K, generator=g) * 0.1).to(DEV), want_stats=True)
-    if shape == "k192_ep":
-        kw.update(ep=(_rand_nhwc(N, H, W, K, 54).to(DEV), None, (torch.rand(N, K, generator=g) + 0.5).to(DEV),
-                      (torch.randn(N, K, generator=g) * 0.2).to(DEV)))
-    init = torch.randn(N, H, W, K, generator=g).to(DEV)
-    res = []
-    for fuse in (False, True, True):
-        monkeypatch.setattr(O, "SPLITK_FUSE", fuse)
-        out = init.clone() if shape == "acc_f32" else None
-        y, st = O.conv(x, K, wp, out=out, **kw)
-        torch.cuda.synchronize()
-        res.append((y, st))
-    for y, st in res[1:]:
-        assert torch.equal(y, res[0][0])
-        if st is not None:
-            assert torch.equal(st.slab, res[0][1].slab)
-    for ctr in O._SPLITK_CTR.values():
-        assert int(ctr.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "s2_split"])
 def test_conv_data_gradient(mode):
     """Data gradients through the generic implicit GEMM; s2 runs the parity-class decomposition of the
