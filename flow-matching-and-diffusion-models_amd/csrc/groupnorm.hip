@@ -69,6 +69,45 @@ __global__ void channel_stats_kernel(const bf16r* __restrict__ x, const bf16r* _
   }
 }
 
+// Slab fold: out row j = sum of slab rows [j*fold, (j+1)*fold) (C channels x 2 sums each), a block per output
+// row reading whole slab rows as coalesced 16-byte vectors, 4 chains per row lane, lanes combined in fixed
+// order.  The (n, group) reductions below read a group's Cg channels (16-64 B of each 0.5-4 KiB slab row) from
+// every row: on config E's single-sample 128^3 levels (32768 rows of 64 pixels, 32 blocks) that ran at
+// < 1 TB/s and 105-293 us per call; folding first leaves them 256 rows.
+__global__ __launch_bounds__(256) void stats_fold_kernel(const float* __restrict__ in, int C, int fold,
+                                                         float* __restrict__ out) {
+  const int V = C / 2;   // 16-byte vectors per slab row
+  const size_t r0 = (size_t)blockIdx.x * fold;
+  __shared__ f32x4 red[256];
+  const int t = threadIdx.x;
+  for (int vb = 0; vb < V; vb += 256) {
+    const int nv = min(256, V - vb);
+    const int R = 256 / nv;   // row lanes
+    const int v = t % nv, rl = t / nv;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (rl < R) {
+      const size_t st = (size_t)R * V;   // f32x4 between a lane's consecutive rows
+      const f32x4* p = (const f32x4*)in + (r0 + rl) * V + vb + v;
+      int r = rl;
+      for (; r + 3 * R < fold; r += 4 * R, p += 4 * st) {
+        a0 += p[0];
+        a1 += p[st];
+        a2 += p[2 * st];
+        a3 += p[3 * st];
+      }
+      for (; r < fold; r += R, p += st) a0 += p[0];
+    }
+    red[t] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (t < nv) {
+      f32x4 sum = red[t];
+      for (int k = 1; k < R; ++k) sum += red[k * nv + t];
+      ((f32x4*)out)[(size_t)blockIdx.x * V + vb + t] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 // one block per (n, group)
 __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const float* __restrict__ st1, int rows1,
                                int N, int HW, int C0, int C1, int G, float eps, const float* __restrict__ gamma,
@@ -384,6 +423,15 @@ extern "C" int fmd_channel_stats(const void* x, const void* y0, const void* y1, 
   return (int)hipGetLastError();
 }
 
+
+extern "C" int fmd_stats_fold(const float* slab, int64_t rows_total, int32_t C, int32_t fold, float* out,
+                              fmd_stream_t s) {
+  if (C < 2 || C % 2 || fold < 1 || rows_total % fold || ((size_t)slab & 15) || ((size_t)out & 15)) return -1;
+  if (rows_total / fold > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL(stats_fold_kernel, dim3((unsigned)(rows_total / fold)), dim3(256), 0, (hipStream_t)s, slab, C,
+                     fold, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int fmd_gn_prep(const float* st0, int32_t rows0, const float* st1, int32_t rows1, int32_t N, int32_t HW,
                            int32_t C0, int32_t C1, int32_t G, float eps, const float* gamma, const float* beta,

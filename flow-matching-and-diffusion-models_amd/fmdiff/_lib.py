@@ -90,6 +90,7 @@ SIGNATURES = {
     "fmd_s2d_tiled_size": [i32, i32, i32],
     "fmd_s2d_tile_weights": [p, i32, i32, i32, i32, p, p],
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],
+    "fmd_stats_fold": [p, i64, i32, i32, p, p],
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
     "fmd_gn_bwd_prep": [p, i32, i32, i32, i32, i32, p, p, p, p, i32, i32, p, p, p, p, p, p, i32, p, i32, p, p],
     "fmd_gn_apply_fwd": [p, p, i32, i32, i64, i32, p, p, i32, p, p],

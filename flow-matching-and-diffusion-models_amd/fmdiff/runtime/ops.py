@@ -56,9 +56,30 @@ def channel_stats(x: torch.Tensor, rows: Optional[int] = None, y: Tuple = None) 
     return Stats(slab, rows)
 
 
+# slabs with at least STATS_FOLD_MIN rows per image are folded STATS_FOLD rows at a time before the GroupNorm
+# (n, group) reductions (fmd_stats_fold): config E's 128^3 levels (32768 rows of 64 pixels)
+STATS_FOLD_MIN = int(os.environ.get("FMD_STATS_FOLD_MIN", "4096") or 0)
+STATS_FOLD = 128
+
+
+def fold_stats(st: Optional[Stats], HW: int) -> Optional[Stats]:
+    """``st`` with STATS_FOLD consecutive slab rows summed (same per-image sums), or ``st`` itself when small."""
+    if st is None or not STATS_FOLD_MIN:
+        return st
+    E = HW // st.rows
+    C = st.slab.shape[1]
+    if E < STATS_FOLD_MIN or E % STATS_FOLD or C % 2 or not st.slab.is_contiguous():
+        return st
+    rows_total = st.slab.shape[0]
+    out = torch.empty((rows_total // STATS_FOLD, C, 2), device=st.slab.device, dtype=F32)
+    _lib.call("fmd_stats_fold", _p(st.slab), rows_total, C, STATS_FOLD, _p(out), stream())
+    return Stats(out, st.rows * STATS_FOLD)
+
+
 def gn_prep(st0: Stats, st1: Optional[Stats], N: int, HW: int, C0: int, C1: int, groups: int, eps: float,
             gamma, beta, emb=None, emb_stride=0, emb_mode=0):
     """Fold GroupNorm (+ scale/shift) into a[n][c], b[n][c]; returns (a, b, mean_rstd)."""
+    st0, st1 = fold_stats(st0, HW), fold_stats(st1, HW)
     dev = st0.slab.device
     Ct = C0 + C1
     a = torch.empty((N, Ct), device=dev, dtype=F32)
@@ -95,6 +116,7 @@ def gb_flush():
 
 def gn_bwd_prep(s12: Stats, N: int, HW: int, Ct: int, groups: int, mr, gamma, beta, dgamma, dbeta,
                 emb=None, emb_stride=0, emb_mode=0, demb=None, demb_stride=0, fwd: Optional[Stats] = None):
+    s12, fwd = fold_stats(s12, HW), fold_stats(fwd, HW)
     dev = s12.slab.device
     P = torch.empty((N, Ct), device=dev, dtype=F32)
     Q = torch.empty((N, Ct), device=dev, dtype=F32)

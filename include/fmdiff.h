@@ -191,6 +191,10 @@ int64_t fmd_wgrad_workspace(const fmd_wgrad_desc* d);
  * the conv prologue. */
 int fmd_channel_stats(const void* x, const void* y0, const void* y1, int32_t C0, int32_t N, int32_t HW, int32_t C,
                       int32_t rows, float* out /* [N*HW/rows][C][2] */, fmd_stream_t s);
+/* Slab fold: out[j] = sum of slab rows [j*fold, (j+1)*fold) of a [rows_total][C][2] statistics slab (fold must not
+ * straddle images: (HW/rows) % fold == 0).  Used before fmd_gn_prep / fmd_gn_bwd_prep on slabs with thousands of
+ * rows per image (config E's 128^3 levels). */
+int fmd_stats_fold(const float* slab, int64_t rows_total, int32_t C, int32_t fold, float* out, fmd_stream_t s);
 int fmd_gn_prep(const float* st0, int32_t rows0, const float* st1, int32_t rows1, int32_t N, int32_t HW,
                 int32_t C0, int32_t C1, int32_t G, float eps, const float* gamma, const float* beta,
                 const float* emb, int32_t emb_stride, int32_t emb_mode /*0 none,1 scale-shift*/,

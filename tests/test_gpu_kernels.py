@@ -257,8 +257,30 @@ def test_wgrad_halo_vs_torch(case):
     torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
 
 
-def test_groupnorm_forward_backward():
+@pytest.mark.parametrize("C,rows_img,N", [(128, 32768, 1), (384, 4096, 2), (1030, 512, 1), (6, 256, 3)])
+def test_stats_fold(C, rows_img, N):
+    """fmd_stats_fold: 128 consecutive slab rows summed (row-lane chains + fixed-order lane combine) vs torch."""
     O = ops()
+    g = torch.Generator().manual_seed(C)
+    slab = torch.randn(N * rows_img, C, 2, generator=g).to(DEV)
+    st = O.fold_stats(O.Stats(slab, 64), rows_img * 64) if rows_img >= O.STATS_FOLD_MIN else None
+    out = torch.empty(N * rows_img // 128, C, 2, device=DEV)
+    from fmdiff import _lib
+    _lib.call("fmd_stats_fold", slab.data_ptr(), N * rows_img, C, 128, out.data_ptr(), O.stream())
+    ref = slab.view(-1, 128, C, 2).double().sum(1).float()
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    if st is not None:
+        assert st.rows == 64 * 128 and torch.equal(st.slab, out)
+
+
+@pytest.mark.parametrize("fold", [False, True])
+def test_groupnorm_forward_backward(fold, monkeypatch):
+    """GroupNorm forward / backward through the slab statistics path; ``fold`` runs the slabs through
+    fmd_stats_fold first (forced on this small problem)."""
+    O = ops()
+    if fold:
+        monkeypatch.setattr(O, "STATS_FOLD_MIN", 2)
+        monkeypatch.setattr(O, "STATS_FOLD", 2)
     N, H, W, C, G = 2, 16, 16, 96, 32
     xb = _rand_nhwc(N, H, W, C, 15, 2.0) .float().add(0.5).to(torch.bfloat16)
     x = _to_nchw(xb).requires_grad_()
