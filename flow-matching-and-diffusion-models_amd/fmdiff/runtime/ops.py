@@ -584,9 +584,10 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
             base = (K // 128) * (Ct // 64) * zt
             splits = max(1, min(tiles, -(-WGRAD_HALO_WG // base), (WGRAD_SLAB_MB << 20) // (K * Ct * 36 * zt)))
         else:
-            # narrow stems (Ct * taps <= 128) put every (tap, cin) pair in one column tile
+            # narrow inputs (Ct < 128, T > 1) tile the flattened (tap, cin) pairs (csrc/wgrad.hip make_args
+            # ``merged``): ceil(T * Ct / 128) column tiles -- the 3-D stem's 27 x 8 is 2 tiles, not 27
             T = ks * ks * (ks if d3 else 1)
-            tiles = -(-K // 128) * (1 if T > 1 and Ct * T <= 128 else -(-Ct // 128) * T)
+            tiles = -(-K // 128) * (-(-(T * Ct) // 128) if T > 1 and Ct < 128 else -(-Ct // 128) * T)
             steps = -(-M // 32)
             # up to WGRAD_CU_MULT workgroups per CU (the kernel is latency-bound at one), >= WGRAD_MIN_STEPS
             # 32-pixel steps per split, partial slabs <= 48 MB
