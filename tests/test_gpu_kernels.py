@@ -134,6 +134,24 @@ def test_conv_splitk_fused_stats(ep):
     torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("N,splits", [(1, None), (3, None), (3, 1)])
+def test_conv_1x1_stats_unsplit_tile(N, splits):
+    """A 1x1 (transposed) conv with K > 64 that runs unsplit on a small image: the host must pick the kernel's
+    128-pixel tile for the fused-statistics test (M = 64 / 192 pixels is not a multiple of it), so the statistics
+    come from the separate pass instead of a kernel error; output and statistics vs torch."""
+    O = ops()
+    H = W = 8
+    Cin = K = 128
+    dy = _rand_nhwc(N, H, W, Cin, 81)
+    w = _w(Cin, K, 1, 82)   # forward weight [Cin_fwd=Cin][K][1][1] of the conv whose data gradient this is
+    got, st = O.conv(dy.to(DEV), K, O.prep_weights(w.to(DEV), 1), ks=1, pad=0, transposed=True, out_hw_=(H, W),
+                     want_stats=True, splits=splits)
+    ref = torch.einsum("nhwc,ck->nhwk", dy.float(), _bfw(w)[:, :, 0, 0])
+    _close(got, ref)
+    refst = O.channel_stats(got, rows=st.rows)
+    torch.testing.assert_close(st.slab, refst.slab, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("mode", ["s1", "s2", "up", "1x1", "s2_split"])
 def test_conv_data_gradient(mode):
     """Data gradients through the generic implicit GEMM; s2 runs the parity-class decomposition of the
