@@ -676,6 +676,138 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d,
   }
 }
 
+// Split-K combine + the GroupNorm forward of the result: a 1024-thread block owns (image n, CB channels) with
+// CB = max(16, Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
+// pixel lane) over the image's pixels (slab sums in four chains, fixed order), bias / per-sample bias / residual,
+// bf16 out, and the channel sums of the rounded values; lanes (shuffles), waves (LDS) and the group's channels
+// (fp64) in fixed order; pass 2 re-reads the lane's own output elements and writes t = SiLU(a*out + b).
+constexpr int CGN_NT = 1024;
+__global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc d, const fmd_gn_out_desc g, int M,
+                                                            int CB) {
+  const int K = d.K;
+  const int HW = (d.Do > 0 ? d.Do : 1) * d.Ho * d.Wo;
+  const size_t total = (size_t)M * K;
+  const int n = blockIdx.x, cb = blockIdx.y * CB;
+  const int nq = CB / 4, PL = CGN_NT / nq;
+  const int tq = threadIdx.x % nq, pl = threadIdx.x / nq;
+  const int c = cb + tq * 4;
+  f32x4 add = {0.f, 0.f, 0.f, 0.f};
+  if (d.bias) add += *(const f32x4*)(d.bias + c);
+  if (d.bias2) add += *(const f32x4*)(d.bias2 + c);
+  if (d.bias_nc) {
+    const float* bn = d.bias_nc + (size_t)n * K + c;
+    add += f32x4{bn[0], bn[1], bn[2], bn[3]};
+  }
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int pp = pl; pp < HW; pp += PL) {
+    const size_t idx = ((size_t)n * HW + pp) * K + c;
+    f32x4 v = *(const f32x4*)(d.ws + idx), v1 = {0.f, 0.f, 0.f, 0.f}, v2 = v1, v3 = v1;
+    int s = 1;
+    for (; s + 4 <= d.splits; s += 4) {
+      v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+      v1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * total + idx);
+      v2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * total + idx);
+      v3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * total + idx);
+    }
+    for (; s < d.splits; ++s) v += *(const f32x4*)(d.ws + (size_t)s * total + idx);
+    v = ((v + v1) + (v2 + v3)) + add;
+    if (d.resid) {
+      const u32x2 r = *(const u32x2*)((const bf16r*)d.resid + idx);
+      v[0] += bf_lo(r[0]); v[1] += bf_hi(r[0]); v[2] += bf_lo(r[1]); v[3] += bf_hi(r[1]);
+    }
+    u32x2 w;
+    w[0] = pack2(v[0], v[1]);
+    w[1] = pack2(v[2], v[3]);
+    *(u32x2*)((bf16r*)d.out + idx) = w;
+    const float wr[4] = {bf_lo(w[0]), bf_hi(w[0]), bf_lo(w[1]), bf_hi(w[1])};
+#pragma unroll
+    for (int r2 = 0; r2 < 4; ++r2) {
+      s1[r2] += wr[r2];
+      s2[r2] += wr[r2] * wr[r2];
+    }
+  }
+  // lanes of one wave holding the same quad sit nq apart: butterfly over those, then the 16 waves via LDS
+  for (int o = nq; o < 64; o <<= 1) {
+#pragma unroll
+    for (int r2 = 0; r2 < 4; ++r2) {
+      s1[r2] += __shfl_xor(s1[r2], o, 64);
+      s2[r2] += __shfl_xor(s2[r2], o, 64);
+    }
+  }
+  __shared__ float red[CGN_NT / 64][64][2];
+  __shared__ float chs[64][2];
+  __shared__ double gst[16][2];
+  __shared__ float ab[64][2];
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (ln < nq) {
+#pragma unroll
+    for (int r2 = 0; r2 < 4; ++r2) { red[wv][ln * 4 + r2][0] = s1[r2]; red[wv][ln * 4 + r2][1] = s2[r2]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * CB) {   // per channel over the 16 waves
+    const int cl = threadIdx.x >> 1, k = threadIdx.x & 1;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < CGN_NT / 64; w2 += 2) { a0 += red[w2][cl][k]; a1 += red[w2 + 1][cl][k]; }
+    chs[cl][k] = a0 + a1;
+  }
+  __syncthreads();
+  const int Cg = K / g.G, ng = CB / Cg;
+  if (threadIdx.x < ng) {   // group sums in fp64 over its Cg channels, E[x^2] - mean^2 (as gn_fused_apply)
+    double t1 = 0.0, t2 = 0.0;
+    for (int cl = threadIdx.x * Cg; cl < (threadIdx.x + 1) * Cg; ++cl) {
+      t1 += (double)chs[cl][0];
+      t2 += (double)chs[cl][1];
+    }
+    const double cnt = (double)Cg * HW;
+    const double mean = t1 / cnt;
+    double var = t2 / cnt - mean * mean;
+    if (var < 0) var = 0;
+    const double rstd = 1.0 / sqrt(var + (double)g.eps);
+    gst[threadIdx.x][0] = mean;
+    gst[threadIdx.x][1] = rstd;
+    const int gi = cb / Cg + threadIdx.x;
+    g.mean_rstd[((size_t)n * g.G + gi) * 2] = (float)mean;
+    g.mean_rstd[((size_t)n * g.G + gi) * 2 + 1] = (float)rstd;
+  }
+  __syncthreads();
+  if (threadIdx.x < CB) {
+    const int cc = cb + threadIdx.x, gl = threadIdx.x / Cg;
+    const float meanf = (float)gst[gl][0], rstd = (float)gst[gl][1];
+    const float gm = g.gamma ? g.gamma[cc] : 1.f, bt = g.beta ? g.beta[cc] : 0.f;
+    float av = rstd * gm;
+    float bv = bt - meanf * av;
+    if (g.emb_mode == 1) {
+      const float sc = 1.f + g.emb[(size_t)n * g.emb_stride + cc];
+      const float sh = g.emb[(size_t)n * g.emb_stride + K + cc];
+      av *= sc;
+      bv = bv * sc + sh;
+    }
+    ab[threadIdx.x][0] = av;
+    ab[threadIdx.x][1] = bv;
+    g.a[(size_t)n * K + cc] = av;
+    g.b[(size_t)n * K + cc] = bv;
+  }
+  __syncthreads();
+  float av[4], bv[4];
+#pragma unroll
+  for (int r2 = 0; r2 < 4; ++r2) { av[r2] = ab[tq * 4 + r2][0]; bv[r2] = ab[tq * 4 + r2][1]; }
+  for (int pp = pl; pp < HW; pp += PL) {   // the lane's own pass-1 stores: program order makes them visible
+    const size_t idx = ((size_t)n * HW + pp) * K + c;
+    const u32x2 w = *(const u32x2*)((const bf16r*)d.out + idx);
+    float y[4] = {bf_lo(w[0]) * av[0] + bv[0], bf_hi(w[0]) * av[1] + bv[1], bf_lo(w[1]) * av[2] + bv[2],
+                  bf_hi(w[1]) * av[3] + bv[3]};
+    if (g.silu) {
+#pragma unroll
+      for (int r2 = 0; r2 < 4; ++r2) y[r2] = siluf_(y[r2]);
+    }
+    u32x2 o;
+    o[0] = pack2(y[0], y[1]);
+    o[1] = pack2(y[2], y[3]);
+    *(u32x2*)((bf16r*)g.t + idx) = o;
+  }
+}
+
 template <int BCO, int BPX, int WM, int WN, int BK, bool GNA = false>
 int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = nullptr) {
   KArgs A;
@@ -712,7 +844,8 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
 
 }  // namespace
 
-extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
+// combine = false: the split-K partial slabs only (fmd_conv_gn runs its own combine)
+static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   hipStream_t s = (hipStream_t)stream;
   // largest output (pixels) run on 64-pixel tiles when split-K (FMD_BPX64_M; mirrored by ops.BPX64_M)
   static const int small_m = [] {
@@ -756,7 +889,7 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
       rc = launch<128, 128, 2, 2, 64>(&dm, s);
   }
   if (rc) return rc;
-  if (d->splits > 1) {
+  if (d->splits > 1 && combine) {
     if (rows_ok) {
       hipLaunchKernelGGL(splitk_reduce_rows, dim3(M / FMD_SPLIT_STATS_ROWS, (d->K + 63) / 64), dim3(256), 0, s, *d, M);
     } else {
@@ -768,6 +901,23 @@ extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
   }
   return rc;
+}
+
+extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) { return conv_run(d, stream, true); }
+
+extern "C" int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t stream) {
+  if (!g || !g->a || !g->b || !g->mean_rstd || !g->t || g->G < 1 || d->K % g->G) return -12;
+  const int Cg = d->K / g->G;
+  if (d->splits < 2 || d->K % 64 || 64 % Cg || d->stats || d->out_f32 || d->accumulate || d->ep_x0 || d->ep_a)
+    return -12;
+  const int CB = Cg > 16 ? Cg : 16;   // channels per block: whole groups, >= 16 (4 quads x 256 pixel lanes)
+  if (g->emb_mode == 1 && !g->emb) return -12;
+  if (!d->ws || d->N < 1) return -12;
+  int rc = conv_run(d, stream, false);
+  if (rc) return rc;
+  const int M = d->N * (d->Do > 0 ? d->Do : 1) * d->Ho * d->Wo;
+  hipLaunchKernelGGL(combine_gn_kernel, dim3(d->N, d->K / CB), dim3(CGN_NT), 0, (hipStream_t)stream, *d, *g, M, CB);
+  return (int)hipGetLastError();
 }
 
 // The split-K combine alone: out = sum of d->splits fp32 slabs in d->ws ([splits][M][K]) + the conv

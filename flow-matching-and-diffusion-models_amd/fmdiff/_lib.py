@@ -50,6 +50,12 @@ class GnApplyDesc(C.Structure):
     ]
 
 
+class GnOutDesc(C.Structure):
+    """Mirror of ``fmd_gn_out_desc``."""
+    _fields_ = [("G", i32), ("eps", f32), ("gamma", p), ("beta", p), ("emb", p), ("emb_stride", i32),
+                ("emb_mode", i32), ("silu", i32), ("a", p), ("b", p), ("mean_rstd", p), ("t", p)]
+
+
 LINCOMB_MAX = 6   # FMD_LINCOMB_MAX
 
 
@@ -80,6 +86,7 @@ SIGNATURES = {
     "fmd_conv": [C.POINTER(ConvDesc), p],
     "fmd_conv_halo": [C.POINTER(ConvDesc), p],
     "fmd_conv_gn_apply": [C.POINTER(ConvDesc), C.POINTER(GnApplyDesc), p],
+    "fmd_conv_gn": [C.POINTER(ConvDesc), C.POINTER(GnOutDesc), p],
     "fmd_wgrad": [C.POINTER(WgradDesc), p],
     "fmd_wgrad_workspace": [C.POINTER(WgradDesc)],
     "fmd_wgrad_halo": [C.POINTER(WgradDesc), p],

@@ -614,12 +614,20 @@ class UNetEngine:
         keep_g = ctx.tape is not None and len(sp) == 3
         gg1 = (torch.empty((N, *sp, Cin), device=x0.t.device, dtype=torch.bfloat16)
                if keep_g and t1 is None and halo1 and not point and Cin % HALO_BK == 0 else None)
+        # small level, split-K conv1: GroupNorm-2 (+ scale/shift) + SiLU inside conv1's combine (fmd_conv_gn);
+        # not with the additive embedding under a tape (its backward needs conv1's statistics slab)
+        gnreq = (dict(groups=g2.num_groups, eps=g2.eps, gamma=g2.weight, beta=g2.bias, emb=eo if ss else None,
+                      emb_stride=es if ss else 0, emb_mode=1 if ss else 0)
+                 if fuse2 and not (add and ctx.tape is not None) else None)
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
                           pro=None if t1 is not None else (a1, b1, True),
-                          bias=c1.bias, bias_nc=eo.contiguous() if add else None, want_stats=add or not fuse2,
-                          wgt_tiled=w1t, gout=gg1, **pk)
+                          bias=c1.bias, bias_nc=eo.contiguous() if add else None,
+                          want_stats=(add and ctx.tape is not None) or not fuse2,
+                          wgt_tiled=w1t, gout=gg1, gn=gnreq, **pk)
         t2 = None
-        if fuse2:
+        if fuse2 and gnreq is not None and "res" in gnreq:
+            a2, b2, mr2, t2 = gnreq["res"]
+        elif fuse2:
             a2, b2, mr2, t2 = ops.gn_fused_apply(h, None, g2.num_groups, g2.eps, g2.weight, g2.bias,
                                                  emb=eo if ss else None, emb_stride=es if ss else 0,
                                                  emb_mode=1 if ss else 0)

@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import _lib
-from .._lib import ConvDesc, GnApplyDesc, WgradDesc
+from .._lib import ConvDesc, GnApplyDesc, GnOutDesc, WgradDesc
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -149,6 +149,16 @@ def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
     """Mirror of fmd_gn_fused_apply's applicability test (csrc/groupnorm.hip)."""
     Cg = C // groups if C % groups == 0 else 0
     return GN_FUSED and Cg > 0 and Cg % 4 == 0 and C0 % 4 == 0 and 256 % (Cg // 4) == 0 and HW * Cg <= GN_FUSED_MAX
+
+
+# the GroupNorm forward of a split-K conv's output inside its combine (fmd_conv_gn); FMD_CONV_GN=0: the separate
+# fmd_gn_fused_apply launch (A/B runs)
+CONV_GN = os.environ.get("FMD_CONV_GN", "1") == "1"
+
+
+def conv_gn_eligible(K: int, groups: int) -> bool:
+    """Mirror of fmd_conv_gn's channel test: whole groups per 64-channel block."""
+    return K % 64 == 0 and K % groups == 0 and 64 % (K // groups) == 0
 
 
 def gn_fused_apply(x0, x1, groups: int, eps: float, gamma, beta, emb=None, emb_stride=0, emb_mode=0, silu=True):
@@ -312,7 +322,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
          pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
          out_f32=False,
          accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
-         wgt2_tiled=None, gout=None, s2d_tiled=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+         wgt2_tiled=None, gout=None, s2d_tiled=None, gn=None) -> Tuple[torch.Tensor, Optional[Stats]]:
     """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``.
     ``want_stats``: True = per-channel statistics of the output (a separate fmd_channel_stats pass when the
     kernel cannot emit them); "free" = only when the kernel emits them (else None: Act statistics are then
@@ -320,6 +330,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     ``gout``: bf16 tensor shaped like the (concatenated) input; the halo path writes the prologue's output
     G = SiLU(a*x+b) into it (the weight gradient's operand).  Requires ``pro``, (C0+C1) % 32 == 0 and a
     halo-eligible problem (:func:`halo_eligible`); raises otherwise.
+    ``gn``: dict(groups, eps, gamma, beta[, emb, emb_stride, emb_mode]) -- when the conv runs split-K and
+    :func:`conv_gn_eligible` holds, its combine also computes the GroupNorm + SiLU of the output (fmd_conv_gn)
+    and stores ``gn["res"] = (a, b, mean_rstd, t)`` as :func:`gn_fused_apply` returns them; otherwise ``gn`` is
+    left without "res" and the caller runs the GroupNorm itself.
     ``s2d_tiled``: :func:`s2d_tile_weights` of the stride-2 conv's weight -- the problem runs on the space-to-depth
     halo kernel (fmd_conv_s2d; the caller checks :func:`s2d_eligible`), ``wgt`` unused."""
     _need_cuda(src0, "conv")
@@ -434,6 +448,20 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         print(f"[conv] N={N} in={Ds}x{Hs}x{Ws}x{C0}+{C1} out={Do}x{Ho}x{Wo}x{K} ks={ks} s={stride} tr={int(transposed)} "
               f"up={int(upsample)} pro={int(pro is not None)} ep={int(ep is not None)} seg2={int(src2 is not None)} "
               f"stats={int(fused_stats)} halo={int(halo)} splits={splits}", file=sys.stderr)
+    if (gn is not None and CONV_GN and splits > 1 and not want_stats and d.stats is None and not out_f32
+            and not accumulate and ep is None and conv_gn_eligible(K, gn["groups"])):
+        a = torch.empty((N, K), device=dev, dtype=F32)
+        b = torch.empty((N, K), device=dev, dtype=F32)
+        mr = torch.empty((N, gn["groups"], 2), device=dev, dtype=F32)
+        t = torch.empty_like(out)
+        g = GnOutDesc()
+        g.G, g.eps, g.gamma, g.beta = gn["groups"], float(gn["eps"]), _p(gn["gamma"]), _p(gn["beta"])
+        emb = gn.get("emb")
+        g.emb, g.emb_stride, g.emb_mode = _p(emb), gn.get("emb_stride", 0), gn.get("emb_mode", 0) if emb is not None else 0
+        g.silu, g.a, g.b, g.mean_rstd, g.t = int(gn.get("silu", True)), _p(a), _p(b), _p(mr), _p(t)
+        _lib.call("fmd_conv_gn", C.byref(d), C.byref(g), stream())
+        gn["res"] = (a, b, mr, t)
+        return out, None
     _lib.call("fmd_conv", C.byref(d), stream())
     if want_stats == "free":   # only statistics the kernel emits for free; the consumer derives others lazily
         return out, st

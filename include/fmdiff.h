@@ -110,6 +110,28 @@ typedef struct fmd_gn_apply_desc {
  * (replaces conv(dy, W_skip^T) + fmd_gn_bwd_apply(extra = that)). */
 int fmd_conv_gn_apply(const fmd_conv_desc* d, const fmd_gn_apply_desc* g, fmd_stream_t s);
 
+/* GroupNorm forward of a split-K conv's output, fused into its split-K combine (fmd_conv_gn).  For each (n, c):
+ * out = conv result (bf16, as fmd_conv writes it); then per (n, group) mean / rstd of out, a = rstd*gamma,
+ * b = beta - mean*a (emb_mode 1: a *= 1 + emb[n][c], b = b*(1 + emb[n][c]) + emb[n][K + c]) and the materialised
+ * t = SiLU(a*out + b) (silu = 0: the affine alone) -- the outputs of fmd_gn_fused_apply on out. */
+typedef struct fmd_gn_out_desc {
+  int32_t G;                /* groups */
+  float eps;
+  const float* gamma;       /* [K] or NULL */
+  const float* beta;        /* [K] or NULL */
+  const float* emb;         /* [N][emb_stride] scale | shift (emb_mode 1) or NULL */
+  int32_t emb_stride, emb_mode, silu;
+  float* a;                 /* [N][K] */
+  float* b;                 /* [N][K] */
+  float* mean_rstd;         /* [N][G][2] */
+  void* t;                  /* bf16 [N][Ho][Wo][K] */
+} fmd_gn_out_desc;
+/* fmd_conv with d->splits > 1 whose combine also produces the GroupNorm of the output (one workgroup per
+ * (image, 64 channels): the group statistics close inside it).  Requires K % 64 == 0, 64 % (K/G) == 0, no
+ * d->stats / out_f32 / accumulate / ep_*.  Replaces fmd_conv + fmd_gn_fused_apply on the small levels
+ * (src/nn/blocks/residual.py:71-76 conv1 -> out_layers GroupNorm + SiLU). */
+int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s);
+
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
 /* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv

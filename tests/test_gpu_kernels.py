@@ -134,6 +134,42 @@ def test_conv_splitk_fused_stats(ep):
     torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("case", ["8x8_k512_ss", "16x16_k128", "4x4_k256_resid", "1x1_k512", "3d_k128"])
+def test_conv_gn_fused_combine(case):
+    """fmd_conv_gn: a split-K conv whose combine also runs the GroupNorm(+scale/shift)+SiLU of its output, vs the
+    same conv through fmd_conv + fmd_gn_fused_apply on that output (a, b, mean/rstd, t)."""
+    O = ops()
+    g = torch.Generator().manual_seed(len(case))
+    d3 = case.startswith("3d")
+    N, H, C, K = {"8x8_k512_ss": (8, 8, 512, 512), "16x16_k128": (4, 16, 128, 128), "4x4_k256_resid": (8, 4, 256, 256),
+                  "1x1_k512": (8, 1, 512, 512), "3d_k128": (1, 8, 128, 128)}[case]
+    G = 32
+    shape = (N, H, H, H, C) if d3 else (N, H, H, C)
+    x = (torch.randn(*shape, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    ks = 1 if H == 1 else 3
+    w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27) if d3 else _w(K, C, ks, 91)
+    wp = O.prep_weights(w.to(DEV), 0)
+    kw = dict(bias=(torch.randn(K, generator=g) * 0.1).to(DEV), bias_nc=(torch.randn(N, K, generator=g) * 0.1).to(DEV),
+              splits=5, force_generic=True, ks=ks, pad=ks // 2)
+    if case.endswith("resid"):
+        kw["resid"] = (torch.randn(*shape[:-1], K, generator=g)).to(torch.bfloat16).to(DEV)
+    gamma, beta = (torch.rand(K, generator=g) + 0.5).to(DEV), (torch.randn(K, generator=g) * 0.1).to(DEV)
+    emb = (torch.randn(N, 2 * K, generator=g) * 0.2).to(DEV) if case.endswith("ss") else None
+    req = dict(groups=G, eps=1e-5, gamma=gamma, beta=beta, emb=emb, emb_stride=2 * K if emb is not None else 0,
+               emb_mode=1 if emb is not None else 0)
+    out, st = O.conv(x, K, wp, gn=req, **kw)
+    assert "res" in req and st is None
+    a, b, mr, t = req["res"]
+    ref, _ = O.conv(x, K, wp, **kw)
+    _close(out, ref.float(), rel=1e-2)
+    ra, rb, rmr, rt = O.gn_fused_apply(out, None, G, 1e-5, gamma, beta, emb=emb,
+                                       emb_stride=2 * K if emb is not None else 0, emb_mode=1 if emb is not None else 0)
+    torch.testing.assert_close(mr, rmr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(a, ra, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(b, rb, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(t.float(), rt.float(), rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("N,splits", [(1, None), (3, None), (3, 1)])
 def test_conv_1x1_stats_unsplit_tile(N, splits):
     """A 1x1 (transposed) conv with K > 64 that runs unsplit on a small image: the host must pick the kernel's
