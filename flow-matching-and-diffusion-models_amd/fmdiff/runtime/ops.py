@@ -154,11 +154,17 @@ def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
 # the GroupNorm forward of a split-K conv's output inside its combine (fmd_conv_gn); FMD_CONV_GN=0: the separate
 # fmd_gn_fused_apply launch (A/B runs)
 CONV_GN = os.environ.get("FMD_CONV_GN", "1") == "1"
+# fewest combine blocks (images x channel blocks) for which the fused form beats the two launches it replaces
+# (latent step profile: 64 blocks 13.1 us vs 5-7 + 5.2 us; 128 blocks 8.0 us, 256 blocks 7.2 us)
+CONV_GN_MIN_BLOCKS = int(os.environ.get("FMD_CONV_GN_MIN_BLOCKS", "128"))
 
 
-def conv_gn_eligible(K: int, groups: int) -> bool:
-    """Mirror of fmd_conv_gn's channel test: whole groups per 64-channel block."""
-    return K % 64 == 0 and K % groups == 0 and 64 % (K // groups) == 0
+def conv_gn_eligible(K: int, groups: int, N: int = 1 << 30) -> bool:
+    """Mirror of fmd_conv_gn's channel test (whole groups per block of max(16, K/groups) <= 64 channels) plus
+    the block-count floor."""
+    if K % 64 or K % groups or 64 % (K // groups):
+        return False
+    return N * (K // max(16, K // groups)) >= CONV_GN_MIN_BLOCKS
 
 
 def gn_fused_apply(x0, x1, groups: int, eps: float, gamma, beta, emb=None, emb_stride=0, emb_mode=0, silu=True):
@@ -449,7 +455,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
               f"up={int(upsample)} pro={int(pro is not None)} ep={int(ep is not None)} seg2={int(src2 is not None)} "
               f"stats={int(fused_stats)} halo={int(halo)} splits={splits}", file=sys.stderr)
     if (gn is not None and CONV_GN and splits > 1 and not want_stats and d.stats is None and not out_f32
-            and not accumulate and ep is None and conv_gn_eligible(K, gn["groups"])):
+            and not accumulate and ep is None and conv_gn_eligible(K, gn["groups"], N)):
         a = torch.empty((N, K), device=dev, dtype=F32)
         b = torch.empty((N, K), device=dev, dtype=F32)
         mr = torch.empty((N, gn["groups"], 2), device=dev, dtype=F32)
