@@ -910,7 +910,15 @@ extern "C" int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd
   const int Cg = d->K / g->G;
   if (d->splits < 2 || d->K % 64 || 64 % Cg || d->stats || d->out_f32 || d->accumulate || d->ep_x0 || d->ep_a)
     return -12;
-  const int CB = Cg > 16 ? Cg : 16;   // channels per block: whole groups, >= 16 (4 quads x 256 pixel lanes)
+  // channels per block: whole groups, at least FMD_CONV_GN_CB (default 4: one quad x 1024 pixel lanes when a group
+  // is 4 channels -- more blocks on the 128-channel levels; latent sampler 82.3 / 82.6 (16) -> 81.8 / 82.0 (8)
+  // -> 81.3 / 81.5 ms (4), interleaved A/B)
+  static const int cb_min = [] {
+    const char* e = getenv("FMD_CONV_GN_CB");
+    const int v = e && *e ? atoi(e) : 4;
+    return v == 8 || v == 16 || v == 32 || v == 64 ? v : 4;
+  }();
+  const int CB = Cg > cb_min ? Cg : cb_min;
   if (g->emb_mode == 1 && !g->emb) return -12;
   if (!d->ws || d->N < 1) return -12;
   int rc = conv_run(d, stream, false);

@@ -157,6 +157,9 @@ CONV_GN = os.environ.get("FMD_CONV_GN", "1") == "1"
 # fewest combine blocks (images x channel blocks) for which the fused form beats the two launches it replaces
 # (latent step profile: 64 blocks 13.1 us vs 5-7 + 5.2 us; 128 blocks 8.0 us, 256 blocks 7.2 us)
 CONV_GN_MIN_BLOCKS = int(os.environ.get("FMD_CONV_GN_MIN_BLOCKS", "128"))
+CONV_GN_CB = int(os.environ.get("FMD_CONV_GN_CB", "4"))   # fewest channels per combine block (fmd_conv_gn)
+if CONV_GN_CB not in (4, 8, 16, 32, 64):
+    CONV_GN_CB = 4
 
 
 def conv_gn_eligible(K: int, groups: int, N: int = 1 << 30) -> bool:
@@ -164,7 +167,7 @@ def conv_gn_eligible(K: int, groups: int, N: int = 1 << 30) -> bool:
     the block-count floor."""
     if K % 64 or K % groups or 64 % (K // groups):
         return False
-    return N * (K // max(16, K // groups)) >= CONV_GN_MIN_BLOCKS
+    return N * (K // max(CONV_GN_CB, K // groups)) >= CONV_GN_MIN_BLOCKS
 
 
 def gn_fused_apply(x0, x1, groups: int, eps: float, gamma, beta, emb=None, emb_stride=0, emb_mode=0, silu=True):

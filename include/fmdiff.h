@@ -127,7 +127,7 @@ typedef struct fmd_gn_out_desc {
   void* t;                  /* bf16 [N][Ho][Wo][K] */
 } fmd_gn_out_desc;
 /* fmd_conv with d->splits > 1 whose combine also produces the GroupNorm of the output (one workgroup per
- * (image, 64 channels): the group statistics close inside it).  Requires K % 64 == 0, 64 % (K/G) == 0, no
+ * (image, whole groups of max(FMD_CONV_GN_CB = 4, C/G) channels): the group statistics close inside it).  Requires K % 64 == 0, 64 % (K/G) == 0, no
  * d->stats / out_f32 / accumulate / ep_*.  Replaces fmd_conv + fmd_gn_fused_apply on the small levels
  * (src/nn/blocks/residual.py:71-76 conv1 -> out_layers GroupNorm + SiLU). */
 int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s);
