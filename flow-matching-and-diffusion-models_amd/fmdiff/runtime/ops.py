@@ -266,7 +266,7 @@ HALO_SPLIT_WG = int(os.environ.get("FMD_HALO_SPLIT_WG", "256"))
 HALO_MIN_CHUNKS = int(os.environ.get("FMD_HALO_MIN_CHUNKS", "2"))
 HALO_SPLIT_CAP = int(os.environ.get("FMD_HALO_SPLIT_CAP", "16"))
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (FMD_HALO_MIN_WG, _lib load)
-HALO_MIN_WG = int(os.environ.get("FMD_HALO_MIN_WG", "128") or 128)
+HALO_MIN_WG = int(os.environ.get("FMD_HALO_MIN_WG", "32") or 32)
 
 
 def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
