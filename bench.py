@@ -71,7 +71,8 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
-        kernel = "conv3x3_halo<false> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)"
+        kernel = "conv3x3_halo9b<false, 2, 0> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)"
+        kid = ["conv3x3_halo9b<false, 2, 0>"]
     elif prob == "dgrad":
         w = ops.prep_weights(wf, 3)
         wt = ops.tile_weights(w)
@@ -79,7 +80,9 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.conv(dy, C, w, out=out, want_stats=True, ep=(x, None, a, b), wgt_tiled=wt)
-        kernel = "conv3x3_halo<false,0> data gradient (flipped taps, SiLU' + GN-backward-sums epilogue, 8x256x256x128->128)"
+        kernel = ("conv3x3_halo9b<false, 0, 0> data gradient (flipped taps, SiLU' + GN-backward-sums epilogue, "
+                  "8x256x256x128->128)")
+        kid = ["conv3x3_halo9b<false, 0, 0>"]
     else:
         dy = torch.randn(N, H, W, K, device=dev, generator=g).to(torch.bfloat16)
         dw = torch.zeros(K, C, 3, 3, device=dev)
@@ -87,7 +90,8 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.wgrad(x, dy, dw, pro=(a, b, True), db=db)
-        kernel = "wgrad_halo_kernel<2> + wgrad_reduce (GN+SiLU recomputed, 8x256x256x128->128x3x3, fp32 dW)"
+        kernel = "wgrad_halo_kernel<2> + wgrad_reduce2 (GN+SiLU recomputed, 8x256x256x128->128x3x3, fp32 dW)"
+        kid = ["wgrad_halo_kernel<2>", "wgrad_reduce2"]
     for _ in range(3):
         fn()
     # In the train step the 134 MB input arrives cold (written by an earlier kernel, evicted by the ones
@@ -105,19 +109,28 @@ def conv_roofline(dev, iters=20, prob="fwd"):
     ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / iters
     del flush
     flops = 2.0 * N * H * W * K * C * 9
-    return dict(kernel=kernel, ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
+    return dict(kernel=kernel, kernel_id=kid, ms=ms, tflops=flops / ms / 1e9, flops_per_launch=flops)
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC summary
-    (profiles/r*_halo_fwd_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes over the same
-    problem, tools/gpu_pmc.sh); None when no summary is committed."""
+def pmc_traffic(kernel_ids):
+    """HBM bytes per launch of the timed kernel(s) from the newest committed rocprofv3 PMC summary whose
+    ``kernel_id`` names exactly these kernels (profiles/r*_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, separate --pmc
+    passes over the same problem, tools/gpu_pmc.sh + tools/pmc_traffic.py); None when no summary of THESE kernels is
+    committed (a summary of another kernel is never reported)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_halo_fwd_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return float(json.load(f)["traffic_bytes_per_launch"])
+    import re
+    want = sorted([kernel_ids] if isinstance(kernel_ids, str) else kernel_ids)
+    best = None
+    for fn in glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")):
+        with open(fn) as f:
+            j = json.load(f)
+        kid = j.get("kernel_id")
+        if kid is None or sorted([kid] if isinstance(kid, str) else kid) != want:
+            continue
+        rnd = int(re.match(r"r(\d+)_", os.path.basename(fn)).group(1))
+        if best is None or rnd > best[0]:
+            best = (rnd, fn, float(j["traffic_bytes_per_launch"]))
+    return None if best is None else dict(bytes=best[2], file=os.path.relpath(best[1], REPO))
 
 
 CONFIG_E_FWD_GFLOP = 32854.2   # SURVEY.md 8(d) E: forward GFLOP per 128^3 sample (torch flop counter on the reference)
@@ -370,15 +383,19 @@ def main():
     if not args.no_roofline:
         roof = conv_roofline(dev)
         log(f"[bench] dominant conv: {roof['ms']:.3f} ms, {roof['tflops']:.1f} TFLOP/s")
+        tr = pmc_traffic(roof["kernel_id"])
         roofline = {"bound": "mfma", "achieved": roof["tflops"], "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": pmc_traffic(), "kernel": roof["kernel"],
-                    "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"]}
+                    "frac": roof["tflops"] / PEAK_BF16_TFLOPS, "traffic": tr and tr["bytes"], "kernel": roof["kernel"],
+                    "kernel_ms": roof["ms"], "flops_per_launch": roof["flops_per_launch"],
+                    "traffic_source": tr and tr["file"]}
         # the same problem's backward kernels (the step's next two largest buckets), same protocol
         back = {"peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s"}
         for prob in ("dgrad", "wgrad"):
             r = conv_roofline(dev, prob=prob)
+            tr = pmc_traffic(r["kernel_id"])
             back[prob] = {"achieved": r["tflops"], "frac": r["tflops"] / PEAK_BF16_TFLOPS, "kernel": r["kernel"],
-                          "kernel_ms": r["ms"], "flops_per_launch": r["flops_per_launch"]}
+                          "kernel_ms": r["ms"], "flops_per_launch": r["flops_per_launch"],
+                          "traffic": tr and tr["bytes"], "traffic_source": tr and tr["file"]}
             log(f"[bench] {prob}: {r['ms']:.3f} ms, {r['tflops']:.1f} TFLOP/s")
     cfg_e = None
     if world == 1 and not args.no_config_e:

@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d,
 }
 
 // Split-K combine + the GroupNorm forward of the result: a 1024-thread block owns (image n, CB channels) with
-// CB = max(16, Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
+// CB = max(FMD_CONV_GN_CB (default 4), Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
 // pixel lane) over the image's pixels (slab sums in four chains, fixed order), bias / per-sample bias / residual,
 // bf16 out, and the channel sums of the rounded values; lanes (shuffles), waves (LDS) and the group's channels
 // (fp64) in fixed order; pass 2 re-reads the lane's own output elements and writes t = SiLU(a*out + b).
@@ -736,7 +736,7 @@ __global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc 
   }
   __shared__ float red[CGN_NT / 64][64][2];
   __shared__ float chs[64][2];
-  __shared__ double gst[16][2];
+  __shared__ double gst[64][2];   // ng = CB / Cg groups per block: up to 64 (CB <= 64, Cg >= 1)
   __shared__ float ab[64][2];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   if (ln < nq) {
@@ -873,7 +873,7 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   if (d->splits > 1) dm.stats = nullptr;
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
-    rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= 128 workgroups of 16x16 tiles (x splits)
+    rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= HALO_MIN_WG (32) workgroups of 16x16 tiles (x splits)
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->gout) return -9;                            // the prologue side output exists only on the halo path
@@ -905,6 +905,22 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
 
 extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) { return conv_run(d, stream, true); }
 
+static int g_conv_gn_cb = -1;
+static int conv_gn_cb() {
+  if (g_conv_gn_cb < 0) {
+    const char* e = getenv("FMD_CONV_GN_CB");
+    const int v = e && *e ? atoi(e) : 4;
+    g_conv_gn_cb = v == 8 || v == 16 || v == 32 || v == 64 ? v : 4;
+  }
+  return g_conv_gn_cb;
+}
+
+extern "C" int fmd_conv_gn_set_block_channels(int32_t cb) {
+  if (cb != 4 && cb != 8 && cb != 16 && cb != 32 && cb != 64) return -1;
+  g_conv_gn_cb = cb;
+  return 0;
+}
+
 extern "C" int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t stream) {
   if (!g || !g->a || !g->b || !g->mean_rstd || !g->t || g->G < 1 || d->K % g->G) return -12;
   const int Cg = d->K / g->G;
@@ -913,11 +929,7 @@ extern "C" int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd
   // channels per block: whole groups, at least FMD_CONV_GN_CB (default 4: one quad x 1024 pixel lanes when a group
   // is 4 channels -- more blocks on the 128-channel levels; latent sampler 82.3 / 82.6 (16) -> 81.8 / 82.0 (8)
   // -> 81.3 / 81.5 ms (4), interleaved A/B)
-  static const int cb_min = [] {
-    const char* e = getenv("FMD_CONV_GN_CB");
-    const int v = e && *e ? atoi(e) : 4;
-    return v == 8 || v == 16 || v == 32 || v == 64 ? v : 4;
-  }();
+  const int cb_min = conv_gn_cb();
   const int CB = Cg > cb_min ? Cg : cb_min;
   if (g->emb_mode == 1 && !g->emb) return -12;
   if (!d->ws || d->N < 1) return -12;

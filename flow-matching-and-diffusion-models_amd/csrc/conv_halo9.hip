@@ -1,30 +1,23 @@
-// Halo-tiled 3x3 stride-1 convolution, v9: the UNet's dominant problem on v_mfma_f32_32x32x16_bf16.
+// Halo-tiled 3x3 stride-1 convolution (v9b): the UNet's dominant problem on v_mfma_f32_32x32x16_bf16.
 //
 // Same tiling contract as conv_halo.hip (16x16-pixel x 128-output-channel tile, 32-channel reduction chunks whose
 // 18x18 halo -- 10x10 under nearest-x2 -- is staged ONCE into LDS with the GroupNorm affine + SiLU applied, two
-// halo buffers, weights pre-tiled so each (chunk, tap) slice is one contiguous 8 KiB block), re-budgeted for
-// registers:
+// halo buffers), re-budgeted for registers:
 //
-// * 256-thread workgroups (4 waves, 2 per CU: one wave of each workgroup per SIMD) at up to 256 VGPRs: each wave
-//   owns a 128-pixel x 64-cout sub-tile = 4 x 2 accumulators of 32x32 (128 VGPRs), twice the round-3 wave tile,
-//   so every fragment read, address and barrier feeds twice the MFMA work.
+// * 256-thread workgroups (4 waves, 2 per CU: one wave of each workgroup per SIMD) at up to 256 VGPRs; a wave owns
+//   one 32-cout quarter of the tile over all 256 pixels (8 accumulators of 32x32).
 // * MFMA 32x32x16: A = activations (rows = 32 pixels = two tile rows, k = 16 channels), B = weights (k = 16
-//   channels, cols = 32 couts).  An MFMA holds the SIMD's vector issue for 8 of its 32 cycles (8 of 16 for the
-//   16x16x32 form), leaving 3x the issue room for the staging transform beside the matrix work.
+//   channels, cols = 32 couts), B fragments straight from L2 (pre-tiled weights, one tap's 32 x 32 slice per wave).
 // * The 9 taps of a chunk are unrolled at compile time: every fragment read is one ds_read_b128 from a fixed base
-//   VGPR with an immediate offset, the weight ring slot of a tap is a constant, and the counted waits are
-//   constants -- no per-step scalar bookkeeping.
-// * Weights: 3-slot LDS ring filled by LDS-DMA two taps ahead (counted vmcnt, raw s_barrier).  Halo of the next
-//   chunk: 6 rounds of one 16-byte piece per thread, each loaded two taps before it is transformed and stored.
+//   VGPR with an immediate offset.  Halo of the next chunk: rounds of one 16-byte piece per thread, each loaded
+//   FMD_H9_LAG taps before it is transformed and stored.
 // * A-fragment pixel map: lanes 0-15 read row 2b of the tile, lanes 16-31 row 2b+1 shifted by 2 columns
 //   (sigma(x) = (x - 2) mod 16), which makes every ds_read_b128 lane group of gfx950 touch 16 distinct bank slots.
-// * Epilogue in the accumulator layout (pixels in registers, couts on lanes): bias / per-sample bias per lane,
+// * Epilogue in the accumulator layout (pixels in registers, couts on lanes): bias as the accumulators' start value,
 //   the residual and the data-gradient side input brought into that layout by two MFMAs against an identity
 //   (exact), per-channel GroupNorm sums in-lane (+ one cross-half add), and the output transposed back to
 //   channels-last by two more MFMAs against a permuted identity, staged in LDS and stored as 16-byte rows.
-//
-// Round-3 problem being fixed: the 512-thread / 128-VGPR kernel spilled (8 VGPR + 28 SGPR), ran 4.85 non-MFMA
-// VALU and 4.3 SALU instructions per MFMA and kept the MFMA pipe 34 % busy (profiles/r3_halo_pmc.txt).
+// (The round-4 v9 variants with an LDS weight ring were measured slower and removed in round 5.)
 #include "halo_args.h"
 
 namespace {
@@ -34,7 +27,6 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 constexpr int NT9 = 256;
 constexpr int TH = 16, TW = 16, BCO = 128, BK = 32, KC = BK / 8;
 constexpr int WTILE = KC * BCO * 16;   // bytes of one tap's weight tile (8 KiB)
-constexpr int NWSLOT = 3;              // weight ring slots (a tap reads slot t % 3; DMA two taps ahead)
 constexpr int CMAX = 512;              // widest GN-prologue input of the affine table
 constexpr int OUT_TILE = TH * TW * BCO * 2;
 constexpr int ZFLAG = 1 << 30;         // staged-piece flag: store zeros (padding)
@@ -55,31 +47,11 @@ struct G9 {
   static constexpr int HBUF = KC * HPAD * 16;                      // bytes per halo buffer
   static constexpr int NPIECE = HPOSP * KC;
   static constexpr int NR = (NPIECE + NT9 - 1) / NT9;              // staging rounds per chunk (6 | 2)
-  static constexpr int SM_W = 2 * HBUF;
-  static constexpr int SM_MAIN = SM_W + NWSLOT * WTILE;
-  static constexpr int SM_COEF = SM_MAIN > OUT_TILE ? SM_MAIN : OUT_TILE;
-  static constexpr int SM_EPI = SM_COEF + 2 * CMAX * 4;
-  static constexpr int SM_BYTES = SM_EPI + 3 * BCO * 4;
   static_assert(NR <= 6 && NR * NT9 >= NPIECE, "staging rounds");
-  static_assert(SM_BYTES <= 163840 / 2, "two workgroups per CU");
 };
 
 FMD_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// end of a step: all but the `keep` youngest vector-memory ops of this wave (weight DMA + halo loads) done, LDS
-// ops done, then the workgroup barrier (raw: __syncthreads would drain the DMA meant to stay in flight)
-FMD_DEV void step_end(int keep) {
-  switch (keep) {
-    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
 }
 
 FMD_DEV bf16x8 as_bf16x8(const u32x4& u) { return __builtin_bit_cast(bf16x8, u); }
@@ -91,535 +63,6 @@ FMD_DEV bf16x8 as_bf16x8(const u32x4& u) { return __builtin_bit_cast(bf16x8, u);
 #else
 #define HDBG9(bit) false
 #endif
-
-// accumulator row pr (0..31) of pixel block pb of wave row-group wpx -> tile-local pixel index (y * 16 + x)
-FMD_DEV int pix_of(int wpx, int pb, int pr) {
-  const int q = pr >> 4;
-  const int cl = q ? ((pr - 18) & 15) : pr;
-  return (8 * wpx + 2 * pb + q) * TW + cl;
-}
-
-// V: 1 = per-tap fragment reads (round-4 first version); 2 = software-pipelined step (A fragments of the next tap
-// prefetched under the current tap's MFMAs, branch-free staging interleaved with the MFMAs)
-template <bool UP, int PRO, int V>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void conv3x3_halo9(const HArgs A) {
-  using G = G9<UP>;
-  constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[G::SM_BYTES];
-  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  float* const coef = (float*)(smem + G::SM_COEF);
-  float* const epi = (float*)(smem + G::SM_EPI);   // [3][BCO]: summed bias, ep_a, ep_b of this tile's couts
-
-  const fmd_conv_desc& d = A.d;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid >> 1, wpx = wid & 1;           // cout half, pixel-row half (8 rows) of the wave
-  const int r = lane & 31, hh = lane >> 5, rr = r >> 4;
-  const int col = rr ? ((r - 18) & 15) : r;          // A-row r -> tile column (sigma on the odd row)
-
-  const int per_img = A.tiles_x * A.tiles_y;
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int tco = b % A.ntc;
-  const int tile = b / A.ntc;
-  const int n = tile / per_img;
-  const int tin = tile - n * per_img;
-  const int smp = A.depth ? n / A.depth : n;
-  const int zz = A.depth ? n - smp * A.depth : 0;
-  const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
-  const int co0 = tco * BCO;
-  const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;
-  const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
-  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
-  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
-  const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
-  const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
-
-  if (PRO != 0) {
-    for (int i = tid; i < 2 * A.C; i += NT9)
-      coef[i] = i < A.C ? d.pro_a[(size_t)smp * A.C + i] : d.pro_b[(size_t)smp * A.C + (i - A.C)];
-  }
-  if (tid < BCO) {
-    const int co = co0 + tid;
-    const bool ok = co < d.K;
-    float bsum = 0.f;
-    if (ok && d.bias) bsum += d.bias[co];
-    if (ok && d.bias2) bsum += d.bias2[co];
-    if (ok && d.bias_nc) bsum += d.bias_nc[(size_t)smp * d.K + co];
-    epi[tid] = bsum;
-    epi[BCO + tid] = (ok && d.ep_a) ? d.ep_a[(size_t)smp * d.K + co] : 0.f;
-    epi[2 * BCO + tid] = (ok && d.ep_b) ? d.ep_b[(size_t)smp * d.K + co] : 0.f;
-  }
-
-  // ---- reduction range of this workgroup (split-K over 3x3 chunks; the 1x1 segment belongs to the last split)
-  const int split = blockIdx.y;
-  const int c_lo = split * A.cps, c_hi = min(A.nchunk1, c_lo + A.cps);
-  const int n_seg2 = split == A.splits - 1 ? A.nchunk2 : 0;
-  const int nsteps_main = (c_hi - c_lo) * 9;
-  const int nsteps = nsteps_main + n_seg2;
-  const int T1 = A.nchunk1 * 9;
-
-  // ---- weights: tap step g (local, from 0) -> absolute slot; ring slot g % 3, two LDS-DMAs of 1 KiB per wave
-  const unsigned char* const wbase1 = (const unsigned char*)(A.wt + (size_t)tco * T1 * (WTILE / 2));
-  const unsigned char* const wbase2 = (const unsigned char*)(A.wt2 + (size_t)tco * A.nchunk2 * (WTILE / 2));
-  const unsigned wvoff = (unsigned)lane * 16;
-  const unsigned wdst = __builtin_amdgcn_readfirstlane(lds_base + G::SM_W + (unsigned)wid * 2048);
-  auto dma = [&](int g, int ring) {   // g past the end: re-fetch the last slot (keeps the vmcnt schedule fixed)
-    const int gg = g < nsteps ? g : nsteps - 1;
-    const unsigned char* src = gg < nsteps_main ? wbase1 + (size_t)(c_lo * 9 + gg) * WTILE
-                                                 : wbase2 + (size_t)(gg - nsteps_main) * WTILE;
-    src += wid * 2048;
-    glds16s(src, wvoff, wdst + ring * WTILE);
-    glds16s(src + 1024, wvoff, wdst + ring * WTILE + 1024);
-  };
-
-  // ---- halo staging: thread = channel group kc of 8-position runs; round q stages position q*64 + p0
-  const int kc = (tid >> 3) & (KC - 1);
-  const int p0 = (tid >> 5) * 8 + (tid & 7);
-  int spix[NR];   // source pixel (y * Ws + x) of round q's position; -1 zero padding; -2 nothing to stage
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    const int pos = q * 64 + p0;
-    const int py = pos / HROW, px = pos - (pos / HROW) * HROW;
-    const int y = hy0 + py, x = hx0 + px;
-    spix[q] = pos >= G::HPOS ? -2 : (y >= 0 && y < d.Hs && x >= 0 && x < d.Ws) ? y * d.Ws + x : -1;
-  }
-  const int sdst0 = (kc * HPAD + p0) * 16;                                           // + q * 1024
-  const int s2pix0 = (n * d.Ho + ty0 + (p0 >> 4)) * d.Wo + tx0 + (p0 & 15);           // + 4q * Wo (1x1 chunks)
-  const int s2dst0 = (kc * HPAD + ((p0 >> 4) + 1) * (TW + 2) + (p0 & 15) + 1) * 16;   // + q * 72 * 16
-  const int HWs = d.Hs * d.Ws;
-
-  // staging source of a chunk (per thread: its 8-channel group)
-  const bf16r* sbase = s0;
-  int scs = 0, simg = 0, scch = 0;
-  bool sok = false, sseg2 = false;
-  auto setup = [&](int chunk) {
-    sseg2 = chunk >= A.nchunk1;
-    if (chunk < 0) {
-      sok = false; sbase = s0; scs = 0; simg = 0; scch = 0;
-    } else if (!sseg2) {
-      int cb = chunk;
-      bool zok = true;
-      int sl = n;
-      if (A.depth) {
-        const int kz = chunk / A.ncb;
-        cb = chunk - kz * A.ncb;
-        const int zl = zz + kz - 1;
-        zok = zl >= 0 && zl < A.depth;
-        sl = smp * A.dsrc + (UP ? zl >> 1 : zl);
-      }
-      const int c = cb * BK + kc * 8;
-      sok = c < A.C && zok;
-      sbase = !sok ? s0 : (c < d.C0) ? s0 + c : s1 + (c - d.C0);
-      scs = (c < d.C0) ? d.C0 : d.C1;
-      simg = sl * HWs;
-      scch = sok ? c : 0;
-    } else {
-      const int c = (chunk - A.nchunk1) * BK + kc * 8;
-      sok = c < A.C23;
-      sbase = !sok ? s2 : (c < d.C2) ? s2 + c : s3 + (c - d.C2);
-      scs = (c < d.C2) ? d.C2 : d.C3;
-      simg = 0;
-      scch = 0;
-    }
-  };
-  u32x4 rh[2];
-  int roff[2];
-  auto load_round = [&](int q) {   // one 16-byte load per thread, always (a dummy read when nothing is staged)
-    int pix = 0, off = -1;
-    bool valid = false;
-    if (sseg2) {
-      if (q < 4) {
-        valid = sok;
-        pix = s2pix0 + 4 * q * d.Wo;
-        off = (s2dst0 + q * 72 * 16) | (valid ? 0 : ZFLAG);
-      }
-    } else {
-      const int sp = spix[q];
-      const bool act = sp != -2;
-      valid = act && sok && sp >= 0;
-      pix = simg + sp;
-      off = !act ? -1 : (sdst0 + q * 1024) | (valid ? 0 : ZFLAG);
-    }
-    const bf16r* src = valid ? sbase + (size_t)pix * scs : s0;
-    rh[q & 1] = *(const u32x4*)src;
-    roff[q & 1] = off;
-  };
-  float ca[8], cb8[8];   // GN affine of the staged chunk's 8 channels
-  auto load_coef = [&]() {
-    if (PRO != 0) {
-      const f32x4 a0 = *(const f32x4*)(coef + scch), a1 = *(const f32x4*)(coef + scch + 4);
-      const f32x4 b0 = *(const f32x4*)(coef + A.C + scch), b1 = *(const f32x4*)(coef + A.C + scch + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ca[e] = a0[e]; ca[4 + e] = a1[e];
-        cb8[e] = b0[e]; cb8[4 + e] = b1[e];
-      }
-    }
-  };
-  auto store_round = [&](int q, int bufoff) {
-    u32x4 v = rh[q & 1];
-    const int o = roff[q & 1];
-    if (PRO != 0 && !sseg2) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float lo = bf_lo(v[e]) * ca[2 * e] + cb8[2 * e];
-        float hi = bf_hi(v[e]) * ca[2 * e + 1] + cb8[2 * e + 1];
-        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-        v[e] = pack2(lo, hi);
-      }
-    }
-    if (o & ZFLAG) v = u32x4{0u, 0u, 0u, 0u};
-    if (o >= 0) *(u32x4*)(smem + bufoff + (o & ~ZFLAG)) = v;
-  };
-
-  // ---- fragment addressing (bytes): A = halo rows of the wave's 4 pixel blocks, B = the ring slot's couts
-  int abase;
-  int uo[9];   // nearest-x2: per-lane offset of each tap
-  if constexpr (UP) {
-    abase = (hh * HPAD + (4 * wpx + 1) * HROW + 1) * 16;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = t / 3, kx = t % 3;
-      const int dy = (rr + ky - 1) >> 1, dx = (col + kx - 1) >> 1;
-      uo[t] = (dy * HROW + dx) * 16;
-    }
-  } else {
-    abase = (hh * HPAD + (8 * wpx + rr) * HROW + col) * 16;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) uo[t] = 0;
-  }
-  const int bbase = G::SM_W + (hh * BCO + 64 * wco + r) * 16;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int pb = 0; pb < 4; ++pb)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[pb][cb][e] = 0.f;
-
-  auto compute = [&](int tap, int hb, int ring) {
-    const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[4], bw[2];
-#pragma unroll
-      for (int pb = 0; pb < 4; ++pb) {
-        const int off = UP ? hb + abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
-                           : hb + abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
-        af[pb] = *(const bf16x8*)(smem + off);
-      }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) bw[cb] = *(const bf16x8*)(smem + bbase + ring * WTILE + s * 4096 + cb * 512);
-#pragma unroll
-      for (int pb = 0; pb < 4; ++pb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) acc[pb][cb] = mfma32(af[pb], bw[cb], acc[pb][cb]);
-    }
-  };
-  auto next_chunk = [&](int c) { return c + 1 < c_hi ? c + 1 : (c + 1 == c_hi && n_seg2 ? A.nchunk1 : -1); };
-
-  // ---- V2 pieces: A fragments of one k-step of a tap, the B fragments of a ring slot, branch-free staging
-  constexpr int DUMMY = (G::HPOS + 2) * 16;   // plane-0 padding slot no fragment read touches: unstaged lanes' store
-  auto readA = [&](bf16x8 (&af)[4], int tap, int hb, int s) {
-    const int ky = tap / 3, kx = tap % 3;
-#pragma unroll
-    for (int pb = 0; pb < 4; ++pb) {
-      const int off = UP ? hb + abase + uo[tap] + (s * 2 * HPAD + pb * HROW) * 16
-                         : hb + abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
-      af[pb] = *(const bf16x8*)(smem + off);
-    }
-  };
-  auto readB = [&](bf16x8 (&bw)[2][2], int ring) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) bw[s][cb] = *(const bf16x8*)(smem + bbase + ring * WTILE + s * 4096 + cb * 512);
-  };
-  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bw)[2]) {
-#pragma unroll
-    for (int pb = 0; pb < 4; ++pb)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) acc[pb][cb] = mfma32(af[pb], bw[cb], acc[pb][cb]);
-  };
-  auto load_round2 = [&](int q) {
-    const int sp = q < NR ? spix[q] : -2;
-    const bool act = sseg2 ? q < 4 : sp != -2;
-    const bool valid = act && sok && (sseg2 || sp >= 0);
-    const int pix = sseg2 ? s2pix0 + 4 * q * d.Wo : simg + sp;
-    const int dst = sseg2 ? s2dst0 + q * 72 * 16 : sdst0 + q * 1024;
-    const bf16r* src = valid ? sbase + (size_t)pix * scs : s0;
-    rh[q & 1] = HDBG9(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)src;
-    roff[q & 1] = !act ? DUMMY : (dst | (valid ? 0 : ZFLAG));
-  };
-  auto transform2 = [&](int q) -> u32x4 {   // the GN affine re-read from LDS (4 ds_read_b128): 16 VGPRs freed
-    const u32x4 raw = rh[q & 1];
-    u32x4 v = raw;
-    if (PRO != 0 && !HDBG9(2)) {
-      const f32x4 a0 = *(const f32x4*)(coef + scch), a1 = *(const f32x4*)(coef + scch + 4);
-      const f32x4 b0 = *(const f32x4*)(coef + A.C + scch), b1 = *(const f32x4*)(coef + A.C + scch + 4);
-      const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const float qb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float lo = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
-        float hi = bf_hi(raw[e]) * qa[2 * e + 1] + qb[2 * e + 1];
-        if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-        v[e] = sseg2 ? raw[e] : pack2(lo, hi);
-      }
-    }
-    const bool z = (roff[q & 1] & ZFLAG) != 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = z ? 0u : v[e];
-    return v;
-  };
-
-  // ---- prologue: weights of steps 0 and 1, the whole first chunk staged
-  __syncthreads();   // affine + epilogue tables
-  dma(0, 0);
-  dma(1, 1);
-  setup(c_lo);
-  load_coef();
-  {
-    u32x4 pv[NR];
-    int po[NR];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      load_round(q);
-      pv[q] = rh[q & 1];
-      po[q] = roff[q & 1];
-    }
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      rh[q & 1] = pv[q];
-      roff[q & 1] = po[q];
-      store_round(q, (c_lo & 1) * HBUF);
-    }
-  }
-  step_end(0);
-
-  // ---- 3x3 chunks: 9 unrolled taps; next chunk staged in rounds (load at tap q, transform + store at tap q + 2)
-  if constexpr (V == 2) {
-    bf16x8 af0[4];   // A fragments (k-step 0) of the current tap, prefetched during the previous tap
-    readA(af0, 0, (c_lo & 1) * HBUF, 0);
-    for (int chunk = c_lo; chunk < c_hi; ++chunk) {
-      const int nx = next_chunk(chunk);
-      setup(nx);
-      const int hb = (chunk & 1) * HBUF, nb = ((chunk + 1) & 1) * HBUF;
-      const int gc = (chunk - c_lo) * 9;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        bf16x8 bw[2][2], af1[4];
-        readB(bw, t % NWSLOT);
-        readA(af1, t, hb, 1);
-        const bool st = t >= 2 && t < NR + 2;
-        u32x4 sv;
-        int so = DUMMY;
-        if (st) {
-          sv = transform2(t - 2);
-          so = roff[t & 1] & ~ZFLAG;
-        }
-        if (!HDBG9(256)) mma(af0, bw[0]);
-        // next tap's k-step-0 fragments: this chunk's buffer, or at the last tap the next chunk's (its staging
-        // finished at tap NR + 1 < 8, before that step's barrier)
-        if (t < 8) readA(af0, t + 1, hb, 0);
-        else readA(af0, 0, nb, 0);
-        if (!HDBG9(256)) mma(af1, bw[1]);
-        if (st) *(u32x4*)(smem + nb + so) = sv;
-        if (!HDBG9(8)) dma(gc + t + 2, (t + 2) % NWSLOT);
-        if (t < NR) load_round2(t);
-        if (HDBG9(128)) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-        else step_end((t >= 1 && t - 1 < NR ? 1 : 0) + 2 + (t < NR ? 1 : 0));
-      }
-    }
-  } else
-  for (int chunk = c_lo; chunk < c_hi; ++chunk) {
-    const int nx = next_chunk(chunk);
-    setup(nx);
-    const int hb = (chunk & 1) * HBUF, nb = ((chunk + 1) & 1) * HBUF;
-    const int gc = (chunk - c_lo) * 9;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t == 1) load_coef();
-      if (t >= 2 && t < NR + 2) store_round(t - 2, nb);
-      dma(gc + t + 2, (t + 2) % NWSLOT);
-      if (t < NR) load_round(t);
-      compute(t, hb, t % NWSLOT);
-      // younger than DMA(g+1) (issued last step): last step's load, this step's DMA pair and load
-      step_end((t >= 1 && t - 1 < NR ? 1 : 0) + 2 + (t < NR ? 1 : 0));
-    }
-  }
-
-  // ---- 1x1 chunks (ResBlock skip conv over src2|src3), one step each; the next chunk loaded whole
-  for (int i = 0; i < n_seg2; ++i) {
-    const int g = nsteps_main + i;
-    const int ch = A.nchunk1 + i;
-    const bool more = i + 1 < n_seg2;
-    setup(more ? ch + 1 : -1);
-    u32x4 sv[4];
-    int so[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool valid = more && sok;
-      const bf16r* src = valid ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2;
-      sv[q] = *(const u32x4*)src;
-      so[q] = !more ? -1 : (s2dst0 + q * 72 * 16) | (valid ? 0 : ZFLAG);
-    }
-    compute(4, (ch & 1) * HBUF, g % NWSLOT);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      u32x4 v = sv[q];
-      if (so[q] & ZFLAG) v = u32x4{0u, 0u, 0u, 0u};
-      if (so[q] >= 0) *(u32x4*)(smem + ((ch + 1) & 1) * HBUF + (so[q] & ~ZFLAG)) = v;
-    }
-    dma(g + 2, (g + 2) % NWSLOT);
-    step_end(2);
-  }
-  step_end(0);   // every DMA landed (the tail re-fetches too) before the LDS is reused
-  if (HDBG9(4)) return;
-
-  // ------------------------------------------------------------ epilogue
-  const int K = d.K, Ho = d.Ho, Wo = d.Wo;
-  if (A.splits > 1) {   // fp32 partial sums of this split ([split][pixel][K]); splitk_reduce applies the epilogue
-    float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
-#pragma unroll
-    for (int pb = 0; pb < 4; ++pb)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int co = co0 + 64 * wco + 32 * cb + r;
-        if (co >= K) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int pr = (e & 3) + 8 * (e >> 2) + 4 * hh;
-          const int pi = pix_of(wpx, pb, pr);
-          const size_t p = ((size_t)n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-          ws[p * K + co] = acc[pb][cb][e];
-        }
-      }
-    return;
-  }
-
-  // (host guarantees here: K % 128 == 0, bf16 output, no accumulate, not both resid and ep_x0)
-  unsigned char* const tileb = smem;   // [256 px][256 B], 16-byte chunk index ^ (pixel & 15)
-  const bool hasx = d.ep_x0 != nullptr;
-  const bool dep = d.ep_a != nullptr;
-  const bool side = d.resid != nullptr || hasx;
-  const bool stats = d.stats != nullptr;
-  if (side) {
-    constexpr int SK = TH * TW * BCO / 8 / NT9;   // 16-byte pieces per thread (16)
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
-      const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-      const int c = co0 + c16 * 8;
-      const bf16r* src = d.resid ? (const bf16r*)d.resid + (size_t)p * K + c
-                         : (c < d.ep_C0) ? (const bf16r*)d.ep_x0 + (size_t)p * d.ep_C0 + c
-                                         : (const bf16r*)d.ep_x1 + (size_t)p * (K - d.ep_C0) + (c - d.ep_C0);
-      *(u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16)) = *(const u32x4*)src;
-    }
-    __syncthreads();
-  }
-  // identity operands: inat (natural k order) brings a [pixel][cout] fragment into the accumulator layout;
-  // iperm (the accumulator-as-operand k order: element j of half h is row 16s + 8(j>>2) + 4h + (j&3)) transposes
-  // an accumulator back to [cout][pixel]
-  bf16x8 inat[2], iperm[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      inat[s][j] = (__bf16)((16 * s + 8 * hh + j) == r ? 1.0f : 0.0f);
-      iperm[s][j] = (__bf16)((16 * s + 8 * (j >> 2) + 4 * hh + (j & 3)) == r ? 1.0f : 0.0f);
-    }
-  float st1[2] = {0.f, 0.f}, st2[2] = {0.f, 0.f};
-#pragma unroll
-  for (int pb = 0; pb < 4; ++pb) {
-    const int pi_l = pix_of(wpx, pb, r);   // pixel of this lane's A row / output column
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int cl = 64 * wco + 32 * cb;    // tile-local first cout of this accumulator
-      f32x16 v = acc[pb][cb];
-      f32x16 xc;
-      if (side) {
-        bf16x8 fr[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int c = cl + 16 * s + 8 * hh;
-          fr[s] = *(const bf16x8*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16));
-        }
-        if (d.resid) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s) v = mfma32(fr[s], inat[s], v);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) xc[e] = 0.f;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) xc = mfma32(fr[s], inat[s], xc);
-        }
-      }
-      const float bias = epi[cl + r];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] += bias;
-      if (hasx && dep) {
-        const float ea = epi[BCO + cl + r], eb = epi[2 * BCO + cl + r];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) v[e] *= silu_grad(ea * xc[e] + eb);
-      }
-      // round to bf16 (the stored value), statistics of the stored value, transpose to [cout][pixel]
-      bf16x8 pf[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        u32x4 u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = pack2(v[8 * s + 2 * e], v[8 * s + 2 * e + 1]);
-        pf[s] = as_bf16x8(u);
-        if (stats) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float w0 = bf_lo(u[e]), w1 = bf_hi(u[e]);
-            st1[cb] += w0 + w1;
-            st2[cb] += hasx ? w0 * xc[8 * s + 2 * e] + w1 * xc[8 * s + 2 * e + 1] : w0 * w0 + w1 * w1;
-          }
-        }
-      }
-      f32x16 z;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) z[e] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) z = mfma32(pf[s], iperm[s], z);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = cl + 8 * g + 4 * hh;   // z registers 4g..4g+3: couts c..c+3 of pixel pi_l
-        u32x2 o;
-        o[0] = pack2(z[4 * g], z[4 * g + 1]);
-        o[1] = pack2(z[4 * g + 2], z[4 * g + 3]);
-        *(u32x2*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16) + (c & 7) * 2) = o;
-      }
-    }
-    if (stats && (pb & 1)) {   // one statistics row per 64 pixels (pixel blocks 2k, 2k+1 of the wave)
-      const int srow = tile * 4 + 2 * wpx + (pb >> 1);
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const float a = st1[cb] + __shfl_xor(st1[cb], 32, 64);
-        const float q = st2[cb] + __shfl_xor(st2[cb], 32, 64);
-        if (hh == 0) {
-          float* sp = d.stats + ((size_t)srow * K + co0 + 64 * wco + 32 * cb + r) * 2;
-          sp[0] = a;
-          sp[1] = q;
-        }
-        st1[cb] = 0.f;
-        st2[cb] = 0.f;
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < TH * TW * BCO / 8 / NT9; ++k) {
-    const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
-    const int p = (n * Ho + ty0 + (pi >> 4)) * Wo + tx0 + (pi & 15);
-    *(u32x4*)((bf16r*)d.out + (size_t)p * K + co0 + c16 * 8) = *(const u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16));
-  }
-}
-
 
 // ---------------------------------------------------------------------------------------------------------------
 // v9b: the same tile, staging and epilogue, with the weights taken straight from L2 into registers.
@@ -1146,15 +589,9 @@ void conv3x3_halo9b(const HArgs A) {
 
 }  // namespace
 
-static int g_halo9 = -1;   // FMD_HALO9: 0 = round-3 kernel for every problem, 1 = v9, 2 = v9 pipelined, else v9b
-
 int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
-  if (g_halo9 < 0) {
-    const char* e = getenv("FMD_HALO9");
-    g_halo9 = (e && *e) ? atoi(e) : 3;
-  }
   const fmd_conv_desc* d = &A.d;
-  if (!g_halo9 || d->gout) return 1;
+  if (d->gout) return 1;
   if (d->upsample && d->src2) return 1;
   if (A.splits <= 1 && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
   if (A.splits > 1 && (d->out_f32 || d->accumulate)) return 1;
@@ -1162,21 +599,7 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const dim3 g(nwg, A.splits);
   const dim3 blk(NT9);
   hipStream_t st = (hipStream_t)stream;
-#define H9_LAUNCH(V)                                                                        \
-  do {                                                                                      \
-    if (d->upsample) {                                                                      \
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<true, 2, V>), g, blk, 0, st, A);      \
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<true, 1, V>), g, blk, 0, st, A); \
-      else hipLaunchKernelGGL((conv3x3_halo9<true, 0, V>), g, blk, 0, st, A);               \
-    } else {                                                                                \
-      if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9<false, 2, V>), g, blk, 0, st, A);     \
-      else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9<false, 1, V>), g, blk, 0, st, A);\
-      else hipLaunchKernelGGL((conv3x3_halo9<false, 0, V>), g, blk, 0, st, A);              \
-    }                                                                                       \
-  } while (0)
-  if (g_halo9 == 1) H9_LAUNCH(1);
-  else if (g_halo9 == 2) H9_LAUNCH(2);
-  else if (d->upsample) {
+  if (d->upsample) {
     if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<true, 2>), g, blk, 0, st, A);
     else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<true, 1>), g, blk, 0, st, A);
     else hipLaunchKernelGGL((conv3x3_halo9b<true, 0>), g, blk, 0, st, A);
@@ -1185,7 +608,6 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
     else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1>), g, blk, 0, st, A);
     else hipLaunchKernelGGL((conv3x3_halo9b<false, 0>), g, blk, 0, st, A);
   }
-#undef H9_LAUNCH
   return (int)hipGetLastError();
 }
 

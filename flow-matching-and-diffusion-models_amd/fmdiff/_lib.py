@@ -107,6 +107,7 @@ SIGNATURES = {
     "fmd_lincomb": [C.POINTER(LincombDesc), p],
     "fmd_sched_step": [C.POINTER(SchedStepDesc), p],
     "fmd_halo_set_min_workgroups": [i32],
+    "fmd_conv_gn_set_block_channels": [i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
     "fmd_prep_weights_t": [p, i32, i32, i32, i32, i32, i32, p, p],

@@ -135,8 +135,10 @@ class FusedTrainStep:
         self.eng = get_engine(model)
         world = world_size(process_group)
         # data parallel: the decoder's gradients (final after backward part 1) go first in the flat buffer
-        # and are all-reduced while the encoder's backward runs
-        self.overlap = (world > 1 if overlap_allreduce is None else bool(overlap_allreduce)) and grad_accum <= 1
+        # and are all-reduced while the encoder's backward runs.  With gradient accumulation the exchange overlaps
+        # the LAST chunk's backward (the earlier chunks' backward passes run whole, as the reference accumulates
+        # .grad over chunks before its optimizer step, flow_matching_lib.py:143-146, 176-182)
+        self.overlap = world > 1 if overlap_allreduce is None else bool(overlap_allreduce)
         # overlapped exchange: the flat buffer is laid out in backward-segment order and cut into
         # ``allreduce_buckets`` contiguous buckets of whole segments; bucket b is all-reduced (async) while
         # the segments of the later buckets run, only the last bucket's exchange is exposed
@@ -172,7 +174,7 @@ class FusedTrainStep:
         self._split = False
 
     # ---------------------------------------------------------------- body
-    def _chunk(self, clean, ldct, noise, t_or_ts, cca=None):
+    def _chunk(self, clean, ldct, noise, t_or_ts, cca=None, last=True):
         N, Cx = clean.shape[:2]
         Cc = ldct.shape[1] if ldct is not None else 0
         Cp = max(8, -(-(Cx + Cc) // 8) * 8)
@@ -190,7 +192,7 @@ class FusedTrainStep:
         dpred = torch.empty(out.shape, device=out.device, dtype=torch.bfloat16)
         ops.mse(out, ta, tb, sign, 1.0 / self.grad_accum, self.loss, self.partial, dpred)
         self.loss_sum.add_(self.loss, alpha=float(N))
-        if self.overlap:
+        if self.overlap and last:
             # bucket 0's segments now; the rest in _bwd_bucket, each after the previous bucket's all-reduce started
             self.eng.backward(ctx, dpred, segs=self.seg_buckets[0][0])
             self._ctx = ctx
@@ -268,7 +270,8 @@ class FusedTrainStep:
                 tt = t[c0:c0 + chunk] if t is not None else torch.randint(0, self.N_train, (cl.shape[0],),
                                                                            device=cl.device)
             cc = context_ca[c0:c0 + chunk].contiguous() if context_ca is not None else None
-            loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt, cc)
+            loss = self._chunk(cl.contiguous(), ld.contiguous() if ld is not None else None, nz.contiguous(), tt, cc,
+                               last=c0 + chunk >= N)
         return loss
 
     # ------------------------------------------------- bookkeeping / state

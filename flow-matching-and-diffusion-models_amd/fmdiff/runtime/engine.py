@@ -413,7 +413,10 @@ class UNetEngine:
                 if not x.need_grad:
                     return
                 g, acc = _gdest(x)
-                if upsample and len(sp) == 2 and S2D_HALO and conv.weight.shape[1] == Cin and ops.s2d_eligible(
+                # the tiled mode-1 weight covers exactly conv.weight.shape[0] gradient channels: a channel-padded dy
+                # would read past it, so such a dy takes the generic path
+                if upsample and len(sp) == 2 and S2D_HALO and conv.weight.shape[1] == Cin and \
+                        dy.shape[-1] == conv.weight.shape[0] and ops.s2d_eligible(
                         N_, 2 * sp[0], 2 * sp[1], sp[0], sp[1], Cin, dy.shape[-1], 4):
                     # nearest-x2 folded into a 4x4 stride-2 gather, on the space-to-depth halo kernel
                     ops.conv(dy, Cin, None, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc),

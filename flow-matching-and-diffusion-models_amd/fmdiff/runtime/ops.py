@@ -163,8 +163,8 @@ if CONV_GN_CB not in (4, 8, 16, 32, 64):
 
 
 def conv_gn_eligible(K: int, groups: int, N: int = 1 << 30) -> bool:
-    """Mirror of fmd_conv_gn's channel test (whole groups per block of max(16, K/groups) <= 64 channels) plus
-    the block-count floor."""
+    """Mirror of fmd_conv_gn's channel test (whole groups per block of max(CONV_GN_CB, K/groups) <= 64 channels,
+    CONV_GN_CB = FMD_CONV_GN_CB, default 4) plus the block-count floor."""
     if K % 64 or K % groups or 64 % (K // groups):
         return False
     return N * (K // max(CONV_GN_CB, K // groups)) >= CONV_GN_MIN_BLOCKS
@@ -291,8 +291,8 @@ def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
 def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, transposed=False, Cin=0,
                   pro=False, ztaps=1) -> bool:
     """Mirror of fmd_conv_halo's applicability test (csrc/conv_halo.hip): 3x3 s1 p1 forward gather,
-    16x16 output tiles, K > 16, at least 128 workgroups (with split-K over channel chunks when the
-    level is small), GN-prologue inputs of at most HALO_CMAX channels."""
+    16x16 output tiles, K > 16, at least HALO_MIN_WG (default 32) workgroups (with split-K over channel chunks
+    when the level is small), GN-prologue inputs of at most HALO_CMAX channels."""
     Ws = Wo // 2 if upsample else Wo
     return (K > 16 and ks == 3 and stride == 1 and pad == 1 and not transposed and not (pro and Cin > HALO_CMAX)
             and Ho % 16 == 0 and Wo % 16 == 0 and (Ho == 2 * Hs if upsample else Ho == Hs)

@@ -135,9 +135,13 @@ int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
 /* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv
- * (default 128; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
+ * (default 32; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
  * halo_splits mirror reads the same variable. */
 int fmd_halo_set_min_workgroups(int32_t n);
+/* Fewest channels per combine block of fmd_conv_gn (4, 8, 16, 32 or 64; default 4, or FMD_CONV_GN_CB at first use):
+ * a block owns max(cb, K / G) channels = whole groups.  Returns -1 for any other value.  A tuning hook; the host's
+ * conv_gn_eligible mirror reads ops.CONV_GN_CB. */
+int fmd_conv_gn_set_block_channels(int32_t cb);
 #define FMD_HALO_BK 32
 /* [K][T][C] bf16 kernel weights -> the halo kernel's per-(cout tile, FMD_HALO_BK-channel chunk, tap) 8 KiB tiles. */
 int64_t fmd_halo_tiled_size(int32_t K, int32_t T, int32_t C);

@@ -134,17 +134,27 @@ def test_conv_splitk_fused_stats(ep):
     torch.testing.assert_close(sb.slab, ref.slab, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("case", ["8x8_k512_ss", "16x16_k128", "4x4_k256_resid", "1x1_k512", "3d_k128"])
+@pytest.mark.parametrize("case", ["8x8_k512_ss", "16x16_k128", "4x4_k256_resid", "1x1_k512", "3d_k128",
+                                  "8x8_k64_cb64", "8x8_k128_cb32", "halo_16x16_c256_pro"])
 def test_conv_gn_fused_combine(case, monkeypatch):
     """fmd_conv_gn: a split-K conv whose combine also runs the GroupNorm(+scale/shift)+SiLU of its output, vs the
-    same conv through fmd_conv + fmd_gn_fused_apply on that output (a, b, mean/rstd, t)."""
+    same conv through fmd_conv + fmd_gn_fused_apply on that output (a, b, mean/rstd, t).  ``_cb64`` / ``_cb32``: 64 /
+    32 channels per combine block with 2- / 4-channel groups (32 / 8 groups in one block); ``halo_``: the production
+    route -- halo-kernel split-K partials (GN+SiLU prologue) into combine_gn_kernel, not the generic conv."""
     O = ops()
+    from fmdiff import _lib
     monkeypatch.setattr(O, "CONV_GN_MIN_BLOCKS", 0)
     g = torch.Generator().manual_seed(len(case))
     d3 = case.startswith("3d")
+    halo = case.startswith("halo")
     N, H, C, K = {"8x8_k512_ss": (8, 8, 512, 512), "16x16_k128": (4, 16, 128, 128), "4x4_k256_resid": (8, 4, 256, 256),
-                  "1x1_k512": (8, 1, 512, 512), "3d_k128": (1, 8, 128, 128)}[case]
+                  "1x1_k512": (8, 1, 512, 512), "3d_k128": (1, 8, 128, 128), "8x8_k64_cb64": (8, 8, 64, 64),
+                  "8x8_k128_cb32": (8, 8, 128, 128), "halo_16x16_c256_pro": (8, 16, 256, 128)}[case]
     G = 32
+    cb = 64 if case.endswith("cb64") else 32 if case.endswith("cb32") else 4
+    if cb != 4:
+        monkeypatch.setattr(O, "CONV_GN_CB", cb)
+        _lib.call("fmd_conv_gn_set_block_channels", cb)
     shape = (N, H, H, H, C) if d3 else (N, H, H, C)
     x = (torch.randn(*shape, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     ks = 1 if H == 1 else 3
@@ -152,6 +162,10 @@ def test_conv_gn_fused_combine(case, monkeypatch):
     wp = O.prep_weights(w.to(DEV), 0)
     kw = dict(bias=(torch.randn(K, generator=g) * 0.1).to(DEV), bias_nc=(torch.randn(N, K, generator=g) * 0.1).to(DEV),
               splits=5, force_generic=True, ks=ks, pad=ks // 2)
+    if halo:   # halo_splits picks the split count (2 images x 1 tile: split-K over the 4 chunks), GN+SiLU prologue
+        kw.update(splits=None, force_generic=False,
+                  pro=((torch.rand(N, C, generator=g) + 0.5).to(DEV), (torch.randn(N, C, generator=g) * 0.1).to(DEV), True))
+        assert O.halo_eligible(N, H, H, H, K, Cin=C, pro=True) and O.halo_splits(N, H, H, K, C) > 1
     if case.endswith("resid"):
         kw["resid"] = (torch.randn(*shape[:-1], K, generator=g)).to(torch.bfloat16).to(DEV)
     gamma, beta = (torch.rand(K, generator=g) + 0.5).to(DEV), (torch.randn(K, generator=g) * 0.1).to(DEV)
@@ -163,12 +177,30 @@ def test_conv_gn_fused_combine(case, monkeypatch):
     a, b, mr, t = req["res"]
     ref, _ = O.conv(x, K, wp, **kw)
     _close(out, ref.float(), rel=1e-2)
-    ra, rb, rmr, rt = O.gn_fused_apply(out, None, G, 1e-5, gamma, beta, emb=emb,
-                                       emb_stride=2 * K if emb is not None else 0, emb_mode=1 if emb is not None else 0)
+    if (K // G) % 4 == 0:
+        ra, rb, rmr, rt = O.gn_fused_apply(out, None, G, 1e-5, gamma, beta, emb=emb,
+                                           emb_stride=2 * K if emb is not None else 0,
+                                           emb_mode=1 if emb is not None else 0)
+    else:   # fmd_gn_fused_apply takes groups of 4k channels only: GroupNorm of the same bf16 output in fp64 torch
+        assert emb is None
+        o = out.double().reshape(N, -1, G, K // G)
+        mean = o.mean(dim=(1, 3))
+        var = (o * o).mean(dim=(1, 3)) - mean * mean
+        rstd = (var + 1e-5).rsqrt()
+        ra = (gamma.double()[None] * rstd.repeat_interleave(K // G, dim=1)).float()
+        rb = (beta.double()[None] - mean.repeat_interleave(K // G, dim=1) * ra.double()).float()
+        rmr = torch.stack([mean, rstd], dim=-1).float()
+        y = out.float() * ra.reshape(N, *([1] * (out.dim() - 2)), K) + rb.reshape(N, *([1] * (out.dim() - 2)), K)
+        rt = y * torch.sigmoid(y)
     torch.testing.assert_close(mr, rmr, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(a, ra, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(b, rb, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(t.float(), rt.float(), rtol=1e-2, atol=1e-2)
+    if halo:   # the split halo conv itself against the unsplit generic conv of the same prologue
+        ref_g, _ = O.conv(x, K, wp, **dict(kw, splits=1, force_generic=True))
+        _close(out, ref_g.float(), rel=1e-2)
+    if cb != 4:
+        _lib.call("fmd_conv_gn_set_block_channels", 4)
 
 
 @pytest.mark.parametrize("N,splits", [(1, None), (3, None), (3, 1)])
