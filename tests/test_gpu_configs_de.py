@@ -54,6 +54,47 @@ def test_config_d_vae_vs_reference_fixture():
     assert all(v < 2e-2 for v in errs.values()), errs
 
 
+def test_config_d_latent_path_vs_reference_fixture():
+    """Config D end to end at its own architecture and size (tests/golden/make_golden_d_latent.py): the reference's
+    LDCT_autoencoder_kl VAE (84 M) + the 4-channel latent LDCT FM UNet (113 M), 256x256 -> 4x32x32, batch 2:
+    encode_vae_batch -> 5 FlowMatchEuler steps from an injected latent -> decode_vae_batch (reference
+    vae_utils.py:54-85, pipelines/utils.py:163-220), through fmdiff.pipelines.latent.latent_flow_sample on the HIP
+    VAE engine and the graph-replayed FusedFlowSampler.  Tolerance: relative L2 < 3e-2 on each stage (bf16 through
+    an encoder, five latent UNet evaluations and a decoder; each alone ~1e-2)."""
+    import seeded_params as SP
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.models.vae import AutoencoderKL
+    from fmdiff.pipelines.latent import encode_vae_batch, latent_flow_sample
+    from fmdiff.pipelines.train.fused import FusedFlowSampler
+    from oracle import spec as S
+    from oracle import unet as U
+    G = torch.load(os.path.join(HERE, "golden", "golden_d_latent.pt"), weights_only=True)
+    meta = json.loads(bytes(G["meta"].tolist()).decode())
+    GV = torch.load(os.path.join(HERE, "golden", "vae_golden_d.pt"), weights_only=True)
+    model = json.loads(bytes(GV["cfg_json"].tolist()).decode())
+    kw = {k: v for k, v in model.items() if k not in ("latent_type", "model_type", "norm_type", "act")}
+    kw["down_channels"] = tuple(kw["down_channels"])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**kw)
+    SP.fill_module(vae, meta["vae_seed"])
+    vae = vae.to(DEV).eval()
+    E, ucfg = meta["E"], meta["ucfg"]
+    unet = DiffusionUNetFactory().build(ucfg, "concatenate", E)
+    unet.load_state_dict(U.seeded_state_dict(S.derive_spec(ucfg, "concatenate", E), meta["unet_seed"]))
+    unet = unet.to(DEV)
+    imgs, init = G["imgs"].to(DEV), G["init"].to(DEV)
+    sampler = FusedFlowSampler(unet, meta["steps"])
+    with torch.no_grad():
+        cond = encode_vae_batch(vae, imgs)
+        lat = sampler.sample(init, cond.contiguous(), use_graph=True)
+        out = latent_flow_sample(vae, sampler, imgs, init, use_graph=True)
+    errs = dict(cond=_rel(cond, G["cond"]), latent=_rel(lat, G["latent"]), out=_rel(out, G["out"]))
+    print("config D latent path vs reference: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    assert out.shape == G["out"].shape
+    assert all(v < 3e-2 for v in errs.values()), errs
+
+
 def _build_e(m):
     from fmdiff.models.generators import DiffusionUNetFactory
     from oracle import spec as S
