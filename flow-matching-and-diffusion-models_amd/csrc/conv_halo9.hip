@@ -55,6 +55,13 @@ FMD_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
 }
 
 FMD_DEV bf16x8 as_bf16x8(const u32x4& u) { return __builtin_bit_cast(bf16x8, u); }
+#ifndef FMD_H9_FENCE
+#define FMD_H9_FENCE 1   // staging transform advanced stage by stage behind register fences: fwd 164.5 / 163.0 ->
+                         // 159.9 / 161.0 us (8x256^2x128, interleaved A/B, round 5), bit-identical outputs
+#endif
+FMD_DEV void fence8_(float (&y)[8]) {
+  asm volatile("" : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]));
+}
 
 // debug ablations (A.dbg via fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG, tools/build_variant.sh):
 // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop, 128 no step barrier, 256 no MFMA
@@ -248,6 +255,28 @@ void conv3x3_halo9b(const HArgs A) {
       const f32x4 b0 = *(const f32x4*)(coef + scb), b1 = *(const f32x4*)(coef + scb + 4);
       const float qa[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       const float qb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#if FMD_H9_FENCE
+      // the 8 elements advance stage by stage (register fences), not element by element
+      float y[8], t[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[2 * e] = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
+        y[2 * e + 1] = bf_hi(raw[e]) * qa[2 * e + 1] + qb[2 * e + 1];
+      }
+      if (PRO == 2) {
+        fence8_(y);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_exp2f(y[i] * -1.4426950408889634f);
+        fence8_(t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_rcpf(1.f + t[i]);
+        fence8_(t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = y[i] * t[i];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = pack2(y[2 * e], y[2 * e + 1]);
+#else
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float lo = bf_lo(raw[e]) * qa[2 * e] + qb[2 * e];
@@ -255,6 +284,7 @@ void conv3x3_halo9b(const HArgs A) {
         if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
         v[e] = pack2(lo, hi);
       }
+#endif
     } else {
       const bool z = (roff[q % SL] & ZFLAG) != 0;
 #pragma unroll
