@@ -26,5 +26,3 @@ struct HArgs {
 // v9 kernel (csrc/conv_halo9.hip): launches the problem A describes if it qualifies; returns 1 (not applicable),
 // 0 (launched) or a hipError_t.  pro: 0 raw input, 1 GroupNorm affine, 2 affine + SiLU.
 int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream);
-// v10 kernel (csrc/conv_halo10.hip, producer / consumer waves, persistent): same contract; tried first.
-int halo10_launch(const HArgs& A, int pro, fmd_stream_t stream);
