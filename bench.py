@@ -168,6 +168,54 @@ def config_e_leg(dev, size=128, steps=5, warmup=2):
     return out
 
 
+LDCT_VAE = dict(in_channels=1, out_channels=1, resolution=256, base_ch=128, down_channels=[128, 256, 512, 512],
+                num_res_blocks=2, attn_resolutions=[], z_channels=4, embed_dim=4, dropout=0.0, use_attention=True,
+                spatial_dims=2, emb_channels=None, use_scale_shift_norm=False, double_z=True, attn_heads=4,
+                attn_dim_head=64)   # model block of the reference's configs/LDCT/LDCT_autoencoder_kl.json
+CONFIG_D_GF = (269.2, 618.7, 7.748)   # encode, decode, one latent UNet step, GFLOP per image
+
+
+def config_d_leg(dev, batch=8, steps=50, reps=3):
+    """BASELINE.json configs[3] on one GPU: AutoencoderKL of LDCT_autoencoder_kl.json (82,599,141 parameters) + the
+    latent FM UNet (the LDCT FM UNet block with 4 latent channels, concatenate conditioning on the encoded latent),
+    random init; encode_vae_batch -> 50-step FlowMatchEuler sampler (graph-replayed) -> decode_vae_batch on
+    synthetic 256x256 images, batch 8 (reference vae_utils.py:54-85, pipelines/utils.py:163-220).  Median of
+    ``reps`` timed passes after one warm-up pass."""
+    import warnings
+    from fmdiff.models.generators import DiffusionUNetFactory
+    from fmdiff.models.vae import AutoencoderKL
+    from fmdiff.pipelines.latent import decode_vae_batch, encode_vae_batch
+    from fmdiff.pipelines.train.fused import FusedFlowSampler
+    torch.manual_seed(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        vae = AutoencoderKL(**LDCT_VAE).to(dev).eval()
+    unet = DiffusionUNetFactory().build(dict(LDCT_FM_UNET, in_channels=4, out_channels=4, sample_size=32),
+                                        "concatenate", 4).to(dev)
+    sampler = FusedFlowSampler(unet, steps)
+    g = torch.Generator(device=dev).manual_seed(3)
+    img = torch.rand(batch, 1, 256, 256, device=dev, generator=g)
+    times = []
+    with torch.no_grad():
+        for r in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            cond = encode_vae_batch(vae, img).contiguous()
+            lat = sampler.sample(torch.randn(cond.shape, device=dev, generator=g), cond, use_graph=True)
+            out = decode_vae_batch(vae, lat)
+            torch.cuda.synchronize()
+            if r:
+                times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]
+    gf = batch * (CONFIG_D_GF[0] + CONFIG_D_GF[1] + steps * CONFIG_D_GF[2])
+    res = dict(workload=f"config D: AutoencoderKL encode -> {steps}-step latent FM-Euler -> decode, batch {batch}, "
+                        f"256x256 -> 4x32x32", images_per_sec=batch / dt, ms=dt * 1e3, tflops=gf / dt / 1e3,
+               mfma_frac=gf / dt / 1e3 / PEAK_BF16_TFLOPS, out_mean=float(out.mean()))
+    del vae, unet, sampler
+    torch.cuda.empty_cache()
+    return res
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -260,6 +308,7 @@ def main():
     ap.add_argument("--no-sampler", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the per-kernel roofline legs")
     ap.add_argument("--no-config-e", action="store_true", help="skip the config E (3-D 128^3) leg")
+    ap.add_argument("--no-config-d", action="store_true", help="skip the config D (latent diffusion) leg")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -404,6 +453,13 @@ def main():
             log(f"[bench] config E: {cfg_e['ms_per_step']:.1f} ms/step, {cfg_e['mfma_frac']:.3f} of peak")
         except Exception as e:  # pragma: no cover
             cfg_e = dict(error=str(e))
+    cfg_d = None
+    if world == 1 and not args.no_config_d:
+        try:
+            cfg_d = config_d_leg(dev)
+            log(f"[bench] config D: {cfg_d['images_per_sec']:.1f} images/s ({cfg_d['ms']:.1f} ms per batch)")
+        except Exception as e:  # pragma: no cover
+            cfg_d = dict(error=str(e))
     step_tflops = train_ips / world * TRAIN_GFLOP_PER_IMAGE / 1e3
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -435,6 +491,7 @@ def main():
         "roofline_backward": back,
         "config_e_ms_per_step": cfg_e.get("ms_per_step") if cfg_e else None,
         "config_e": cfg_e,
+        "config_d": cfg_d,
         "cpu_baseline": cpu,
     }
     print(json.dumps(res), flush=True)

@@ -369,6 +369,10 @@ class FusedTrainStep:
             dst.copy_(src)
         self.flat.grad.zero_()
         del snap
+        # the weight layouts are created lazily by the first forward, after that step's refresh: refresh once
+        # more here so the batched job tables exist before capture (a table built while capturing would be a
+        # host-to-device copy inside the graph) -- with warmup_iters=1 no eager refresh has seen them yet
+        self.eng.invalidate_weights()
         g = torch.cuda.CUDAGraph()
         # multi-rank: thread-local capture, so the process group's watchdog thread may keep querying its
         # (already completed) events while this thread records

@@ -15,5 +15,5 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 step bench gpurun_out/bench.json timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5}
 step prof gpurun_out/prof/bench.json timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-  -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --sampler-steps 5 --no-config-e
+  -d gpurun_out/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --sampler-steps 5 --no-config-e --no-config-d
 find gpurun_out/prof -name "*stats*"
