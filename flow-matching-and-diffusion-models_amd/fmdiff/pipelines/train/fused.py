@@ -42,8 +42,11 @@ def _own_stream(fn):
     inf) -- with the graphs replayed on the null stream, with a host synchronisation between the replay and the
     all-reduce, and also with this hand-off to a private stream; with the whole process on a created stream
     (``torch.cuda.set_stream`` before any work, as bench.py and the trainer loop do) every run was bit-identical
-    to the eager reference.  The cause is not established, so a multi-rank step from the null stream is refused
-    (RuntimeError) rather than run on possibly corrupt gradients; single-process callers keep the hand-off."""
+    to the eager reference.  Round 5 ruled out the stream half of that chain: graph replays on the null stream
+    handed to a created stream by an event (or ``wait_stream``) are ordered exactly (tests/test_gpu_null_stream.py,
+    every copy bit-exact), so the fault lies on the collective side, which no pool box (one GPU) can exercise over
+    RCCL.  Until it can be, a multi-rank step from the null stream is refused (RuntimeError) rather than run on
+    possibly corrupt gradients; single-process callers keep the hand-off."""
     @functools.wraps(fn)
     def wrapped(self, *a, **kw):
         cur = torch.cuda.current_stream()

@@ -253,3 +253,21 @@ def test_model_throughput_fields_match_reference_formulas():
                    "model_seconds_per_sample": "0.25000000", "model_calls": 100}
     empty = model_throughput({}, 0)
     assert empty["model_samples_per_second"] == "0.000000" and empty["model_seconds_per_sample"] == "0.00000000"
+
+
+# ------------------------------------------------------------------ bench.py's roofline traffic lookup
+def test_bench_pmc_traffic_matches_timed_kernel_only():
+    """bench.py reports ``roofline.traffic`` only from a committed PMC summary of the very kernel(s) it times
+    (profiles/r*_traffic.json ``kernel_id``), the newest round first; any other kernel gets None."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    fwd = bench.pmc_traffic("conv3x3_halo9b<false, 2, 0>")
+    assert fwd is not None and fwd["file"].startswith("profiles/r5_")
+    assert 2.5e8 < fwd["bytes"] < 4e8   # ~1.05x the 276.8 MB algorithmic bytes of the 8x256^2x128 problem
+    wg = bench.pmc_traffic(["wgrad_reduce2", "wgrad_halo_kernel<2>"])   # order-free set of kernels
+    assert wg is not None and wg["file"].endswith("r5_wgrad_traffic.json")
+    assert bench.pmc_traffic("conv3x3_halo<false, 2, false>") is None   # round 3's kernel: not the timed one
+    assert bench.pmc_traffic(["wgrad_halo_kernel<2>"]) is None          # a subset is not the timed pair

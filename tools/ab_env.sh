@@ -10,7 +10,7 @@ if [ -n "$AB_TESTS" ]; then
   rc=$?; echo "tests rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 for setting in $AB; do
-  env ${setting//,/ } timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-sampler --no-roofline --no-config-e \
+  env ${setting//,/ } timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-sampler --no-roofline --no-config-e --no-config-d \
     > gpurun_out/ab_$setting.json 2> gpurun_out/ab_$setting.err
   rc=$?; echo "$setting rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$setting.json)"; [ $rc -eq 0 ] || exit $rc
 done

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for r in 1 2; do
   for v in "$@"; do
     if [ "$v" = product ]; then lib=""; else lib="FMD_LIB=$V/libfmdiff_$v.so"; fi
-    env $lib timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-sampler \
+    env $lib timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-sampler --no-config-e --no-config-d \
       > gpurun_out/abl_${v}_$r.json 2> gpurun_out/abl_${v}_$r.err
     rc=$?; echo "$v $r rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abl_${v}_$r.json)"; [ $rc -eq 0 ] || exit $rc
   done
