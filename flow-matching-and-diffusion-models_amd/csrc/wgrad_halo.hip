@@ -286,264 +286,6 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// Deeper pipeline (round 5).  wgrad_halo_kernel keeps one tile of lookahead: the loads of tile t+1 are issued at
-// the start of tile t and waited for at its end, and the per-tile fetch round trip (~3.5 us with every CU
-// streaming; the kernel without MFMAs still took 72 % of its time) is longer than a tile's MFMAs (~1.9 us).  Here
-// both operands run TWO tiles ahead: dY by LDS-DMA into a third LDS stage, x (which needs the GN+SiLU transform on
-// its way to LDS) into two register sets used in turn; the GN affine of the workgroup's samples sits in an LDS
-// table, so the loop holds no hipcc-visible global load (hipcc's waitcnt pass does not see the asm loads, and a
-// visible load would make it drain every outstanding one).  Counted waits: per tile a wave issues DY_OPS DMAs then
-// XLD x loads, so before storing tile t+1's x the wave lets the DY_OPS + XLD ops of tile t+2 stay in flight.
-constexpr int DSTG = 3;                          // dY LDS stages
-constexpr int ABN = 4;                           // samples of GN affine in the LDS table
-constexpr int DY_OPS = 4;                        // dY DMA instructions per wave per tile
-
-template <int PRO, bool UPS>
-__global__ __launch_bounds__(512) void wgrad_halo_pipe(const HWArgs A) {
-  __shared__ __attribute__((aligned(16))) bf16r lds[2 * XBUF + DSTG * DBUF];
-  __shared__ __attribute__((aligned(16))) float abt[ABN][2][WCI];
-  bf16r* xb = lds;
-  bf16r* db_ = lds + 2 * XBUF;
-  const unsigned db_base = (unsigned)(size_t)(__attribute__((address_space(3))) bf16r*)db_;
-  const fmd_wgrad_desc& d = A.d;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wco = wid >> 2, wci = wid & 3;
-  const int l16 = lane & 15, lq = lane >> 4;
-  const int rq = l16 >> 2, rp = lane & 3;
-
-  int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int tci = b % A.nci; b /= A.nci;
-  const int tco = b % A.ntc; b /= A.ntc;
-  const int split = b;
-  const int kz = A.depth ? tci / A.ncc : 0;
-  const int zsh = A.depth ? kz - 1 : 0;
-  const int co0 = tco * WCO, ci0 = (A.depth ? tci - kz * A.ncc : tci) * WCI;
-  const int T = A.depth ? 27 : 9;
-  const int t0 = split * A.per_split, t1 = min(A.ntiles, t0 + A.per_split);
-  const bool do_bias = d.db != nullptr && tci == 0;
-
-  const bf16r* __restrict__ dy = (const bf16r*)d.dy;
-  const bf16r* __restrict__ s0 = (const bf16r*)d.src0;
-  const bf16r* __restrict__ s1 = (const bf16r*)d.src1;
-  const int kx8 = (tid >> 3) & 7;
-  const int c = ci0 + kx8 * 8;
-  const char* xsrc = (const char*)((c < d.C0) ? s0 + c : s1 + (c - d.C0));
-  const unsigned xcs2 = 2u * (unsigned)((c < d.C0) ? d.C0 : d.C1);   // bytes per source pixel
-  const int per_img = A.tiles_x * A.tiles_y;
-  auto sample_of = [&](int t) { const int n = t / per_img; return A.depth ? n / A.depth : n; };
-  const int smp0 = t0 < t1 ? sample_of(t0) : 0;
-
-  if (PRO != 0) {   // GN affine of samples smp0 .. smp0 + ABN - 1 (the host guarantees a split spans <= ABN)
-    for (int e = tid; e < ABN * 2 * WCI; e += NT) {
-      const int s = e / (2 * WCI), w = (e / WCI) & 1, cc = e % WCI, sm = smp0 + s;
-      abt[s][w][cc] = sm < d.N ? (w ? d.pro_b : d.pro_a)[(size_t)sm * A.C + ci0 + cc] : 0.f;
-    }
-  }
-
-  auto tile_org = [&](int t, int& n, int& ty0, int& tx0) {
-    n = t / per_img;
-    const int r = t - n * per_img;
-    ty0 = (r / A.tiles_x) * WTH;
-    tx0 = (r - (r / A.tiles_x) * A.tiles_x) * WTW;
-  };
-  // staging slot k of this thread for tile t: global element offset (pixel 0 when padding / inactive) and LDS
-  // offset (-1 inactive, bit 30 zero padding)
-  // per-tile (workgroup-uniform) part of the x staging addresses
-  struct TileX { int ty0, tx0, srcsl; bool zok; };
-  auto tile_x = [&](int t) {
-    TileX X;
-    int n;
-    tile_org(t, n, X.ty0, X.tx0);
-    const int smp = A.depth ? n / A.depth : n;
-    const int zl = A.depth ? n - smp * A.depth + zsh : 0;
-    X.zok = !A.depth || (zl >= 0 && zl < A.depth);
-    X.srcsl = A.depth ? smp * A.dsrc + (UPS ? zl >> 1 : zl) : n;
-    return X;
-  };
-  // staging slot k of this thread: 32-bit byte offset from xsrc (0 for padding / inactive; the host keeps the
-  // source under 4 GiB) and LDS offset (-1 inactive, bit 30 zero padding)
-  auto x_slot = [&](const TileX& X, int k, unsigned& boff, int& lo) {
-    const int pos = (tid & 7) + 8 * (tid >> 6) + (NT / 8) * k;
-    const bool act = pos < HPOSW;
-    const int hy = act ? pos / HR : 0, hx = act ? pos - (pos / HR) * HR : 0;
-    const int y = X.ty0 - 1 + hy, x = X.tx0 - 1 + hx;
-    const bool valid = act && X.zok && (unsigned)y < (unsigned)d.Ho && (unsigned)x < (unsigned)d.Wo;
-    const int sy = UPS ? y >> 1 : y, sx = UPS ? x >> 1 : x;
-    boff = valid ? (unsigned)((X.srcsl * d.Hs + sy) * d.Ws + sx) * xcs2 : 0u;
-    lo = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
-  };
-  // x loads of tile t into r (asm: untracked by hipcc; every lane issues all XLD so the per-wave count is fixed)
-  auto x_issue = [&](int t, u32x4 (&r)[XLD]) {
-    const TileX X = tile_x(t);
-#pragma unroll
-    for (int k = 0; k < XLD; ++k) {
-      unsigned boff;
-      int lo;
-      x_slot(X, k, boff, lo);
-      const char* p = xsrc + boff;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[k]) : "v"(p) : "memory");
-    }
-  };
-  auto dma_dy = [&](int t, int buf) {
-    int n, ty0, tx0;
-    tile_org(t, n, ty0, tx0);
-#pragma unroll
-    for (int j = 0; j < DY_OPS; ++j) {
-      const int idx = wid * 4 + j, plane = idx >> 1, half = idx & 1;
-      const int pos = half * 64 + lane;
-      const int pix = (n * d.Ho + ty0 + (pos >> 4)) * d.Wo + tx0 + (pos & 15);
-      const unsigned dst = db_base + (unsigned)(buf * DBUF + (plane * DPAD + half * 64) * 8) * 2;
-      glds16(dy + (size_t)pix * A.ldy + co0 + plane * 8, __builtin_amdgcn_readfirstlane(dst));
-    }
-  };
-  // transform (GN affine [+ SiLU] from the LDS table) and store tile t's x from r into x buffer buf
-  auto store_x = [&](int t, const u32x4 (&r)[XLD], int buf) {
-    const int sl = PRO != 0 ? sample_of(t) - smp0 : 0;
-    float pa[8], pb[8];
-    if (PRO != 0) {
-      const f32x4 a0 = *(const f32x4*)&abt[sl][0][kx8 * 8], a1 = *(const f32x4*)&abt[sl][0][kx8 * 8 + 4];
-      const f32x4 b0 = *(const f32x4*)&abt[sl][1][kx8 * 8], b1 = *(const f32x4*)&abt[sl][1][kx8 * 8 + 4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { pa[e] = a0[e]; pa[4 + e] = a1[e]; pb[e] = b0[e]; pb[4 + e] = b1[e]; }
-    }
-    const TileX X = tile_x(t);
-#pragma unroll
-    for (int k = 0; k < XLD; ++k) {
-      unsigned boff;
-      int o;
-      x_slot(X, k, boff, o);
-      u32x4 v = r[k];
-      if (PRO != 0) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float lo = bf_lo(v[e]) * pa[2 * e] + pb[2 * e];
-          float hi = bf_hi(v[e]) * pa[2 * e + 1] + pb[2 * e + 1];
-          if (PRO == 2) { lo = siluf_(lo); hi = siluf_(hi); }
-          v[e] = pack2(lo, hi);
-        }
-      }
-      if (o & (1 << 30)) v = u32x4{0u, 0u, 0u, 0u};
-      if (o >= 0) *(u32x4*)(xb + buf * XBUF + (o & ~(1 << 30))) = v;
-    }
-  };
-
-  f32x4 acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbs[4] = {0.f, 0.f, 0.f, 0.f};
-
-  const bf16r* const abase = db_ + ((wco * 8 + (rp >> 1)) * DPAD + (lq >> 1) * WTW + 8 * (lq & 1) + rq) * 8 + (rp & 1) * 4;
-  const bf16r* const bbase = xb + ((wci * 2 + (rp >> 1)) * XPAD + (lq >> 1) * HR + 8 * (lq & 1) + rq) * 8 + (rp & 1) * 4;
-  auto readA = [&](int dbuf, int ks, bf16x8 (&a)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16r* p = abase + dbuf * DBUF + (ks * 2 * WTW + 2 * i * DPAD) * 8;
-      const s16x4 lo = ds_read_tr16(p), hi = ds_read_tr16(p + 4 * 8);
-      a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    }
-  };
-  auto compute = [&](int xbuf, int dbuf) {
-    bf16x8 af[2][4], bq[3];
-    auto readB = [&](int sl) {
-      const int ks = sl / 9, tap = sl % 9, ky = tap / 3, kx = tap % 3;
-      const bf16r* p = bbase + xbuf * XBUF + ((2 * ks + ky) * HR + kx) * 8;
-      const s16x4 lo = ds_read_tr16(p), hi = ds_read_tr16(p + 4 * 8);
-      bq[sl % 3] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    readA(dbuf, 0, af[0]);
-    readB(0);
-    readB(1);
-#pragma unroll
-    for (int sl = 0; sl < 36; ++sl) {
-      const int ks = sl / 9, tap = sl % 9;
-      if (tap == 4 && ks < 3) readA(dbuf, ks + 1, af[(ks + 1) & 1]);
-      if (sl + 2 < 36) readB(sl + 2);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][tap] = mfma16(af[ks & 1][i], bq[sl % 3], acc[i][tap]);
-    }
-  };
-  auto bias_sums = [&](int dbuf) {
-    bf16x8 a[4];
-    readA(dbuf, wci, a);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float sacc = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sacc += (float)a[i][e];
-      dbs[i] += sacc;
-    }
-  };
-  // one tile: the loads of tile t+2 go out first, tile t runs from LDS, then tile t+1's x (loaded one tile ago,
-  // in nxt) is transformed into the other x buffer; fre receives tile t+2's x.  The asm loads and waits run
-  // unconditionally (tiles past the split's end re-load its last tile), so every wave's count is the same at
-  // every wait and the register sets never pass through a control-flow merge (where hipcc may copy them before
-  // the data lands)
-  auto body = [&](int t, u32x4 (&nxt)[XLD], u32x4 (&fre)[XLD]) {
-    const int j = t - t0;
-    dma_dy(min(t + 2, t1 - 1), (j + 2) % DSTG);
-    x_issue(min(t + 2, t1 - 1), fre);
-    if (t < t1) {
-      compute(j & 1, j % DSTG);
-      if (do_bias) bias_sums(j % DSTG);
-    }
-    asm volatile("s_waitcnt vmcnt(7)" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]) :: "memory");
-    if (t + 1 < t1) store_x(t + 1, nxt, (j + 1) & 1);
-    __syncthreads();   // tile t+1's x stored, its dY landed (every wave waited for its own DMAs); buffers of t free
-  };
-  static_assert(XLD == 3 && DY_OPS + XLD == 7, "counted waits assume 4 DMAs + 3 x loads per wave per tile");
-
-  if (t0 < t1) {
-    u32x4 rA[XLD], rB[XLD];
-    __syncthreads();   // the affine table
-    dma_dy(t0, 0);
-    x_issue(t0, rA);
-    dma_dy(min(t0 + 1, t1 - 1), 1);
-    x_issue(min(t0 + 1, t1 - 1), rB);
-    asm volatile("s_waitcnt vmcnt(7)" : "+v"(rA[0]), "+v"(rA[1]), "+v"(rA[2]) :: "memory");
-    store_x(t0, rA, 0);
-    __syncthreads();
-    for (int t = t0; t < t1; t += 2) {
-      body(t, rB, rA);
-      body(t + 1, rA, rB);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-loads (LDS-DMA included) land in this workgroup
-  }
-
-  const size_t per = (size_t)d.K * T * A.C;
-  float* ws = d.ws + (size_t)split * per;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
-        const int ci = ci0 + wci * 16 + l16;
-        ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[i][tap][r];
-      }
-  if (do_bias) {
-    float* red = (float*)lds;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dbs[i] += __shfl_xor(dbs[i], 16, 64);
-      dbs[i] += __shfl_xor(dbs[i], 32, 64);
-    }
-    __syncthreads();
-    if (lq == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[wci * WCO + wco * 64 + 16 * i + l16] = dbs[i];
-    }
-    __syncthreads();
-    if (tid < WCO) {
-      const float v = red[tid] + red[WCO + tid] + red[2 * WCO + tid] + red[3 * WCO + tid];
-      d.ws[(size_t)A.splits * per + (size_t)split * d.K + co0 + tid] = v;
-    }
-  }
-}
-
 }  // namespace
 
 // 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
@@ -582,23 +324,6 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int nwg = A.ntc * A.nci * A.splits;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
-  static const int pipe = [] {
-    const char* e = getenv("FMD_WGRAD_PIPE");
-    return e && *e ? atoi(e) : 0;
-  }();
-  const long long tiles_per_sample = (long long)A.tiles_x * A.tiles_y * (d3 ? d->Do : 1);
-  const long long src_bytes = 2LL * (d3 ? (long long)d->N * d->Ds : (long long)d->N) * d->Hs * d->Ws *
-                              (d->C0 > d->C1 ? d->C0 : d->C1);
-  if (pipe && (pro == 0 || A.per_split <= (ABN - 1) * tiles_per_sample) && src_bytes < (1LL << 32)) {
-#define FMD_WGP(P, U) hipLaunchKernelGGL((wgrad_halo_pipe<P, U>), dim3(nwg), dim3(NT), 0, st, A)
-    if (d->upsample) {
-      if (pro == 2) FMD_WGP(2, true); else if (pro == 1) FMD_WGP(1, true); else FMD_WGP(0, true);
-    } else {
-      if (pro == 2) FMD_WGP(2, false); else if (pro == 1) FMD_WGP(1, false); else FMD_WGP(0, false);
-    }
-#undef FMD_WGP
-    return (int)hipGetLastError();
-  }
   if (pro == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(nwg), dim3(NT), 0, st, A);
   else if (pro == 1) hipLaunchKernelGGL(wgrad_halo_kernel<1>, dim3(nwg), dim3(NT), 0, st, A);
   else hipLaunchKernelGGL(wgrad_halo_kernel<0>, dim3(nwg), dim3(NT), 0, st, A);
