@@ -89,12 +89,18 @@ FMD_DEV TilePos tile_pos(const HeadArgs& A, int t) {
   return P;
 }
 
-// KZ = 1: 2-D; KZ = 3: 3-D (one depth plane of taps per pass over the chunk, zero depth padding)
-template <int KT, int KZ>
-__global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
-  __shared__ __attribute__((aligned(16))) u32x4 halo[KCP * HPADP];
-  __shared__ __attribute__((aligned(16))) unsigned int wl[KT][9][CK / 2];   // chunk weights [k][tap][c pair], bf16x2
-  const int tid = threadIdx.x;
+// KZ = 1: 2-D; KZ = 3: 3-D (one depth plane of taps per pass over the chunk, zero depth padding).
+// CG chunk groups: a workgroup of CG x 256 threads, group g taking the 32-channel chunks g, g + CG, ... of the tile
+// with its own halo / weight buffers, the groups' sums combined in LDS at the end -- for grids of a few tiles (the
+// latent UNet's 32^2 head: 32 tiles of 16x16, 4 chunks each; the VAE encoder's 512-channel head: 16 chunks), where a
+// single 256-thread group would walk every chunk serially on 32 of the 256 CUs
+template <int KT, int KZ, int CG>
+__global__ __launch_bounds__(NTH * CG) void head_fwd(const HeadArgs A) {
+  __shared__ __attribute__((aligned(16))) u32x4 halo_all[CG][KCP * HPADP];
+  __shared__ __attribute__((aligned(16))) unsigned int wl_all[CG][KT][9][CK / 2];   // chunk weights [k][tap][c pair]
+  const int tid = threadIdx.x % NTH, grp = threadIdx.x / NTH;
+  u32x4* halo = halo_all[grp];
+  unsigned int (*wl)[9][CK / 2] = wl_all[grp];
   const TilePos P = tile_pos(A, blockIdx.x);
   const int n = P.n, ty0 = P.ty0, tx0 = P.tx0;
   const int py = tid >> 4, px = tid & 15;
@@ -102,42 +108,66 @@ __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
   float acc[KT][2];
 #pragma unroll
   for (int k = 0; k < KT; ++k) acc[k][0] = acc[k][1] = 0.f;
-  for (int c0 = 0; c0 < A.C; c0 += CK)
-  for (int kz = 0; kz < KZ; ++kz) {
-    const int zz = P.z + kz - KZ / 2;
-    if (zz < 0 || zz >= A.D) continue;   // zero depth padding (uniform over the workgroup)
-    stage_halo(halo, A.h, P.sl + zz - P.z, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
-    for (int i = tid; i < KT * 9 * (CK / 2); i += NTH) {
-      const int k = i / (9 * (CK / 2)), r = i - k * 9 * (CK / 2), tap = r / (CK / 2), cp = r - tap * (CK / 2);
-      const size_t w0 = ((size_t)k * A.C + c0 + 2 * cp) * (9 * KZ) + kz * 9 + tap;
-      wl[k][tap][cp] = k < A.K ? pack2(A.w[w0], A.w[w0 + 9 * KZ]) : 0u;
-    }
-    __syncthreads();
-    // bf16 operands straight from LDS into v_dot2c_f32_bf16 (two products per op, fp32 accumulate):
-    // no per-tap unpacking of the halo, a quarter of the fp32-FMA form's VALU ops
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int pos = (py + tap / 3) * HR + px + tap % 3;
-#pragma unroll
-      for (int kc = 0; kc < KCP; ++kc) {
-        const u32x4 v = halo[kc * HPADP + pos];
-#pragma unroll
-        for (int k = 0; k < KT; ++k) {
-          const u32x4 w = *(const u32x4*)&wl[k][tap][kc * 4];
-          float a = acc[k][kc & 1];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            // copy the vector lanes to scalars first: __builtin_bit_cast of an ext_vector element lvalue
-            // reads lane 0 (hipcc 7.2), which silently dotted the first channel pair four times
-            const unsigned int ve = v[e], we = w[e];
-            a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_, ve), __builtin_bit_cast(bf16x2_, we), a,
-                                                false);
-          }
-          acc[k][kc & 1] = a;
+  const int rounds = (A.C / CK + CG - 1) / CG;   // every group passes the same barriers
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int c0 = (rd * CG + grp) * CK;
+    const bool act = c0 < A.C;
+    for (int kz = 0; kz < KZ; ++kz) {
+      const int zz = P.z + kz - KZ / 2;
+      if (zz < 0 || zz >= A.D) continue;   // zero depth padding (uniform over the workgroup)
+      if (act) {
+        stage_halo(halo, A.h, P.sl + zz - P.z, n, A.H, A.W, A.C, ty0, tx0, c0, A.pa, A.pb, tid);
+        for (int i = tid; i < KT * 9 * (CK / 2); i += NTH) {
+          const int k = i / (9 * (CK / 2)), r = i - k * 9 * (CK / 2), tap = r / (CK / 2), cp = r - tap * (CK / 2);
+          const size_t w0 = ((size_t)k * A.C + c0 + 2 * cp) * (9 * KZ) + kz * 9 + tap;
+          wl[k][tap][cp] = k < A.K ? pack2(A.w[w0], A.w[w0 + 9 * KZ]) : 0u;
         }
       }
+      __syncthreads();
+      // bf16 operands straight from LDS into v_dot2c_f32_bf16 (two products per op, fp32 accumulate):
+      // no per-tap unpacking of the halo, a quarter of the fp32-FMA form's VALU ops
+      if (act) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int pos = (py + tap / 3) * HR + px + tap % 3;
+#pragma unroll
+          for (int kc = 0; kc < KCP; ++kc) {
+            const u32x4 v = halo[kc * HPADP + pos];
+#pragma unroll
+            for (int k = 0; k < KT; ++k) {
+              const u32x4 w = *(const u32x4*)&wl[k][tap][kc * 4];
+              float a = acc[k][kc & 1];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                // copy the vector lanes to scalars first: __builtin_bit_cast of an ext_vector element lvalue
+                // reads lane 0 (hipcc 7.2), which silently dotted the first channel pair four times
+                const unsigned int ve = v[e], we = w[e];
+                a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_, ve), __builtin_bit_cast(bf16x2_, we),
+                                                    a, false);
+              }
+              acc[k][kc & 1] = a;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float sum[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) sum[k] = acc[k][0] + acc[k][1];
+  if (CG > 1) {   // groups 1.. hand their sums to group 0 through LDS (the halo buffers are free after the barrier)
+    float* red = (float*)&halo_all[0][0];
+    if (grp > 0) {
+#pragma unroll
+      for (int k = 0; k < KT; ++k) red[((grp - 1) * KT + k) * NTH + tid] = sum[k];
     }
     __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int g = 1; g < CG; ++g)
+#pragma unroll
+      for (int k = 0; k < KT; ++k) sum[k] += red[((g - 1) * KT + k) * NTH + tid];
   }
   const size_t p = ((size_t)(P.sl * A.H) + ty0 + py) * A.W + tx0 + px;
   float* o = A.out + p * A.Kp;
@@ -149,7 +179,7 @@ __global__ __launch_bounds__(256) void head_fwd(const HeadArgs A) {
       float r = 0.f;
 #pragma unroll
       for (int j = 0; j < KT; ++j)
-        if (j == kk) r = acc[j][0] + acc[j][1];
+        if (j == kk) r = sum[j];
       v[e] = kk < A.K ? r + (A.bias ? A.bias[kk] : 0.f) : 0.f;
     }
     *(f32x4*)(o + k) = v;
@@ -411,7 +441,26 @@ int fmd_head_fwd(const void* h, int32_t N, int32_t D, int32_t H, int32_t W, int3
   A.bias = bias;
   A.out = out;
   hipStream_t st = (hipStream_t)s;
-  HEAD_LAUNCH(head_fwd, dim3(A.ntiles), A, st);
+  // chunk groups when the tiles alone leave most CUs idle (fewer than 128 tiles) and there are chunks to share
+  const bool cg4 = A.ntiles < 128 && C >= 4 * CK;
+#define FMD_HEAD_FWD(CGV)                                                                              \
+  do {                                                                                                 \
+    const dim3 g(A.ntiles), b(NTH * CGV);                                                              \
+    if (A.T == 27) {                                                                                   \
+      if (kt_of(K) == 1) hipLaunchKernelGGL((head_fwd<1, 3, CGV>), g, b, 0, st, A);                    \
+      else hipLaunchKernelGGL((head_fwd<2, 3, CGV>), g, b, 0, st, A);                                  \
+    } else {                                                                                           \
+      switch (kt_of(K)) {                                                                              \
+        case 1: hipLaunchKernelGGL((head_fwd<1, 1, CGV>), g, b, 0, st, A); break;                      \
+        case 2: hipLaunchKernelGGL((head_fwd<2, 1, CGV>), g, b, 0, st, A); break;                      \
+        case 4: hipLaunchKernelGGL((head_fwd<4, 1, CGV>), g, b, 0, st, A); break;                      \
+        default: hipLaunchKernelGGL((head_fwd<8, 1, CGV>), g, b, 0, st, A); break;                     \
+      }                                                                                                \
+    }                                                                                                  \
+  } while (0)
+  if (cg4) FMD_HEAD_FWD(4);
+  else FMD_HEAD_FWD(1);
+#undef FMD_HEAD_FWD
   return (int)hipGetLastError();
 }
 

@@ -766,13 +766,15 @@ def test_weight_cache_cubic_batched_refresh_matches_individual_preps():
         assert torch.equal(got, ref), (kind, wi, mode)
 
 
-@pytest.mark.parametrize("K", [1, 3])
-def test_head_kernels_vs_torch(K):
+@pytest.mark.parametrize("K,C", [(1, 64), (3, 64), (1, 160), (8, 512)])
+def test_head_kernels_vs_torch(K, C):
     """csrc/head.hip: GN-affine+SiLU -> 3x3 conv to K <= 8 channels (fp32 out, Kp = 8), its data gradient
     (SiLU' epilogue + GN-backward sums) and weight/bias gradients, vs torch fp32 autograd on the same
-    bf16-rounded inputs.  Tolerance: 1e-2 x max|ref| (bf16 transformed activations / bf16 dz)."""
+    bf16-rounded inputs.  Tolerance: 1e-2 x max|ref| (bf16 transformed activations / bf16 dz).  12 tiles: from
+    C = 128 the forward runs as 4 chunk groups per workgroup (C = 160: 5 chunks, groups idle in the second round;
+    C = 512, K = 8: the VAE encoder's head shape)."""
     O = ops()
-    N, H, W, C = 2, 32, 48, 64
+    N, H, W = 2, 32, 48
     g = torch.Generator().manual_seed(11)
     h = _rand_nhwc(N, H, W, C, 12)
     a = torch.rand(N, C, generator=g) + 0.5
@@ -791,7 +793,8 @@ def test_head_kernels_vs_torch(K):
     br = bias.clone().requires_grad_()
     ref = F.conv2d(t, wr, br, padding=1)
     _close(out[..., :K], ref.permute(0, 2, 3, 1), rel=1e-2)
-    assert out[..., K:].abs().max().item() == 0.0
+    if K < out.shape[-1]:
+        assert out[..., K:].abs().max().item() == 0.0
     dref = _to_nchw(dpred)[:, :K]
     ref.backward(dref)
     dw = torch.zeros(K, C, 3, 3, device=DEV)
@@ -812,14 +815,14 @@ def test_head_kernels_vs_torch(K):
     torch.testing.assert_close(s[..., 1], (dzd * xs).sum(1), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("K", [1, 2])
-def test_head_kernels_3d_vs_torch(K):
+@pytest.mark.parametrize("K,C", [(1, 64), (2, 64), (1, 160)])
+def test_head_kernels_3d_vs_torch(K, C):
     """csrc/head.hip with depth (D > 0): GN-affine+SiLU -> 3x3x3 conv (zero depth padding) to K <= 2
     channels, its data gradient + GN-backward sums and its weight/bias gradients, vs torch fp32 conv3d
     autograd on the same bf16 inputs (the ConvND(dims=3) head of src/models/unet/unet.py:286-293).
     Tolerance: 1e-2 x max|ref| as in the 2-D test."""
     O = ops()
-    N, D, H, W, C = 2, 5, 16, 32, 64
+    N, D, H, W = 2, 5, 16, 32
     g = torch.Generator().manual_seed(21)
     h = (torch.randn(N, D, H, W, C, generator=g)).to(torch.bfloat16)
     a = torch.rand(N, C, generator=g) + 0.5

@@ -3,8 +3,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+i=0
 for setting in $AB; do
-  env $setting timeout -k 10 200 python tools/bench_latent.py ${LATENT_ARGS} > gpurun_out/abl_$setting.json 2> gpurun_out/abl_$setting.err
-  rc=$?; echo "$setting rc=$rc $(grep -o '"images_per_sec": [0-9.]*\|"sample": [0-9.]*' gpurun_out/abl_$setting.json | tr '\n' ' ')"
+  i=$((i + 1))
+  env $setting timeout -k 10 200 python tools/bench_latent.py ${LATENT_ARGS} > gpurun_out/abl_$i.json 2> gpurun_out/abl_$i.err
+  rc=$?; echo "$setting rc=$rc $(grep -o '"images_per_sec": [0-9.]*\|"sample": [0-9.]*' gpurun_out/abl_$i.json | tr '\n' ' ')"
   [ $rc -eq 0 ] || exit $rc
 done
