@@ -680,7 +680,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d,
 // CB = max(FMD_CONV_GN_CB (default 4), Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
 // pixel lane) over the image's pixels (slab sums in four chains, fixed order), bias / per-sample bias / residual,
 // bf16 out, and the channel sums of the rounded values; lanes (shuffles), waves (LDS) and the group's channels
-// (fp64) in fixed order; pass 2 re-reads the lane's own output elements and writes t = SiLU(a*out + b).
+// (fp64) in fixed order; pass 2 writes t = SiLU(a*out + b) from the lane's own output elements (the first pixel's
+// kept in registers, later ones re-read).
 constexpr int CGN_NT = 1024;
 __global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc d, const fmd_gn_out_desc g, int M,
                                                             int CB) {
@@ -699,6 +700,7 @@ __global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc 
     add += f32x4{bn[0], bn[1], bn[2], bn[3]};
   }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  u32x2 wkeep = {0u, 0u};   // the lane's first pixel's output, kept for pass 2 (on the small levels its only one)
   for (int pp = pl; pp < HW; pp += PL) {
     const size_t idx = ((size_t)n * HW + pp) * K + c;
     f32x4 v = *(const f32x4*)(d.ws + idx), v1 = {0.f, 0.f, 0.f, 0.f}, v2 = v1, v3 = v1;
@@ -719,6 +721,7 @@ __global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc 
     w[0] = pack2(v[0], v[1]);
     w[1] = pack2(v[2], v[3]);
     *(u32x2*)((bf16r*)d.out + idx) = w;
+    if (pp == pl) wkeep = w;
     const float wr[4] = {bf_lo(w[0]), bf_hi(w[0]), bf_lo(w[1]), bf_hi(w[1])};
 #pragma unroll
     for (int r2 = 0; r2 < 4; ++r2) {
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(CGN_NT) void combine_gn_kernel(const fmd_conv_desc 
   for (int r2 = 0; r2 < 4; ++r2) { av[r2] = ab[tq * 4 + r2][0]; bv[r2] = ab[tq * 4 + r2][1]; }
   for (int pp = pl; pp < HW; pp += PL) {   // the lane's own pass-1 stores: program order makes them visible
     const size_t idx = ((size_t)n * HW + pp) * K + c;
-    const u32x2 w = *(const u32x2*)((const bf16r*)d.out + idx);
+    const u32x2 w = pp == pl ? wkeep : *(const u32x2*)((const bf16r*)d.out + idx);
     float y[4] = {bf_lo(w[0]) * av[0] + bv[0], bf_hi(w[0]) * av[1] + bv[1], bf_lo(w[1]) * av[2] + bv[2],
                   bf_hi(w[1]) * av[3] + bv[3]};
     if (g.silu) {
