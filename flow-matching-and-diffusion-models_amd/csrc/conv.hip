@@ -850,15 +850,8 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
 // combine = false: the split-K partial slabs only (fmd_conv_gn runs its own combine)
 static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   hipStream_t s = (hipStream_t)stream;
-  // largest output (pixels) run on 64-pixel tiles when split-K (FMD_BPX64_M; mirrored by ops.BPX64_M)
-  static const int small_m = [] {
-    const char* e = getenv("FMD_BPX64_M");
-    return e && *e ? atoi(e) : 2048;
-  }();
-  static const int tiny_m = [] {
-    const char* e = getenv("FMD_BPX32_M");
-    return e && *e ? atoi(e) : 128;
-  }();
+  // largest output (pixels) run on 64- / 32-pixel tiles when split-K (mirrored by ops.BPX64_M / BPX32_M)
+  constexpr int small_m = 2048, tiny_m = 128;
   const int C = d->C0 + d->C1;
   if ((d->C0 % 8) || (d->C1 % 8) || (d->C2 % 8) || (d->C3 % 8) || d->ks < 1 || d->N < 1) return -1;
   if (d->C3 && !d->src3) return -6;
@@ -908,15 +901,8 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
 
 extern "C" int fmd_conv(const fmd_conv_desc* d, fmd_stream_t stream) { return conv_run(d, stream, true); }
 
-static int g_conv_gn_cb = -1;
-static int conv_gn_cb() {
-  if (g_conv_gn_cb < 0) {
-    const char* e = getenv("FMD_CONV_GN_CB");
-    const int v = e && *e ? atoi(e) : 4;
-    g_conv_gn_cb = v == 8 || v == 16 || v == 32 || v == 64 ? v : 4;
-  }
-  return g_conv_gn_cb;
-}
+static int g_conv_gn_cb = 4;   // fmd_conv_gn_set_block_channels (runtime/tuning.py CONV_GN_CB)
+static int conv_gn_cb() { return g_conv_gn_cb; }
 
 extern "C" int fmd_conv_gn_set_block_channels(int32_t cb) {
   if (cb != 4 && cb != 8 && cb != 16 && cb != 32 && cb != 64) return -1;

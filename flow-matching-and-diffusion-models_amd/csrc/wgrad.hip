@@ -244,33 +244,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WArgs A) {
   }
 }
 
-// Stage 1 of a wide split-K reduction: group g sums slabs [g*Q, (g+1)*Q) into slab g*Q (in place:
-// every group writes only inside its own range).  16-byte loads, 4 independent chains.
-__global__ void wgrad_reduce_stage1(const WArgs A, int splits, int Q) {
-  const fmd_wgrad_desc& d = A.d;
-  const size_t per = (size_t)d.K * A.T * A.C;
-  const size_t nvec = per / 4;
-  const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int s0 = blockIdx.y * Q, s1 = min(splits, s0 + Q);
-  if (d.db && v < (size_t)d.K) {   // bias partials, same grouping
-    const float* wb = d.ws + (size_t)splits * per;
-    float b = 0.f;
-    for (int s = s0; s < s1; ++s) b += wb[(size_t)s * d.K + v];
-    ((float*)wb)[(size_t)s0 * d.K + v] = b;
-  }
-  if (v >= nvec) return;
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    a0 += *(const f32x4*)(d.ws + (size_t)s * per + v * 4);
-    a1 += *(const f32x4*)(d.ws + (size_t)(s + 1) * per + v * 4);
-    a2 += *(const f32x4*)(d.ws + (size_t)(s + 2) * per + v * 4);
-    a3 += *(const f32x4*)(d.ws + (size_t)(s + 3) * per + v * 4);
-  }
-  for (; s < s1; ++s) a0 += *(const f32x4*)(d.ws + (size_t)s * per + v * 4);
-  *(f32x4*)(d.ws + (size_t)s0 * per + v * 4) = (a0 + a1) + (a2 + a3);
-}
-
 // Sum the split-K slabs ws[s*sstride][k][tap][c] (s < nsl) and write the reference layout dW[k][c][tap]
 // (+ db from the same, possibly pre-reduced, bias slabs).  A block owns (k, 64 channels): it reads
 // [tap][64 c] runs and writes the contiguous dW[k][c0:c0+64][:] run through LDS.
@@ -400,34 +373,14 @@ extern "C" int fmd_wgrad(const fmd_wgrad_desc* d, fmd_stream_t stream) {
     rc = (int)hipGetLastError();
   }
   if (rc) return rc;
-  const size_t per = (size_t)d->K * A.T * A.C;
-  // FMD_WGRAD_REDUCE (A/B runs): 1 (default) = wgrad_reduce2 in one pass (train step 22.61 -> 22.20 ms),
-  // 0 = stage 1 (> 8 splits) + wgrad_reduce (round 3), 2 = stage 1 + wgrad_reduce2
-  static const int red_mode = [] {
-    const char* e = getenv("FMD_WGRAD_REDUCE");
-    return e && *e ? atoi(e) : 1;
-  }();
   if (A.T > 27) return -4;
-  auto final_pass = [&](int nsl_, int sstride_) {
-    if (red_mode && A.C % 4 == 0) {
-      const int sl = max(1, min(nsl_, 512 / (16 * A.T)));
-      hipLaunchKernelGGL(wgrad_reduce2, dim3(d->K, (A.C + RC - 1) / RC), dim3(512), 0, s, A, splits, nsl_, sstride_, sl);
-    } else {
-      hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, nsl_, sstride_);
-    }
-    return (int)hipGetLastError();
-  };
-  if (red_mode == 1 && A.C % 4 == 0) return final_pass(splits, 1);
-  const int vblocks = (int)((per / 4 + 255) / 256);
-  int nsl = splits, sstride = 1;
-  if (splits > 8) {   // two stages: enough threads in flight for a wide split
-    const int Q = 8;
-    sstride = Q;
-    nsl = (splits + Q - 1) / Q;
-    const int b1 = vblocks > (d->K + 255) / 256 ? vblocks : (d->K + 255) / 256;
-    hipLaunchKernelGGL(wgrad_reduce_stage1, dim3(b1, nsl), dim3(256), 0, s, A, splits, Q);
-    rc = (int)hipGetLastError();
-    if (rc) return rc;
+  // one pass: wgrad_reduce2 (all taps per block, slabs over slab lanes); wgrad_reduce when C % 4 != 0.  (Round 3's
+  // two-stage form -- groups of 8 slabs summed in place, then wgrad_reduce -- was 0.4 ms per train step slower.)
+  if (A.C % 4 == 0) {
+    const int sl = max(1, min(splits, 512 / (16 * A.T)));
+    hipLaunchKernelGGL(wgrad_reduce2, dim3(d->K, (A.C + RC - 1) / RC), dim3(512), 0, s, A, splits, splits, 1, sl);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce, dim3(d->K, (A.C + RC - 1) / RC), dim3(256), 0, s, A, splits, splits, 1);
   }
-  return final_pass(nsl, sstride);
+  return (int)hipGetLastError();
 }

@@ -174,8 +174,11 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, i32)
-        if os.environ.get("FMD_HALO_MIN_WG"):
-            check(L.fmd_halo_set_min_workgroups(int(os.environ["FMD_HALO_MIN_WG"])), "fmd_halo_set_min_workgroups")
+        from .runtime import tuning   # FMD_TUNE overrides the library mirrors too
+        if tuning.overridden("HALO_MIN_WG"):
+            check(L.fmd_halo_set_min_workgroups(tuning.get("HALO_MIN_WG")), "fmd_halo_set_min_workgroups")
+        if tuning.overridden("CONV_GN_CB"):
+            check(L.fmd_conv_gn_set_block_channels(tuning.get("CONV_GN_CB")), "fmd_conv_gn_set_block_channels")
         _lib = L
     return _lib
 

@@ -26,13 +26,12 @@ accumulated straight into ``param.grad`` (fp32, reference layout).
 from __future__ import annotations
 
 import math
-import os
 import weakref
 from typing import List, Optional, Tuple
 
 import torch
 
-from . import ops
+from . import ops, tuning
 from ..nn.blocks.attention import DiffusersAttentionND, SpatialCrossAttention, SpatialSelfAttention
 from ..nn.blocks.residual import ResBlockND
 from ..nn.ops.convolution import ConvND
@@ -43,16 +42,16 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 CPAD = 8      # NHWC channel padding of the model input / output (16-byte rows)
 HALO_BK = 32  # input channels per halo-kernel chunk (FMD_HALO_BK, include/fmdiff.h)
-# 3-D: materialise the GN+SiLU operand of depth-tap halo convs (FMD_MAT3D=0: fused prologue + G side output)
-MAT3D = os.environ.get("FMD_MAT3D", "1") == "1"
+# 3-D: materialise the GN+SiLU operand of depth-tap halo convs (MAT3D=0: fused prologue + G side output)
+MAT3D = bool(tuning.get("MAT3D"))
 # 3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks (csrc/conv_halo.hip)
-DEPTH_HALO = os.environ.get("FMD_DEPTH_HALO", "1") == "1"
+DEPTH_HALO = bool(tuning.get("DEPTH_HALO"))
 # stride-2 3x3 forwards and nearest-x2 data gradients on the space-to-depth halo kernel (fmd_conv_s2d); 0: the
-# implicit GEMM (A/B runs)
-S2D_HALO = os.environ.get("FMD_S2D_HALO", "1") == "1"
-# ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); FMD_POINT_1X1=0 for A/B runs
-POINT_1X1 = os.environ.get("FMD_POINT_1X1", "1") == "1"
-# training, 3-D fused-prologue halo convs (FMD_MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
+# implicit GEMM (A/B runs, runtime/tuning.py)
+S2D_HALO = bool(tuning.get("S2D_HALO"))
+# ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); POINT_1X1=0 for A/B runs
+POINT_1X1 = bool(tuning.get("POINT_1X1"))
+# training, 3-D fused-prologue halo convs (MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
 # (fmd_conv_desc.gout), which would otherwise recompute G once per depth tap.  Not on 2-D: there the extra
 # 2 B/element of HBM writes cost the forward more than the weight gradient saves.
 

@@ -7,14 +7,13 @@ captured into a hipGraph.  Activations are NHWC bf16 ``[N, H, W, C]``.
 from __future__ import annotations
 
 import ctypes as C
-import os
-import sys
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
 import torch
 
 from .. import _lib
+from . import tuning
 from .._lib import ConvDesc, GnApplyDesc, GnOutDesc, WgradDesc
 
 BF16 = torch.bfloat16
@@ -58,7 +57,7 @@ def channel_stats(x: torch.Tensor, rows: Optional[int] = None, y: Tuple = None) 
 
 # slabs with at least STATS_FOLD_MIN rows per image are folded STATS_FOLD rows at a time before the GroupNorm
 # (n, group) reductions (fmd_stats_fold): config E's 128^3 levels (32768 rows of 64 pixels)
-STATS_FOLD_MIN = int(os.environ.get("FMD_STATS_FOLD_MIN", "4096") or 0)
+STATS_FOLD_MIN = tuning.get("STATS_FOLD_MIN")
 STATS_FOLD = 128
 
 
@@ -142,7 +141,7 @@ def gn_apply_fwd(x0, x1, a, b, silu=True):
 
 
 GN_FUSED_MAX = 16384   # elements per (n, group) that fmd_gn_fused_apply holds in one workgroup's registers
-GN_FUSED = os.environ.get("FMD_GN_FUSED", "1") == "1"   # A/B switch (0: slab statistics + gn_prep + apply)
+GN_FUSED = bool(tuning.get("GN_FUSED"))   # A/B switch (0: slab statistics + gn_prep + apply)
 
 
 def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
@@ -153,18 +152,18 @@ def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
 
 # the GroupNorm forward of a split-K conv's output inside its combine (fmd_conv_gn); FMD_CONV_GN=0: the separate
 # fmd_gn_fused_apply launch (A/B runs)
-CONV_GN = os.environ.get("FMD_CONV_GN", "1") == "1"
+CONV_GN = bool(tuning.get("CONV_GN"))
 # fewest combine blocks (images x channel blocks) for which the fused form beats the two launches it replaces
 # (latent step profile: 64 blocks 13.1 us vs 5-7 + 5.2 us; 128 blocks 8.0 us, 256 blocks 7.2 us)
-CONV_GN_MIN_BLOCKS = int(os.environ.get("FMD_CONV_GN_MIN_BLOCKS", "128"))
-CONV_GN_CB = int(os.environ.get("FMD_CONV_GN_CB", "4"))   # fewest channels per combine block (fmd_conv_gn)
+CONV_GN_MIN_BLOCKS = tuning.get("CONV_GN_MIN_BLOCKS")
+CONV_GN_CB = tuning.get("CONV_GN_CB")   # fewest channels per combine block (fmd_conv_gn; _lib sets the library's)
 if CONV_GN_CB not in (4, 8, 16, 32, 64):
-    CONV_GN_CB = 4
+    raise ValueError(f"CONV_GN_CB must be 4, 8, 16, 32 or 64, not {CONV_GN_CB}")
 
 
 def conv_gn_eligible(K: int, groups: int, N: int = 1 << 30) -> bool:
     """Mirror of fmd_conv_gn's channel test (whole groups per block of max(CONV_GN_CB, K/groups) <= 64 channels,
-    CONV_GN_CB = FMD_CONV_GN_CB, default 4) plus the block-count floor."""
+    CONV_GN_CB from runtime/tuning.py, default 4) plus the block-count floor."""
     if K % 64 or K % groups or 64 % (K // groups):
         return False
     return N * (K // max(CONV_GN_CB, K // groups)) >= CONV_GN_MIN_BLOCKS
@@ -237,14 +236,14 @@ def out_hw(Hs, ks, stride, pad, upsample):
 
 # split-K of the generic implicit GEMM on small grids: >= SPLIT_MIN_STEPS k-steps per split, about
 # SPLIT_CU_MULT workgroups per CU, at most SPLIT_CAP splits (env overrides for A/B measurements)
-SPLIT_MIN_STEPS = int(os.environ.get("FMD_SPLIT_MIN_STEPS", "2"))
-SPLIT_CU_MULT = int(os.environ.get("FMD_SPLIT_CU_MULT", "2"))
-SPLIT_CAP = int(os.environ.get("FMD_SPLIT_CAP", "64"))
+SPLIT_MIN_STEPS = tuning.get("SPLIT_MIN_STEPS")
+SPLIT_CU_MULT = tuning.get("SPLIT_CU_MULT")
+SPLIT_CAP = tuning.get("SPLIT_CAP")
 # outputs of at most BPX64_M pixels (K > 64, split-K) run on 64-pixel tiles (csrc/conv.hip small_m, FMD_BPX64_M)
 # (train step 24.94 / 25.03 -> 24.83 / 24.87 ms, config D batch 8 77 -> 82.6 images/s); at most BPX32_M: 32-pixel
 # tiles (the latent UNet's 4x4 .. 1x1 levels: 82.3 -> 83.1 images/s)
-BPX64_M = int(os.environ.get("FMD_BPX64_M", "2048") or 0)
-BPX32_M = int(os.environ.get("FMD_BPX32_M", "128") or 0)
+BPX64_M = 2048
+BPX32_M = 128
 
 
 def _choose_splits(M, K, nk, bpx=128, bco=128):
@@ -254,7 +253,6 @@ def _choose_splits(M, K, nk, bpx=128, bco=128):
     return max(1, min(nk // SPLIT_MIN_STEPS, -(-SPLIT_CU_MULT * NUM_CU // tiles), SPLIT_CAP))
 
 
-_CONV_LOG = os.environ.get("FMD_CONV_LOG", "0") == "1"   # debug: one line per conv launch on stderr
 HALO_CMAX = 512   # widest GN-prologue input of the halo kernel's affine table (csrc/conv_halo.hip CMAX)
 HALO_BK = 32      # input channels per halo chunk (FMD_HALO_BK)
 SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT_STATS_ROWS)
@@ -262,11 +260,11 @@ SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT
 
 # halo split-K on the small levels: ~HALO_SPLIT_WG workgroups, >= HALO_MIN_CHUNKS 32-channel chunks per split,
 # <= HALO_SPLIT_CAP splits (env overrides for A/B runs)
-HALO_SPLIT_WG = int(os.environ.get("FMD_HALO_SPLIT_WG", "256"))
-HALO_MIN_CHUNKS = int(os.environ.get("FMD_HALO_MIN_CHUNKS", "2"))
-HALO_SPLIT_CAP = int(os.environ.get("FMD_HALO_SPLIT_CAP", "16"))
+HALO_SPLIT_WG = tuning.get("HALO_SPLIT_WG")
+HALO_MIN_CHUNKS = tuning.get("HALO_MIN_CHUNKS")
+HALO_SPLIT_CAP = tuning.get("HALO_SPLIT_CAP")
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (FMD_HALO_MIN_WG, _lib load)
-HALO_MIN_WG = int(os.environ.get("FMD_HALO_MIN_WG", "32") or 32)
+HALO_MIN_WG = tuning.get("HALO_MIN_WG")
 
 
 def halo_splits(N, Ho, Wo, K, Cin, ztaps=1) -> int:
@@ -453,10 +451,6 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         slab = torch.empty((M // rows, K, 2), device=dev, dtype=F32)
         d.stats = _p(slab)
         st = Stats(slab, rows)
-    if _CONV_LOG:
-        print(f"[conv] N={N} in={Ds}x{Hs}x{Ws}x{C0}+{C1} out={Do}x{Ho}x{Wo}x{K} ks={ks} s={stride} tr={int(transposed)} "
-              f"up={int(upsample)} pro={int(pro is not None)} ep={int(ep is not None)} seg2={int(src2 is not None)} "
-              f"stats={int(fused_stats)} halo={int(halo)} splits={splits}", file=sys.stderr)
     if (gn is not None and CONV_GN and splits > 1 and not want_stats and d.stats is None and not out_f32
             and not accumulate and ep is None and conv_gn_eligible(K, gn["groups"], N)):
         a = torch.empty((N, K), device=dev, dtype=F32)
@@ -555,15 +549,15 @@ def head_wgrad(dpred, K, h, pro, dw, db):
 
 
 # generic weight-gradient split-K: >= WGRAD_MIN_STEPS 32-pixel steps per split, ~WGRAD_CU_MULT workgroups per CU
-WGRAD_MIN_STEPS = int(os.environ.get("FMD_WGRAD_MIN_STEPS", "8"))
-WGRAD_CU_MULT = int(os.environ.get("FMD_WGRAD_CU_MULT", "4"))
+WGRAD_MIN_STEPS = tuning.get("WGRAD_MIN_STEPS")
+WGRAD_CU_MULT = tuning.get("WGRAD_CU_MULT")
 # workgroups the halo weight gradient aims for (one per CU); fewer means fewer pixel splits, i.e. smaller
 # split-K slabs (their write + reduce read) at the small levels (FMD_WGRAD_HALO_WG: A/B override)
-WGRAD_HALO_WG = int(os.environ.get("FMD_WGRAD_HALO_WG", "0") or 0) or NUM_CU
+WGRAD_HALO_WG = tuning.get("WGRAD_HALO_WG") or NUM_CU
 # split-K slab caps (MB): the partial slabs' write + reduce read bound the small levels (A/B: FMD_WGRAD_SLAB_MB,
 # FMD_WGRAD_GEN_SLAB_MB)
-WGRAD_SLAB_MB = int(os.environ.get("FMD_WGRAD_SLAB_MB", "96") or 96)
-WGRAD_GEN_SLAB_MB = int(os.environ.get("FMD_WGRAD_GEN_SLAB_MB", "48") or 48)
+WGRAD_SLAB_MB = tuning.get("WGRAD_SLAB_MB")
+WGRAD_GEN_SLAB_MB = tuning.get("WGRAD_GEN_SLAB_MB")
 
 
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:

@@ -1,0 +1,57 @@
+"""Dispatch constants of the runtime (kernel-path choices and split heuristics), in one table.
+
+Every value is the measured default (DESIGN.md section 8 and the round logs cite the A/B runs behind each).  The
+only runtime override is ONE environment variable for A/B runs on the GPU box::
+
+    FMD_TUNE="HALO_MIN_WG=64,SPLIT_CAP=8" python bench.py
+
+Unknown names raise, so a typo cannot silently measure the default.  (``FMD_LIB`` -- which library file to load --
+is the other variable the package reads; tools/build_variant.sh builds instrumented libraries for it.)
+"""
+from __future__ import annotations
+
+import os
+
+# name: (default, meaning)
+TABLE = {
+    # ---- kernel-path switches (1 = on; 0 = the older path, kept for A/B and parity bisection)
+    "MAT3D": (1, "3-D: materialise the GN+SiLU operand of depth-tap halo convs once (0: fused prologue + G side "
+                 "output)"),
+    "DEPTH_HALO": (1, "3x3x3 stride-1 convs on the halo kernel with (depth tap, channel block) chunks"),
+    "S2D_HALO": (1, "stride-2 3x3 forwards / nearest-x2 data gradients on the space-to-depth halo kernel"),
+    "POINT_1X1": (1, "ResBlock 3x3 convs on 1x1 images as their centre tap"),
+    "GN_FUSED": (1, "small levels: GroupNorm statistics + affine + SiLU operand in one launch"),
+    "CONV_GN": (1, "split-K conv1 -> GroupNorm-2 in the split combine (fmd_conv_gn)"),
+    # ---- split heuristics
+    "CONV_GN_MIN_BLOCKS": (128, "fmd_conv_gn only from this many combine blocks up"),
+    "CONV_GN_CB": (4, "fmd_conv_gn combine block channels (4, 8, 16, 32, 64; at least one group)"),
+    "STATS_FOLD_MIN": (4096, "statistics slabs with at least this many rows per image are folded first"),
+    "SPLIT_MIN_STEPS": (2, "generic conv split-K: at least this many K-steps per split"),
+    "SPLIT_CU_MULT": (2, "generic conv split-K: target workgroups per CU"),
+    "SPLIT_CAP": (64, "generic conv split-K: most splits"),
+    "HALO_SPLIT_WG": (256, "halo conv split-K: target workgroups"),
+    "HALO_MIN_CHUNKS": (2, "halo conv split-K: at least this many 32-channel chunks per split"),
+    "HALO_SPLIT_CAP": (16, "halo conv split-K: most splits"),
+    "HALO_MIN_WG": (32, "halo conv only from this many workgroups (tiles x cout tiles x splits) up"),
+    "WGRAD_MIN_STEPS": (8, "generic weight gradient: at least this many 32-pixel steps per split"),
+    "WGRAD_CU_MULT": (4, "generic weight gradient: target workgroups per CU"),
+    "WGRAD_HALO_WG": (0, "halo weight gradient: target workgroups (0 = one per CU)"),
+    "WGRAD_SLAB_MB": (96, "halo weight gradient: split-K slab cap (MB)"),
+    "WGRAD_GEN_SLAB_MB": (48, "generic weight gradient: split-K slab cap (MB)"),
+}
+
+_over = {}
+for _item in filter(None, (s.strip() for s in os.environ.get("FMD_TUNE", "").split(","))):
+    _k, _, _v = _item.partition("=")
+    if _k not in TABLE or not _v:
+        raise ValueError(f"FMD_TUNE: unknown or empty setting {_item!r} (known: {', '.join(TABLE)})")
+    _over[_k] = int(_v)
+
+
+def get(name: str) -> int:
+    """The value of one constant: its FMD_TUNE override, else the table default."""
+    return _over.get(name, TABLE[name][0])
+
+
+def overridden(name: str) -> bool:
+    return name in _over

@@ -284,7 +284,7 @@ def test_wgrad(mode):
 
 @pytest.mark.parametrize("splits,generic", [(3, False), (20, False), (64, False), (37, True)])
 def test_wgrad_split_combine(splits, generic):
-    """The weight-gradient split-K combine (wgrad_reduce / wgrad_reduce2, FMD_WGRAD_REDUCE): wide splits (more than 16 slab lanes), accumulate into
+    """The weight-gradient split-K combine (wgrad_reduce2): wide splits (more than 16 slab lanes), accumulate into
     dW/db, vs torch; repeated runs are bit-identical (fixed summation order)."""
     O = ops()
     N, H, W, C, K = 4, 32, 32, 64, 128

@@ -271,3 +271,22 @@ def test_bench_pmc_traffic_matches_timed_kernel_only():
     assert wg is not None and wg["file"].endswith("r5_wgrad_traffic.json")
     assert bench.pmc_traffic("conv3x3_halo<false, 2, false>") is None   # round 3's kernel: not the timed one
     assert bench.pmc_traffic(["wgrad_halo_kernel<2>"]) is None          # a subset is not the timed pair
+
+
+def test_tuning_table_and_override(monkeypatch):
+    """runtime/tuning.py: every dispatch constant in one table, FMD_TUNE the only override; unknown names raise
+    (a typo must not silently measure the default)."""
+    import importlib
+    from fmdiff.runtime import tuning
+    try:
+        monkeypatch.setenv("FMD_TUNE", "HALO_MIN_WG=64, SPLIT_CAP=8")
+        t = importlib.reload(tuning)
+        assert t.get("HALO_MIN_WG") == 64 and t.get("SPLIT_CAP") == 8 and t.overridden("SPLIT_CAP")
+        assert t.get("HALO_SPLIT_WG") == t.TABLE["HALO_SPLIT_WG"][0] and not t.overridden("HALO_SPLIT_WG")
+        monkeypatch.setenv("FMD_TUNE", "HALO_MIN_WGS=64")
+        with pytest.raises(ValueError):
+            importlib.reload(tuning)
+    finally:
+        monkeypatch.delenv("FMD_TUNE", raising=False)
+        importlib.reload(tuning)
+    assert not tuning._over
