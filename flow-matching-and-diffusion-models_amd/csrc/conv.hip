@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows(const fmd_conv_desc d,
 }
 
 // Split-K combine + the GroupNorm forward of the result: a 1024-thread block owns (image n, CB channels) with
-// CB = max(FMD_CONV_GN_CB (default 4), Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
+// CB = max(CONV_GN_CB (default 4; fmd_conv_gn_set_block_channels), Cg) -- whole groups, so the group statistics close inside it.  Pass 1: lanes = (4-channel quad,
 // pixel lane) over the image's pixels (slab sums in four chains, fixed order), bias / per-sample bias / residual,
 // bf16 out, and the channel sums of the rounded values; lanes (shuffles), waves (LDS) and the group's channels
 // (fp64) in fixed order; pass 2 writes t = SiLU(a*out + b) from the lane's own output elements (the first pixel's
@@ -915,7 +915,7 @@ extern "C" int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd
   const int Cg = d->K / g->G;
   if (d->splits < 2 || d->K % 64 || 64 % Cg || d->stats || d->out_f32 || d->accumulate || d->ep_x0 || d->ep_a)
     return -12;
-  // channels per block: whole groups, at least FMD_CONV_GN_CB (default 4: one quad x 1024 pixel lanes when a group
+  // channels per block: whole groups, at least CONV_GN_CB (default 4: one quad x 1024 pixel lanes when a group
   // is 4 channels -- more blocks on the 128-channel levels; latent sampler 82.3 / 82.6 (16) -> 81.8 / 82.0 (8)
   // -> 81.3 / 81.5 ms (4), interleaved A/B)
   const int cb_min = conv_gn_cb();

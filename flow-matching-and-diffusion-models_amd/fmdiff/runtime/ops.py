@@ -150,7 +150,7 @@ def gn_fused_eligible(HW: int, C: int, C0: int, groups: int) -> bool:
     return GN_FUSED and Cg > 0 and Cg % 4 == 0 and C0 % 4 == 0 and 256 % (Cg // 4) == 0 and HW * Cg <= GN_FUSED_MAX
 
 
-# the GroupNorm forward of a split-K conv's output inside its combine (fmd_conv_gn); FMD_CONV_GN=0: the separate
+# the GroupNorm forward of a split-K conv's output inside its combine (fmd_conv_gn); CONV_GN=0 (runtime/tuning.py): the separate
 # fmd_gn_fused_apply launch (A/B runs)
 CONV_GN = bool(tuning.get("CONV_GN"))
 # fewest combine blocks (images x channel blocks) for which the fused form beats the two launches it replaces
@@ -239,7 +239,7 @@ def out_hw(Hs, ks, stride, pad, upsample):
 SPLIT_MIN_STEPS = tuning.get("SPLIT_MIN_STEPS")
 SPLIT_CU_MULT = tuning.get("SPLIT_CU_MULT")
 SPLIT_CAP = tuning.get("SPLIT_CAP")
-# outputs of at most BPX64_M pixels (K > 64, split-K) run on 64-pixel tiles (csrc/conv.hip small_m, FMD_BPX64_M)
+# outputs of at most BPX64_M pixels (K > 64, split-K) run on 64-pixel tiles (csrc/conv.hip small_m)
 # (train step 24.94 / 25.03 -> 24.83 / 24.87 ms, config D batch 8 77 -> 82.6 images/s); at most BPX32_M: 32-pixel
 # tiles (the latent UNet's 4x4 .. 1x1 levels: 82.3 -> 83.1 images/s)
 BPX64_M = 2048
@@ -263,7 +263,7 @@ SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT
 HALO_SPLIT_WG = tuning.get("HALO_SPLIT_WG")
 HALO_MIN_CHUNKS = tuning.get("HALO_MIN_CHUNKS")
 HALO_SPLIT_CAP = tuning.get("HALO_SPLIT_CAP")
-# fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (FMD_HALO_MIN_WG, _lib load)
+# fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (tuning HALO_MIN_WG, applied at _lib load)
 HALO_MIN_WG = tuning.get("HALO_MIN_WG")
 
 
@@ -552,10 +552,10 @@ def head_wgrad(dpred, K, h, pro, dw, db):
 WGRAD_MIN_STEPS = tuning.get("WGRAD_MIN_STEPS")
 WGRAD_CU_MULT = tuning.get("WGRAD_CU_MULT")
 # workgroups the halo weight gradient aims for (one per CU); fewer means fewer pixel splits, i.e. smaller
-# split-K slabs (their write + reduce read) at the small levels (FMD_WGRAD_HALO_WG: A/B override)
+# split-K slabs (their write + reduce read) at the small levels (tuning WGRAD_HALO_WG: A/B override)
 WGRAD_HALO_WG = tuning.get("WGRAD_HALO_WG") or NUM_CU
-# split-K slab caps (MB): the partial slabs' write + reduce read bound the small levels (A/B: FMD_WGRAD_SLAB_MB,
-# FMD_WGRAD_GEN_SLAB_MB)
+# split-K slab caps (MB): the partial slabs' write + reduce read bound the small levels (A/B: tuning WGRAD_SLAB_MB,
+# WGRAD_GEN_SLAB_MB)
 WGRAD_SLAB_MB = tuning.get("WGRAD_SLAB_MB")
 WGRAD_GEN_SLAB_MB = tuning.get("WGRAD_GEN_SLAB_MB")
 

@@ -127,7 +127,7 @@ typedef struct fmd_gn_out_desc {
   void* t;                  /* bf16 [N][Ho][Wo][K] */
 } fmd_gn_out_desc;
 /* fmd_conv with d->splits > 1 whose combine also produces the GroupNorm of the output (one workgroup per
- * (image, whole groups of max(FMD_CONV_GN_CB = 4, C/G) channels): the group statistics close inside it).  Requires K % 64 == 0, 64 % (K/G) == 0, no
+ * (image, whole groups of max(CB = 4 or fmd_conv_gn_set_block_channels, C/G) channels): the group statistics close inside it).  Requires K % 64 == 0, 64 % (K/G) == 0, no
  * d->stats / out_f32 / accumulate / ep_*.  Replaces fmd_conv + fmd_gn_fused_apply on the small levels
  * (src/nn/blocks/residual.py:71-76 conv1 -> out_layers GroupNorm + SiLU). */
 int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s);
@@ -135,10 +135,10 @@ int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s
 /* Input channels per halo-kernel chunk (csrc/conv_halo.hip). */
 #define FMD_SPLIT_STATS_ROWS 16   /* pixels per statistics row of a split-K conv */
 /* Fewest workgroups (16x16 tiles x cout tiles x split-K chunks) a 2-D problem needs to take the halo conv
- * (default 32; fewer go to the implicit GEMM).  Also settable with FMD_HALO_MIN_WG at load time; the host's
- * halo_splits mirror reads the same variable. */
+ * (default 32; fewer go to the implicit GEMM).  The Python side applies its tuning table's HALO_MIN_WG through it
+ * (fmdiff/runtime/tuning.py); the host's halo_splits mirror reads the same table entry. */
 int fmd_halo_set_min_workgroups(int32_t n);
-/* Fewest channels per combine block of fmd_conv_gn (4, 8, 16, 32 or 64; default 4, or FMD_CONV_GN_CB at first use):
+/* Fewest channels per combine block of fmd_conv_gn (4, 8, 16, 32 or 64; default 4):
  * a block owns max(cb, K / G) channels = whole groups.  Returns -1 for any other value.  A tuning hook; the host's
  * conv_gn_eligible mirror reads ops.CONV_GN_CB. */
 int fmd_conv_gn_set_block_channels(int32_t cb);
