@@ -789,9 +789,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < g_halo_min_wg) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
-  {   // the v9b kernel (csrc/conv_halo9.hip) takes every problem it supports (v11 first when its A/B hook is on)
-    const int rc11 = halo11_launch(A, pro, stream);
-    if (rc11 != 1) return rc11;
+  {   // the v9b kernel (csrc/conv_halo9.hip) takes every problem it supports
     const int rc9 = halo9_launch(A, pro, stream);
     if (rc9 != 1) return rc9;
   }

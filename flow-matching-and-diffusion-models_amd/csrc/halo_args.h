@@ -26,5 +26,3 @@ struct HArgs {
 // v9 kernel (csrc/conv_halo9.hip): launches the problem A describes if it qualifies; returns 1 (not applicable),
 // 0 (launched) or a hipError_t.  pro: 0 raw input, 1 GroupNorm affine, 2 affine + SiLU.
 int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream);
-// v11 experiment (csrc/conv_halo11.hip): same contract; launches only when enabled by fmd_debug_halo11(1).
-int halo11_launch(const HArgs& A, int pro, fmd_stream_t stream);

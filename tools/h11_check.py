@@ -1,7 +1,7 @@
 """v11 (ping-pong halo conv, csrc/conv_halo11.hip) against v9b on the GPU box: bit-equality of outputs and
 statistics, then interleaved HIP-event timings, on config B's 256^2 problems.
 
-usage: python tools/h11_check.py [--iters 30]
+usage: python tools/h11_check.py [--iters 30]   (needs the library built at commit 0a067f5, where v11 lives)
 """
 import argparse
 import ctypes
