@@ -162,39 +162,43 @@ __global__ void linear_dw_kernel(const float* __restrict__ x, int B, int I, int 
   }
 }
 
-// dx[b][i] += f'(x) * sum_o dy[b][o] w[o][i].  Grid (I/64, O/256): each wave sums 64 rows o
-// for 64 columns i and all b (<= 32), waves combine in LDS, blocks combine with fp32 atomics
-// (dx must be initialised by the caller).
+// dx[b][i] (+)= f'(x) * sum_o dy[b][o] w[o][i].  Grid (I/64, B): a block owns 64 columns of one batch row; its 4 waves
+// sum contiguous quarters of the O rows (dy row in LDS, w rows read coalesced, 8 in flight), then meet in LDS in
+// fixed order -- deterministic, no atomics, no memset.  (The first form, grid (I/64, O/256) with fp32 atomics across
+// the O blocks, ran the time MLP's 512 x 512 layer on 16 blocks: 75 us per train step.)
 __global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ x, int B, int I,
                                                         const float* __restrict__ w, int O, int in_silu,
                                                         const float* __restrict__ dy, int dys,
-                                                        float* __restrict__ dx) {
+                                                        float* __restrict__ dx, int acc) {
+  extern __shared__ float dyr[];   // [O] this block's dy row
+  __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;
-  const int o0 = blockIdx.y * 256 + wv * 64;
-  float acc[32];
-#pragma unroll
-  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
-  if (i < I) {
-    for (int o = o0; o < min(O, o0 + 64); ++o) {
-      const float wv_ = w[(size_t)o * I + i];
-#pragma unroll
-      for (int b = 0; b < 32; ++b)
-        if (b < B) acc[b] += dy[(size_t)b * dys + o] * wv_;
-    }
-  }
-  __shared__ float red[4][32][64];
-#pragma unroll
-  for (int b = 0; b < 32; ++b)
-    if (b < B) red[wv][b][lane] = acc[b];
+  const int i = blockIdx.x * 64 + lane, b = blockIdx.y;
+  for (int o = threadIdx.x; o < O; o += 256) dyr[o] = dy[(size_t)b * dys + o];
   __syncthreads();
-  for (int k = threadIdx.x; k < B * 64; k += 256) {
-    const int b = k >> 6, l = k & 63;
-    const int ii = blockIdx.x * 64 + l;
-    if (ii >= I) continue;
-    float s = red[0][b][l] + red[1][b][l] + red[2][b][l] + red[3][b][l];
-    if (in_silu) s *= silu_grad(x[(size_t)b * I + ii]);
-    atomicAdd(dx + (size_t)b * I + ii, s);
+  const int per = (O + 3) / 4, o0 = wv * per, o1 = min(O, o0 + per);
+  float a0 = 0.f, a1 = 0.f;
+  if (i < I) {
+    int o = o0;
+    for (; o + 8 <= o1; o += 8) {
+      float wv8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wv8[k] = w[(size_t)(o + k) * I + i];
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        a0 += dyr[o + k] * wv8[k];
+        a1 += dyr[o + k + 1] * wv8[k + 1];
+      }
+    }
+    for (; o < o1; ++o) a0 += dyr[o] * w[(size_t)o * I + i];
+  }
+  red[wv][lane] = a0 + a1;
+  __syncthreads();
+  if (wv == 0 && i < I) {
+    float sv = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (in_silu) sv *= silu_grad(x[(size_t)b * I + i]);
+    float* d = dx + (size_t)b * I + i;
+    *d = acc ? *d + sv : sv;
   }
 }
 
@@ -668,26 +672,40 @@ __global__ __launch_bounds__(256) void glinear_bwd_kernel(const float* __restric
   float dx[32][4];
 #pragma unroll
   for (int b = 0; b < 32; ++b) dx[b][0] = dx[b][1] = dx[b][2] = dx[b][3] = 0.f;
-  for (int rr = rg; rr < nr; rr += nrg) {
-    const int r = bi.y + rr;
-    const f32x4 w4 = *(const f32x4*)(g.w + (size_t)r * I + i4);
-    f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+  // rows in batches of RB: their weight and dW loads issued together (one memory latency per batch, not one per
+  // row -- the per-row dW read-modify-write serialised the first form at ~85 us per train step)
+  constexpr int RB = 8;
+  for (int r0 = rg; r0 < nr; r0 += RB * nrg) {
+    f32x4 w4[RB], dw4[RB];
 #pragma unroll
-    for (int b = 0; b < 32; ++b) {
-      if (b < B) {
-        const float dv = ds[rr * B + b];
-        const f32x4 x4 = *(const f32x4*)(xs + b * I + i4);
-        gw += dv * x4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dx[b][e] += dv * w4[e];
-      }
+    for (int j = 0; j < RB; ++j) {
+      const int rr = r0 + j * nrg;
+      const size_t o = (size_t)(bi.y + (rr < nr ? rr : 0)) * I + i4;
+      w4[j] = *(const f32x4*)(g.w + o);
+      dw4[j] = *(const f32x4*)(g.dw + o);
     }
-    f32x4* dwp = (f32x4*)(g.dw + (size_t)r * I + i4);
-    *dwp = *dwp + gw;
-    if (q == 0 && g.db) {
-      float sb = 0.f;
-      for (int b = 0; b < B; ++b) sb += ds[rr * B + b];
-      g.db[r] += sb;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int rr = r0 + j * nrg;
+      if (rr >= nr) break;
+      const int r = bi.y + rr;
+      f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        if (b < B) {
+          const float dv = ds[rr * B + b];
+          const f32x4 x4 = *(const f32x4*)(xs + b * I + i4);
+          gw += dv * x4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dx[b][e] += dv * w4[j][e];
+        }
+      }
+      *(f32x4*)(g.dw + (size_t)r * I + i4) = dw4[j] + gw;
+      if (q == 0 && g.db) {
+        float sb = 0.f;
+        for (int b = 0; b < B; ++b) sb += ds[rr * B + b];
+        g.db[r] += sb;
+      }
     }
   }
   float* pp = part + ((size_t)blockIdx.x * nrg + rg) * B * I;
@@ -696,20 +714,37 @@ __global__ __launch_bounds__(256) void glinear_bwd_kernel(const float* __restric
     if (b < B) *(f32x4*)(pp + (size_t)b * I + i4) = f32x4{dx[b][0], dx[b][1], dx[b][2], dx[b][3]};
 }
 
-// dx[b][i] (+)= silu'(x) * sum_p part[p][b][i]
-__global__ void glinear_dx_reduce(const float* __restrict__ part, int np, int B, int I, const float* __restrict__ x,
-                                  int in_silu, float* __restrict__ dx, int acc) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < B * I; e += gridDim.x * blockDim.x) {
-    float v0 = 0.f, v1 = 0.f;
-    int p = 0;
-    for (; p + 2 <= np; p += 2) { v0 += part[(size_t)p * B * I + e]; v1 += part[(size_t)(p + 1) * B * I + e]; }
-    if (p < np) v0 += part[(size_t)p * B * I + e];
-    float v = v0 + v1;
+// dx[b][i] (+)= silu'(x) * sum_p part[p][b][i].  A 1024-thread block owns 64 elements: 16 partial groups (threads
+// e + 64 g) each sum partials p = g, g + 16, ... in two chains, then the groups meet in LDS in fixed order
+// (deterministic).  The first form -- one thread per element walking all np (several hundred) partials -- ran on 16
+// blocks for 86 us per train step.
+constexpr int GLR_G = 16;
+__global__ __launch_bounds__(1024) void glinear_dx_reduce(const float* __restrict__ part, int np, int B, int I,
+                                                          const float* __restrict__ x, int in_silu,
+                                                          float* __restrict__ dx, int acc) {
+  __shared__ float red[GLR_G][64];
+  const int el = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  const size_t BI = (size_t)B * I;
+  float v0 = 0.f, v1 = 0.f;
+  if (e < B * I) {
+    int p = g;
+    for (; p + GLR_G < np; p += 2 * GLR_G) {
+      v0 += part[(size_t)p * BI + e];
+      v1 += part[(size_t)(p + GLR_G) * BI + e];
+    }
+    if (p < np) v0 += part[(size_t)p * BI + e];
+  }
+  red[g][el] = v0 + v1;
+  __syncthreads();
+  if (g == 0 && e < B * I) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < GLR_G; ++k) v += red[k][el];
     if (in_silu) v *= silu_grad(x[e]);
     dx[e] = acc ? dx[e] + v : v;
   }
 }
-
 
 // ------------------------------------------------------------------ batched weight layouts
 // One launch re-derives every bf16 kernel layout of the UNet from the fp32 masters after the
@@ -934,7 +969,7 @@ int fmd_grouped_linear_bwd(const float* x, int32_t B, int32_t I, const void* gro
                      I, (const GLGroup*)groups, (const int2*)blocks, in_silu, dy, dy_stride, ws);
   int rc = (int)hipGetLastError();
   if (rc || !dx) return rc;
-  hipLaunchKernelGGL(glinear_dx_reduce, dim3(grid_for((long long)B * I)), dim3(256), 0, (hipStream_t)s, ws,
+  hipLaunchKernelGGL(glinear_dx_reduce, dim3((B * I + 63) / 64), dim3(1024), 0, (hipStream_t)s, ws,
                      nblk * (1024 / I), B, I, x, in_silu, dx, dx_acc);
   return (int)hipGetLastError();
 }
@@ -949,13 +984,9 @@ int fmd_linear_bwd(const float* x, int32_t B, int32_t I, const float* w, int32_t
     if (rc) return rc;
   }
   if (dx) {
-    if (!dx_acc) {   // the kernel accumulates with atomics
-      int rc = (int)hipMemsetAsync(dx, 0, sizeof(float) * (size_t)B * I, (hipStream_t)s);
-      if (rc) return rc;
-    }
-    if (B > 32) return -1;
-    hipLaunchKernelGGL(linear_dx_kernel, dim3((I + 63) / 64, (O + 255) / 256), dim3(256), 0, (hipStream_t)s, x, B, I,
-                       w, O, in_silu, dy, dy_stride, dx);
+    if (B > 32 || (size_t)O * 4 > 48 * 1024) return -1;
+    hipLaunchKernelGGL(linear_dx_kernel, dim3((I + 63) / 64, B), dim3(256), (size_t)O * 4, (hipStream_t)s, x, B, I,
+                       w, O, in_silu, dy, dy_stride, dx, dx_acc);
     return (int)hipGetLastError();
   }
   return 0;

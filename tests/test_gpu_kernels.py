@@ -574,6 +574,19 @@ def test_time_embedding_and_linear():
         torch.testing.assert_close(dw.cpu(), wr.grad, rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(db.cpu(), br.grad, rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(dx.cpu(), x.grad, rtol=1e-4, atol=1e-4)
+        # dx accumulation, and the 512 x 512 layer of the time MLP (I = O = 512, 8 column blocks x 8 batch rows)
+        dx2 = dx.clone()
+        O.linear_bwd(x.detach().to(DEV), w.to(DEV), dy.to(DEV), dw, db, dx=dx2, dx_acc=True, in_silu=silu)
+        torch.testing.assert_close(dx2.cpu(), 2 * x.grad, rtol=1e-4, atol=1e-4)
+        x5 = torch.randn(8, 512)
+        w5 = torch.randn(512, 512) * 0.05
+        dy5 = torch.randn(8, 512)
+        dx5 = torch.empty(8, 512, device=DEV)
+        O.linear_bwd(x5.to(DEV), w5.to(DEV), dy5.to(DEV), None, None, dx=dx5, in_silu=silu)
+        ref5 = dy5 @ w5
+        if silu:
+            ref5 = ref5 * torch.sigmoid(x5) * (1 + x5 * (1 - torch.sigmoid(x5)))
+        torch.testing.assert_close(dx5.cpu(), ref5, rtol=1e-4, atol=1e-4)
 
 
 def test_adamw_matches_torch():
