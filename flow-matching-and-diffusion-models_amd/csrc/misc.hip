@@ -111,28 +111,30 @@ __global__ void temb_kernel(const float* __restrict__ t, int N, int dim, int fli
   }
 }
 
-// y[b][o] = sum_i f(x[b][i]) w[o][i] + bias[o]; one wave per output row, B <= 32
-__global__ void linear_kernel(const float* __restrict__ x, int B, int I, const float* __restrict__ w,
-                              const float* __restrict__ bias, int O, int in_silu, float* __restrict__ y, int ys) {
+// y[b][o] = sum_i f(x[b][i]) w[o][i] + bias[o]; one wave per output row, B <= BM.  Rows b >= B read row B - 1 (so
+// the unrolled loads carry no branch and issue together) and are never stored.  The first form guarded every x load
+// with b < B, which serialised them: ~20 us for the 512 x 128 time-MLP layer.
+template <int BM>
+__global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ x, int B, int I,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     int O, int in_silu, float* __restrict__ y, int ys) {
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (wid >= O) return;
-  float acc[32];
+  float acc[BM];
 #pragma unroll
-  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+  for (int b = 0; b < BM; ++b) acc[b] = 0.f;
+#pragma unroll 2
   for (int i = lane; i < I; i += 64) {
     const float wv = w[(size_t)wid * I + i];
+    float xv[BM];
 #pragma unroll
-    for (int b = 0; b < 32; ++b) {
-      if (b < B) {
-        float xv = x[(size_t)b * I + i];
-        if (in_silu) xv = siluf_(xv);
-        acc[b] += wv * xv;
-      }
-    }
+    for (int b = 0; b < BM; ++b) xv[b] = x[(size_t)min(b, B - 1) * I + i];
+#pragma unroll
+    for (int b = 0; b < BM; ++b) acc[b] += wv * (in_silu ? siluf_(xv[b]) : xv[b]);
   }
 #pragma unroll
-  for (int b = 0; b < 32; ++b) {
+  for (int b = 0; b < BM; ++b) {
     if (b < B) {
       const float s = wave_sum(acc[b]);
       if (lane == 0) y[(size_t)b * ys + wid] = s + (bias ? bias[wid] : 0.f);
@@ -605,38 +607,72 @@ __global__ void add_bf16_kernel(const bf16r* __restrict__ a, bf16r* __restrict__
 // the groups' output rows are concatenated ([B][sum O]); a block owns 64 rows of one group.
 struct GLGroup { const float* w; const float* b; float* dw; float* db; long long O; long long off; };
 
+// x [B][I] -> LDS (SiLU applied), 16-byte loads issued four at a time (the scalar one-load-per-iteration staging
+// loop was a chain of 16 L2 round trips per block)
+FMD_DEV void glinear_stage_x(const float* __restrict__ x, int n4, int in_silu, float* __restrict__ xs) {
+  for (int e0 = threadIdx.x; e0 < n4; e0 += 4 * 256) {
+    f32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = e0 + k * 256;
+      v[k] = ((const f32x4*)x)[e < n4 ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = e0 + k * 256;
+      if (e < n4) {
+        f32x4 o = v[k];
+        if (in_silu) o = f32x4{siluf_(o[0]), siluf_(o[1]), siluf_(o[2]), siluf_(o[3])};
+        ((f32x4*)xs)[e] = o;
+      }
+    }
+  }
+}
+
+// A block = 64 rows of one group; 4 lanes per row, lane p reads columns p*4 + 16k.  The weight loads run in batches
+// of WB (one memory latency per batch); the first batch is issued before the x staging.  Batch rows b >= B read x row
+// B - 1 and are never stored.
+template <int BM>
 __global__ __launch_bounds__(256) void glinear_fwd_kernel(const float* __restrict__ x, int B, int I,
                                                           const GLGroup* __restrict__ G, const int2* __restrict__ blk,
                                                           int in_silu, float* __restrict__ y, int ys) {
   extern __shared__ float xs[];   // [B][I] (SiLU applied)
-  for (int e = threadIdx.x; e < B * I; e += blockDim.x) {
-    const float v = x[e];
-    xs[e] = in_silu ? siluf_(v) : v;
-  }
-  __syncthreads();
+  constexpr int WB = 16;
   const int2 bi = blk[blockIdx.x];
   const GLGroup g = G[bi.x];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = bi.y + wid * 16 + (lane >> 2), p = lane & 3;
   const bool act = r < g.O;
-  float acc[32];
+  const float* wr = g.w + (size_t)(act ? r : bi.y) * I + p * 4;   // idle lanes re-read a valid row
+  f32x4 w4[WB];
+  auto load = [&](int c0) {   // columns c0 + 16 j (+ p*4); c0 + 16 j < I is wave-uniform
 #pragma unroll
-  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
-  if (act) {
-    const float* wr = g.w + (size_t)r * I;
-    for (int i = p * 4; i < I; i += 16) {
-      const f32x4 w4 = *(const f32x4*)(wr + i);
+    for (int j = 0; j < WB; ++j) w4[j] = *(const f32x4*)(wr + (c0 + 16 * j < I ? c0 + 16 * j : 0));
+  };
+  load(0);
+  glinear_stage_x(x, B * I / 4, in_silu, xs);
+  __syncthreads();
+  float acc[BM];
 #pragma unroll
-      for (int b = 0; b < 32; ++b) {
-        if (b < B) {
-          const f32x4 x4 = *(const f32x4*)(xs + b * I + i);
-          acc[b] += w4[0] * x4[0] + w4[1] * x4[1] + w4[2] * x4[2] + w4[3] * x4[3];
+  for (int b = 0; b < BM; ++b) acc[b] = 0.f;
+  for (int c0 = 0;;) {
+#pragma unroll
+    for (int j = 0; j < WB; ++j) {
+      const int c = c0 + 16 * j;
+      if (c < I) {
+#pragma unroll
+        for (int b = 0; b < BM; ++b) {
+          const f32x4 x4 = *(const f32x4*)(xs + min(b, B - 1) * I + c + p * 4);
+          acc[b] += w4[j][0] * x4[0] + w4[j][1] * x4[1] + w4[j][2] * x4[2] + w4[j][3] * x4[3];
         }
       }
     }
+    c0 += 16 * WB;
+    if (c0 >= I) break;
+    load(c0);
   }
 #pragma unroll
-  for (int b = 0; b < 32; ++b) {
+  for (int b = 0; b < BM; ++b) {
     if (b < B) {
       float v = acc[b];
       v += __shfl_xor(v, 1, 64);
@@ -647,36 +683,27 @@ __global__ __launch_bounds__(256) void glinear_fwd_kernel(const float* __restric
 }
 
 // dW[r][i] += sum_b dy[b][r] xin[b][i];  db[r] += sum_b dy[b][r];  dx partial[blk][rg][b][i] = sum_r dy[b][r] W[r][i]
+// A thread owns one column quad (q) of rows rg, rg + nrg, ...; rows run in batches of RB whose weight and dW loads
+// are issued together (the first batch before the staging).  dy rows are staged as [64][BM] with zeros for b >= B,
+// so the unrolled batch loop needs no guard; db is one read-modify-write per row by thread rr (the per-row serial
+// db update of the first form was most of its 85 us).
+template <int BM>
 __global__ __launch_bounds__(256) void glinear_bwd_kernel(const float* __restrict__ x, int B, int I,
                                                           const GLGroup* __restrict__ G, const int2* __restrict__ blk,
                                                           int in_silu, const float* __restrict__ dy, int dys,
                                                           float* __restrict__ part) {
-  extern __shared__ float sm[];   // xin [B][I] | dy rows [64][B]
+  extern __shared__ float sm[];   // xin [B][I] | dy rows [64][BM]
+  constexpr int RB = BM <= 8 ? 16 : 8;
   float* xs = sm;
   float* ds = sm + B * I;
   const int2 bi = blk[blockIdx.x];
   const GLGroup g = G[bi.x];
   const int nr = min(64, (int)g.O - bi.y);
-  for (int e = threadIdx.x; e < B * I; e += blockDim.x) {
-    const float v = x[e];
-    xs[e] = in_silu ? siluf_(v) : v;
-  }
-  for (int e = threadIdx.x; e < 64 * B; e += blockDim.x) {
-    const int rr = e / B, b = e - rr * B;
-    ds[e] = rr < nr ? dy[(size_t)b * dys + g.off + bi.y + rr] : 0.f;
-  }
-  __syncthreads();
   const int nq = I / 4, nrg = blockDim.x / nq;
   const int q = threadIdx.x % nq, rg = threadIdx.x / nq;
   const int i4 = q * 4;
-  float dx[32][4];
-#pragma unroll
-  for (int b = 0; b < 32; ++b) dx[b][0] = dx[b][1] = dx[b][2] = dx[b][3] = 0.f;
-  // rows in batches of RB: their weight and dW loads issued together (one memory latency per batch, not one per
-  // row -- the per-row dW read-modify-write serialised the first form at ~85 us per train step)
-  constexpr int RB = 8;
-  for (int r0 = rg; r0 < nr; r0 += RB * nrg) {
-    f32x4 w4[RB], dw4[RB];
+  f32x4 w4[RB], dw4[RB];
+  auto load = [&](int r0) {
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const int rr = r0 + j * nrg;
@@ -684,33 +711,45 @@ __global__ __launch_bounds__(256) void glinear_bwd_kernel(const float* __restric
       w4[j] = *(const f32x4*)(g.w + o);
       dw4[j] = *(const f32x4*)(g.dw + o);
     }
+  };
+  load(rg);
+  glinear_stage_x(x, B * I / 4, in_silu, xs);
+  for (int e = threadIdx.x; e < 64 * BM; e += blockDim.x) {
+    const int rr = e / BM, b = e - rr * BM;
+    ds[e] = (rr < nr && b < B) ? dy[(size_t)b * dys + g.off + bi.y + rr] : 0.f;
+  }
+  __syncthreads();
+  if (g.db && (int)threadIdx.x < nr) {
+    float sb = 0.f;
+    for (int b = 0; b < B; ++b) sb += ds[threadIdx.x * BM + b];
+    g.db[bi.y + threadIdx.x] += sb;
+  }
+  float dx[BM][4];
+#pragma unroll
+  for (int b = 0; b < BM; ++b) dx[b][0] = dx[b][1] = dx[b][2] = dx[b][3] = 0.f;
+  for (int r0 = rg;;) {
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const int rr = r0 + j * nrg;
       if (rr >= nr) break;
-      const int r = bi.y + rr;
       f32x4 gw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int b = 0; b < 32; ++b) {
-        if (b < B) {
-          const float dv = ds[rr * B + b];
-          const f32x4 x4 = *(const f32x4*)(xs + b * I + i4);
-          gw += dv * x4;
+      for (int b = 0; b < BM; ++b) {
+        const float dv = ds[rr * BM + b];
+        const f32x4 x4 = *(const f32x4*)(xs + min(b, B - 1) * I + i4);
+        gw += dv * x4;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) dx[b][e] += dv * w4[j][e];
-        }
+        for (int e = 0; e < 4; ++e) dx[b][e] += dv * w4[j][e];
       }
-      *(f32x4*)(g.dw + (size_t)r * I + i4) = dw4[j] + gw;
-      if (q == 0 && g.db) {
-        float sb = 0.f;
-        for (int b = 0; b < B; ++b) sb += ds[rr * B + b];
-        g.db[r] += sb;
-      }
+      *(f32x4*)(g.dw + (size_t)(bi.y + rr) * I + i4) = dw4[j] + gw;
     }
+    r0 += RB * nrg;
+    if (r0 >= nr) break;
+    load(r0);
   }
   float* pp = part + ((size_t)blockIdx.x * nrg + rg) * B * I;
 #pragma unroll
-  for (int b = 0; b < 32; ++b)
+  for (int b = 0; b < BM; ++b)
     if (b < B) *(f32x4*)(pp + (size_t)b * I + i4) = f32x4{dx[b][0], dx[b][1], dx[b][2], dx[b][3]};
 }
 
@@ -944,15 +983,20 @@ int fmd_timestep_embedding(const float* t, int32_t N, int32_t dim, int32_t flip,
 
 int fmd_linear(const float* x, int32_t B, int32_t I, const float* w, const float* b, int32_t O, int32_t in_silu,
                float* y, int32_t y_stride, fmd_stream_t s) {
-  if (B > 32) return -1;
-  LAUNCH(linear_kernel, (O + 3) / 4, x, B, I, w, b, O, in_silu, y, y_stride);
+  if (B < 1 || B > 32) return -1;
+  if (B <= 8) {
+    LAUNCH(linear_kernel<8>, (O + 3) / 4, x, B, I, w, b, O, in_silu, y, y_stride);
+  } else {
+    LAUNCH(linear_kernel<32>, (O + 3) / 4, x, B, I, w, b, O, in_silu, y, y_stride);
+  }
 }
 
 int fmd_grouped_linear(const float* x, int32_t B, int32_t I, const void* groups, const void* blocks, int32_t nblk,
                        int32_t in_silu, float* y, int32_t y_stride, fmd_stream_t s) {
   if (B < 1 || B > 32 || I % 16 || (size_t)B * I * 4 > 64 * 1024) return -1;
-  hipLaunchKernelGGL(glinear_fwd_kernel, dim3(nblk), dim3(256), (size_t)B * I * 4, (hipStream_t)s, x, B, I,
-                     (const GLGroup*)groups, (const int2*)blocks, in_silu, y, y_stride);
+  auto* kern = B <= 8 ? glinear_fwd_kernel<8> : glinear_fwd_kernel<32>;
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), (size_t)B * I * 4, (hipStream_t)s, x, B, I, (const GLGroup*)groups,
+                     (const int2*)blocks, in_silu, y, y_stride);
   return (int)hipGetLastError();
 }
 
@@ -964,9 +1008,12 @@ int fmd_grouped_linear_bwd(const float* x, int32_t B, int32_t I, const void* gro
                            int32_t nblk, int32_t in_silu, const float* dy, int32_t dy_stride, float* dx,
                            int32_t dx_acc, float* ws, fmd_stream_t s) {
   if (B < 1 || B > 32 || (I != 128 && I != 256 && I != 512 && I != 1024)) return -1;
-  if ((size_t)(B * I + 64 * B) * 4 > 64 * 1024) return -1;
-  hipLaunchKernelGGL(glinear_bwd_kernel, dim3(nblk), dim3(256), (size_t)(B * I + 64 * B) * 4, (hipStream_t)s, x, B,
-                     I, (const GLGroup*)groups, (const int2*)blocks, in_silu, dy, dy_stride, ws);
+  const int bm = B <= 8 ? 8 : 32;
+  const size_t lds = (size_t)(B * I + 64 * bm) * 4;
+  if (lds > 64 * 1024) return -1;
+  auto* kern = bm == 8 ? glinear_bwd_kernel<8> : glinear_bwd_kernel<32>;
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), lds, (hipStream_t)s, x, B, I, (const GLGroup*)groups,
+                     (const int2*)blocks, in_silu, dy, dy_stride, ws);
   int rc = (int)hipGetLastError();
   if (rc || !dx) return rc;
   hipLaunchKernelGGL(glinear_dx_reduce, dim3((B * I + 63) / 64), dim3(1024), 0, (hipStream_t)s, ws,

@@ -555,6 +555,13 @@ def test_time_embedding_and_linear():
         got = O.timestep_embedding(t.to(DEV), dim, flip, shift)
         torch.testing.assert_close(got.cpu(), timestep_embedding(t, dim, flip_sin_to_cos=flip, freq_shift=shift),
                                    rtol=2e-5, atol=2e-4)
+    for Bf, If in ((1, 128), (5, 200), (20, 512), (32, 64)):   # fmd_linear's 8- and 32-row instances, ragged I
+        xf = torch.randn(Bf, If)
+        wf = torch.randn(300, If) * 0.05
+        bf = torch.randn(300) * 0.1
+        for silu in (False, True):
+            got = O.linear(xf.to(DEV), wf.to(DEV), bf.to(DEV), in_silu=silu)
+            torch.testing.assert_close(got.cpu(), F.linear(F.silu(xf) if silu else xf, wf, bf), rtol=1e-4, atol=1e-4)
     x = torch.randn(8, 128, requires_grad=True)
     w = torch.randn(512, 128) * 0.05
     b = torch.randn(512) * 0.1
@@ -700,13 +707,14 @@ def test_halo_conv_bench_problem_vs_torch(case):
                                atol=2e-1)
 
 
+@pytest.mark.parametrize("B,I", [(8, 512), (3, 128), (20, 256), (1, 1024)])
 @pytest.mark.parametrize("in_silu", [False, True])
-def test_grouped_linear_vs_torch(in_silu):
-    """fmd_grouped_linear(_bwd): several emb projections (O = 256, 1024, 128) in one launch each way."""
+def test_grouped_linear_vs_torch(in_silu, B, I):
+    """fmd_grouped_linear(_bwd): several emb projections (O = 256, 1024, 100) in one launch each way; batches
+    below, at and above the 8-row kernel instance (B = 20 runs the 32-row one), a ragged last row block."""
     O = ops()
     torch.manual_seed(5)
-    B, I = 8, 512
-    lins = [torch.nn.Linear(I, n).to(DEV) for n in (256, 1024, 128)]
+    lins = [torch.nn.Linear(I, n).to(DEV) for n in (256, 1024, 100)]
     x = torch.randn(B, I, device=DEV)
     gl = O.GroupedLinear(lins, in_silu)
     y = gl.forward(x)

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/ -m gpu -x -q -k "linear or grouped or train or golden or unet" \
   --timeout 200 --timeout-method thread > gpurun_out/r5d_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r5d_tests.log; [ $rc -eq 0 ] || exit $rc
-bash tools/ab_libs_step.sh product oldmisc || exit $?
+bash tools/ab_libs_step.sh product ${AB_VARIANT:-oldmisc} || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_d -o run -- \
   python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler --no-config-e --no-config-d \
   > gpurun_out/prof_d/bench.json 2> gpurun_out/prof_d/bench.err
