@@ -92,6 +92,11 @@ FMD_DEV void fence8_(float (&y)[8]) {
 // block of 4 x cout "channels" (class-major, one class per 128-cout tile), meeting dy at offsets {0, +1} (taps
 // 1 | 2, 0 per dimension; 9 of the 16 tap-classes non-zero); the epilogue writes the class's pixels.
 // MODE: 0 plain 3x3, 1 S2D, 2 D2S.
+//
+// 3-D (A.depth > 0) stride-2 modes: depth is handled by chunks, in-plane as above.  S2D: images are the N*Do output
+// slices and chunk = (depth tap kz < ks, plane, block) stages full-resolution slice 2z + kz - 1 (zeros outside the
+// sample).  D2S: images are the N*Ds gradient slices, the output classes are 8 (depth parity, a, b; class-major) and
+// chunk = (depth offset dz, block) stages gradient slice z + dz; class (c, a, b) writes full-resolution slice 2z + c.
 template <bool UP, int PRO, int MODE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
@@ -134,7 +139,11 @@ void conv3x3_halo9b(const HArgs A) {
   // output pixel of tile-local pixel pi (y * 16 + x); D2S: the class's full-resolution pixel
   auto opix = [&](int pi) -> int {
     const int y = ty0 + (pi >> 4), x = tx0 + (pi & 15);
-    return D2S ? (n * d.Ho + 2 * y + (ocls >> 1)) * d.Wo + 2 * x + (ocls & 1) : (n * d.Ho + y) * d.Wo + x;
+    if (D2S) {
+      const int no = A.depth ? smp * d.Do + 2 * zz + (ocls >> 2) : n;
+      return (no * d.Ho + 2 * y + ((ocls >> 1) & 1)) * d.Wo + 2 * x + (ocls & 1);
+    }
+    return (n * d.Ho + y) * d.Wo + x;
   };
   const int hy0 = UP ? (ty0 >> 1) - 1 : ty0 - 1;
   const int hx0 = UP ? (tx0 >> 1) - 1 : tx0 - 1;
@@ -207,9 +216,22 @@ void conv3x3_halo9b(const HArgs A) {
       int sl = n;
       int poff = 0;
       if (S2D) {
-        const int pl = chunk / A.ncb;   // plane (a, b) = (pl >> 1, pl & 1)
-        cb = chunk - pl * A.ncb;
+        int ch = chunk;
+        if (A.depth) {   // 3-D: depth tap kz of a (kz, plane, block) chunk
+          const int kz = ch / (4 * A.ncb);
+          ch -= kz * 4 * A.ncb;
+          const int zl = 2 * zz + kz - 1;
+          zok = zl >= 0 && zl < A.dsrc;
+          sl = smp * A.dsrc + zl;
+        }
+        const int pl = ch / A.ncb;   // plane (a, b) = (pl >> 1, pl & 1)
+        cb = ch - pl * A.ncb;
         poff = (pl >> 1) * d.Ws + (pl & 1);
+      } else if (D2S && A.depth) {   // 3-D: depth offset dz of a (dz, block) chunk
+        const int dz = chunk / A.ncb;
+        cb = chunk - dz * A.ncb;
+        zok = zz + dz < A.dsrc;
+        sl = smp * A.dsrc + zz + dz;
       } else if (A.depth) {
         const int kz = chunk / A.ncb;
         cb = chunk - kz * A.ncb;
@@ -413,7 +435,7 @@ void conv3x3_halo9b(const HArgs A) {
     // S2D: this chunk's plane (a, b) reads halo rows / columns {0, +1} where a / b = 0; D2S: always {0, +1}
     int hadj = D2S ? HROW * 16 + 16 : 0;
     if (S2D) {
-      const int pl = chunk / A.ncb;
+      const int pl = (chunk % (4 * A.ncb)) / A.ncb;
       hadj = ((pl >> 1) ? 0 : HROW * 16) + ((pl & 1) ? 0 : 16);
     }
 #pragma unroll
@@ -596,7 +618,7 @@ void conv3x3_halo9b(const HArgs A) {
       *(u32x2*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16) + (c & 7) * 2) = o;
     }
     if (stats && (pb & 1)) {   // one statistics row per 64 pixels (= pixel blocks 2k, 2k+1: 4 tile rows)
-      const int srow = (D2S ? tile * 4 + ocls : tile) * 4 + (pb >> 1);
+      const int srow = (D2S ? tile * (A.depth ? 8 : 4) + ocls : tile) * 4 + (pb >> 1);
       const float a = st1 + __shfl_xor(st1, 32, 64);
       const float q = st2 + __shfl_xor(st2, 32, 64);
       if (hh == 0) {
@@ -657,12 +679,19 @@ FMD_DEV int s2d_tap(int a, int i) { return a ? 2 * i : 1 + 2 * i; }
 //            S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1}, S(3) = {0}
 //   mode 2 (data gradient of a stride-2 3x3, D2S): rows = 4C class-major, inner = K; class a meets dy offset u with
 //            tap ky = (a ? (u ? 0 : 2) : (u ? none : 1)), columns alike
-__global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode,
+// 3-D masters (d3, [K][C][3][3][3]): the chunks gain a leading depth index -- mode 0 the depth tap kz < 3, mode 1 the
+// folded depth tap kz < 4 (S(kz) as in-plane), mode 2 the depth offset dz < 2 with 8 classes (depth parity c = class
+// >> 2 meeting dz with tap kd = c ? (dz ? 0 : 2) : (dz ? none : 1))
+__host__ __device__ inline int s2d_depth_groups(int mode, int ks, int d3) { return !d3 ? 1 : mode == 0 ? ks : mode == 1 ? 4 : 2; }
+
+__global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int C, int ks, int mode, int d3,
                                         bf16r* __restrict__ out, long long total) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
-  const int R = mode == 0 ? K : mode == 1 ? C : 4 * C, Ci = mode == 0 ? C : K;
-  const int nch = (mode == 2 ? Ci : 4 * Ci) / BK;
+  const int R = mode == 0 ? K : mode == 1 ? C : (d3 ? 8 : 4) * C, Ci = mode == 0 ? C : K;
+  const int nch2 = (mode == 2 ? Ci : 4 * Ci) / BK;   // chunks per depth group
+  const int nch = s2d_depth_groups(mode, ks, d3) * nch2;
+  const int kt = d3 ? 3 : 1;                          // depth extent of the master
   long long t = e;
   const int j = (int)(t % 8); t /= 8;
   const int co = (int)(t % BCO); t /= BCO;
@@ -671,13 +700,15 @@ __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int 
   const int chunk = (int)(t % nch); t /= nch;
   const int tco = (int)t;
   const int row = tco * BCO + co;
-  const int ch = chunk * BK + kc * 8 + j;   // inner channel (modes 0, 1: plane-major over 4*Ci)
+  const int kz = chunk / nch2;
+  const int ch = (chunk - kz * nch2) * BK + kc * 8 + j;   // inner channel (modes 0, 1: plane-major over 4*Ci)
   float val = 0.f;
   if (mode == 2) {
     const int cls = row / C, c = row - cls * C;
-    const int a = cls >> 1, b = cls & 1, uu = tap >> 1, vv = tap & 1;
+    const int a = (cls >> 1) & 1, b = cls & 1, uu = tap >> 1, vv = tap & 1;
     const int ky = a ? (uu ? 0 : 2) : (uu ? -1 : 1), kx = b ? (vv ? 0 : 2) : (vv ? -1 : 1);
-    if (row < R && ky >= 0 && kx >= 0) val = w[(((size_t)ch * C + c) * 3 + ky) * 3 + kx];
+    const int kd = !d3 ? 0 : (cls >> 2) ? (kz ? 0 : 2) : (kz ? -1 : 1);
+    if (row < R && ky >= 0 && kx >= 0 && kd >= 0) val = w[((((size_t)ch * C + c) * kt + kd) * 3 + ky) * 3 + kx];
     out[e] = (bf16r)f2bf(val);
     return;
   }
@@ -685,12 +716,14 @@ __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int 
   const int u = s2d_tap(pl >> 1, tap >> 1), v = s2d_tap(pl & 1, tap & 1);
   if (row < R) {
     if (!mode) {
-      if (u < ks && v < ks) val = w[(((size_t)row * C + ci) * ks + u) * ks + v];
+      if (u < ks && v < ks) val = w[((((size_t)row * C + ci) * kt + kz) * ks + u) * ks + v];
     } else {
-      const int ylo = u == 0 ? 2 : u == 3 ? 0 : 2 - u, yhi = u == 0 ? 2 : u == 3 ? 0 : 3 - u;
-      const int xlo = v == 0 ? 2 : v == 3 ? 0 : 2 - v, xhi = v == 0 ? 2 : v == 3 ? 0 : 3 - v;
-      for (int ky = ylo; ky <= yhi; ++ky)
-        for (int kx = xlo; kx <= xhi; ++kx) val += w[(((size_t)ci * C + row) * 3 + ky) * 3 + kx];
+      auto lo = [](int q) { return q == 0 ? 2 : q == 3 ? 0 : 2 - q; };
+      auto hi = [](int q) { return q == 0 ? 2 : q == 3 ? 0 : 3 - q; };
+      const int dlo = d3 ? lo(kz) : 0, dhi = d3 ? hi(kz) : 0;
+      for (int kd = dlo; kd <= dhi; ++kd)
+        for (int ky = lo(u); ky <= hi(u); ++ky)
+          for (int kx = lo(v); kx <= hi(v); ++kx) val += w[((((size_t)ci * C + row) * kt + kd) * 3 + ky) * 3 + kx];
     }
   }
   out[e] = (bf16r)f2bf(val);
@@ -698,47 +731,63 @@ __global__ void s2d_tile_weights_kernel(const float* __restrict__ w, int K, int 
 
 }  // namespace
 
+extern "C" int64_t fmd_s2d_tiled_size_nd(int32_t K, int32_t C, int32_t mode, int32_t ks, int32_t dims) {
+  const int d3 = dims == 3;
+  const int64_t R = mode == 0 ? K : mode == 1 ? C : (d3 ? 8LL : 4LL) * C, Ci = mode == 0 ? C : K;
+  return ((R + BCO - 1) / BCO) * s2d_depth_groups(mode, ks, d3) * ((mode == 2 ? Ci : 4 * Ci) / BK) * 4 * KC * BCO * 8;
+}
+
 extern "C" int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode) {
-  const int64_t R = mode == 0 ? K : mode == 1 ? C : 4LL * C, Ci = mode == 0 ? C : K;
-  return ((R + BCO - 1) / BCO) * ((mode == 2 ? Ci : 4 * Ci) / BK) * 4 * KC * BCO * 8;
+  return fmd_s2d_tiled_size_nd(K, C, mode, 3, 2);
+}
+
+extern "C" int fmd_s2d_tile_weights_nd(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t dims,
+                                       void* out, fmd_stream_t stream) {
+  const int Ci = mode ? K : C;
+  if (dims != 2 && dims != 3) return -1;
+  if (mode < 0 || mode > 2 || (mode == 0 && ks != 3 && ks != 4) || (mode != 0 && ks != 3) || Ci % BK) return -1;
+  if (dims == 3 && ks != 3) return -1;
+  if (mode == 2 && C % BCO) return -1;   // one output class per 128-row tile
+  const long long total = fmd_s2d_tiled_size_nd(K, C, mode, ks, dims);
+  hipLaunchKernelGGL(s2d_tile_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, w, K, C, ks, mode, (int)(dims == 3), (bf16r*)out, total);
+  return (int)hipGetLastError();
 }
 
 extern "C" int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out,
                                     fmd_stream_t stream) {
-  const int Ci = mode ? K : C;
-  if (mode < 0 || mode > 2 || (mode == 0 && ks != 3 && ks != 4) || (mode != 0 && ks != 3) || Ci % BK) return -1;
-  if (mode == 2 && C % BCO) return -1;   // one output class per 128-row tile
-  const long long total = fmd_s2d_tiled_size(K, C, mode);
-  hipLaunchKernelGGL(s2d_tile_weights_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, w, K, C, ks, mode, (bf16r*)out, total);
-  return (int)hipGetLastError();
+  return fmd_s2d_tile_weights_nd(w, K, C, ks, mode, 2, out, stream);
 }
 
 extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->stride != 2 || d->pad != 1 || (d->ks != 3 && d->ks != 4) || d->transposed || d->upsample) return 1;
-  if (d->Do > 0 || d->Ds > 0 || d->src2 || d->gout || d->out_f32 || d->splits > 1) return 1;
+  const bool d3 = d->Do > 0 || d->Ds > 0;   // 3-D: the depth taps as chunks (kz, plane, block)
+  if (d3 && d->Ds != 2 * d->Do) return 1;
+  if (d->src2 || d->gout || d->out_f32 || d->splits > 1) return 1;
   if (d->Hs != 2 * d->Ho || d->Ws != 2 * d->Wo || d->Ho % TH || d->Wo % TW) return 1;
   const int C = d->C0 + d->C1;
   if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;
   if (d->pro_a && C > CMAX) return 1;
   if (d->accumulate && (d->resid || d->ep_x0)) return 1;
-  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
-      (long long)d->N * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
+  const long long Ns = (long long)d->N * (d3 ? d->Ds : 1), No = (long long)d->N * (d3 ? d->Do : 1);
+  if (Ns * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      No * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
   HArgs A;
   A.d = *d;
   if (d->accumulate) {   // out += conv: the old output enters as the residual side input of the same tile
     A.d.resid = d->out;
     A.d.accumulate = 0;
   }
+  A.d.N = (int)No;           // images: the output (depth) slices
   A.C = C;
   A.C23 = 0;
   A.tiles_x = d->Wo / TW;
   A.tiles_y = d->Ho / TH;
   A.ntc = d->K / BCO;
-  A.depth = 0;
-  A.dsrc = 0;
-  A.ncb = C / BK;            // chunks per plane
-  A.nchunk1 = 4 * A.ncb;     // plane-major
+  A.depth = d3 ? d->Do : 0;
+  A.dsrc = d3 ? d->Ds : 0;
+  A.ncb = C / BK;                              // chunks per plane
+  A.nchunk1 = (d3 ? d->ks : 1) * 4 * A.ncb;    // (depth tap,) plane-major
   A.nchunk2 = 0;
   A.nsteps_slots = A.nchunk1 * 4;
   A.splits = 1;
@@ -747,7 +796,7 @@ extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt2 = nullptr;
   A.tbuf = nullptr;
   A.dbg = 0;
-  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   const dim3 g(nwg), blk(NT9);
@@ -760,28 +809,32 @@ extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
 
 extern "C" int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (!d->transposed || d->stride != 2 || d->pad != 1 || d->ks != 3 || d->upsample) return 1;
-  if (d->Do > 0 || d->Ds > 0 || d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->pro_a) return 1;
+  const bool d3 = d->Do > 0 || d->Ds > 0;   // 3-D: 8 output classes, chunks (depth offset, block)
+  if (d3 && d->Do != 2 * d->Ds) return 1;
+  if (d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->pro_a) return 1;
   if (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws || d->Hs % TH || d->Ws % TW) return 1;
   const int C = d->C0 + d->C1;
   if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;
   if (d->accumulate && (d->resid || d->ep_x0)) return 1;
-  if ((long long)d->N * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
-      (long long)d->N * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
+  const long long Ns = (long long)d->N * (d3 ? d->Ds : 1), No = (long long)d->N * (d3 ? d->Do : 1);
+  if (Ns * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
+      No * d->Ho * d->Wo * d->K >= (1LL << 31)) return 1;
   HArgs A;
   A.d = *d;
   if (d->accumulate) {
     A.d.resid = d->out;
     A.d.accumulate = 0;
   }
+  A.d.N = (int)Ns;           // images: the gradient's (depth) slices
   A.C = C;
   A.C23 = 0;
-  A.tiles_x = d->Ws / TW;    // tiles over the low-resolution input grid; 4 output classes per tile
+  A.tiles_x = d->Ws / TW;    // tiles over the low-resolution input grid; 4 (3-D: 8) output classes per tile
   A.tiles_y = d->Hs / TH;
-  A.ntc = 4 * (d->K / BCO);
-  A.depth = 0;
-  A.dsrc = 0;
+  A.ntc = (d3 ? 8 : 4) * (d->K / BCO);
+  A.depth = d3 ? d->Ds : 0;
+  A.dsrc = d3 ? d->Ds : 0;
   A.ncb = C / BK;
-  A.nchunk1 = A.ncb;
+  A.nchunk1 = (d3 ? 2 : 1) * A.ncb;
   A.nchunk2 = 0;
   A.nsteps_slots = A.nchunk1 * 4;
   A.splits = 1;
@@ -790,7 +843,7 @@ extern "C" int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.wt2 = nullptr;
   A.tbuf = nullptr;
   A.dbg = 0;
-  const int nwg = d->N * A.tiles_x * A.tiles_y * A.ntc;
+  const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;
   hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 2>), dim3(nwg), dim3(NT9), 0, (hipStream_t)stream, A);
   return (int)hipGetLastError();

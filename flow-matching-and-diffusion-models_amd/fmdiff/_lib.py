@@ -96,6 +96,8 @@ SIGNATURES = {
     "fmd_conv_d2s": [C.POINTER(ConvDesc), p],
     "fmd_s2d_tiled_size": [i32, i32, i32],
     "fmd_s2d_tile_weights": [p, i32, i32, i32, i32, p, p],
+    "fmd_s2d_tiled_size_nd": [i32, i32, i32, i32, i32],
+    "fmd_s2d_tile_weights_nd": [p, i32, i32, i32, i32, i32, p, p],
     "fmd_channel_stats": [p, p, p, i32, i32, i32, i32, i32, p, p],
     "fmd_stats_fold": [p, i64, i32, i32, p, p],
     "fmd_gn_prep": [p, i32, p, i32, i32, i32, i32, i32, i32, f32, p, p, p, i32, i32, p, p, p, p],
@@ -156,7 +158,7 @@ SIGNATURES = {
     "fmd_head_wgrad_workspace": [i32, i32, i32, i32, i32, i32],
     "fmd_head_wgrad": [p, i32, p, p, p, i32, i32, i32, i32, i32, p, p, p, p],
 }
-_RESTYPE = {"fmd_linear_attention_workspace": i64, "fmd_linear_attention_state": i64, "fmd_wgrad_workspace": i64, "fmd_head_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_s2d_tiled_size": i64, "fmd_grouped_linear_bwd_workspace": i64}
+_RESTYPE = {"fmd_linear_attention_workspace": i64, "fmd_linear_attention_state": i64, "fmd_wgrad_workspace": i64, "fmd_head_wgrad_workspace": i64, "fmd_halo_tiled_size": i64, "fmd_s2d_tiled_size": i64, "fmd_s2d_tiled_size_nd": i64, "fmd_grouped_linear_bwd_workspace": i64}
 
 _lib = None
 

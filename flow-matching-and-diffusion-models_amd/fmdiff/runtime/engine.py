@@ -49,6 +49,7 @@ DEPTH_HALO = bool(tuning.get("DEPTH_HALO"))
 # stride-2 3x3 forwards and nearest-x2 data gradients on the space-to-depth halo kernel (fmd_conv_s2d); 0: the
 # implicit GEMM (A/B runs, runtime/tuning.py)
 S2D_HALO = bool(tuning.get("S2D_HALO"))
+S2D_3D = S2D_HALO and bool(tuning.get("S2D_3D"))
 # ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); POINT_1X1=0 for A/B runs
 POINT_1X1 = bool(tuning.get("POINT_1X1"))
 # training, 3-D fused-prologue halo convs (MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
@@ -276,7 +277,7 @@ class WeightCache:
         return self._c[key]["buf"]
 
     def s2d(self, w: torch.Tensor, mode: int):
-        """Stride-2 halo tiles of a 2-D 3x3 weight (fmd_s2d_tile_weights): mode 0 the stride-2 forward, 1 the data
+        """Stride-2 halo tiles of a 3x3 (3x3x3) weight (fmd_s2d_tile_weights_nd): mode 0 the stride-2 forward, 1 the data
         gradient of the conv on a nearest-x2 input, 2 the stride-2 data gradient; re-derived by one launch per
         optimizer step."""
         key = (id(w), "s2d", mode)
@@ -389,9 +390,11 @@ class UNetEngine:
             halo = DEPTH_HALO and stride == 1 and ops.halo_eligible(
                 N_ * Do_, sp[1], ops.out_hw(sp[1], 3, 1, 1, upsample), ops.out_hw(sp[2], 3, 1, 1, upsample),
                 conv.out_channels, upsample=upsample, Cin=Cin, ztaps=3)
-        s2d = (S2D_HALO and stride == 2 and len(sp) == 2 and conv.weight.shape[1] == Cin and
-               ops.s2d_eligible(N_, sp[0], sp[1], sp[0] // 2, sp[1] // 2, conv.out_channels, Cin, 3))
-        if s2d:   # DownsampleND's conv on the space-to-depth halo kernel
+        s2d = S2D_HALO and stride == 2 and conv.weight.shape[1] == Cin and (
+            ops.s2d_eligible(N_, sp[0], sp[1], sp[0] // 2, sp[1] // 2, conv.out_channels, Cin, 3) if len(sp) == 2
+            else S2D_3D and ops.s2d_eligible(N_, sp[1], sp[2], sp[1] // 2, sp[2] // 2, conv.out_channels, Cin, 3,
+                                             sp[0], sp[0] // 2))
+        if s2d:   # DownsampleND's conv on the space-to-depth halo kernel (3-D: depth taps as chunks)
             out, st = ops.conv(x.t, conv.out_channels, None, ks=3, stride=2, pad=1, bias=conv.bias, want_stats="free",
                                s2d_tiled=self.wc.s2d(conv.weight, 0))
         else:
@@ -418,6 +421,12 @@ class UNetEngine:
                         dy.shape[-1] == conv.weight.shape[0] and ops.s2d_eligible(
                         N_, 2 * sp[0], 2 * sp[1], sp[0], sp[1], Cin, dy.shape[-1], 4):
                     # nearest-x2 folded into a 4x4 stride-2 gather, on the space-to-depth halo kernel
+                    ops.conv(dy, Cin, None, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc),
+                             s2d_tiled=self.wc.s2d(conv.weight, 1))
+                elif upsample and len(sp) == 3 and S2D_3D and conv.weight.shape[1] == Cin and \
+                        dy.shape[-1] == conv.weight.shape[0] and ops.s2d_eligible(
+                        N_, 2 * sp[1], 2 * sp[2], sp[1], sp[2], Cin, dy.shape[-1], 4, 2 * sp[0], sp[0]):
+                    # 3-D: the nearest-x2 copy folded into a 4x4x4 stride-2 gather (the depth taps as chunks)
                     ops.conv(dy, Cin, None, ks=4, stride=2, pad=1, out_hw_=sp, out=g, accumulate=bool(acc),
                              s2d_tiled=self.wc.s2d(conv.weight, 1))
                 elif upsample and len(sp) == 2:
@@ -535,10 +544,12 @@ class UNetEngine:
             halo = self._halo_ok(dy.shape[0], sp, Cin, dy.shape[-1])
             base, tiled = self._wts(w, 3, halo, Kpad, None)
             return ops.conv(dy, Cin, base, ks=3, stride=1, pad=1, out_hw_=sp, wgt_tiled=tiled, **kw)
-        if (S2D_HALO and len(sp) == 2 and Kpad is None and w.dim() == 4 and w.shape[1] == Cin and
-                not kw.get("pro") and ops.d2s_eligible(dy.shape[0], dy.shape[1], dy.shape[2], sp[0], sp[1], Cin,
-                                                       dy.shape[-1])):
-            # transposed stride-2 gather onto the depth-to-space view, on the halo kernel
+        if S2D_HALO and Kpad is None and w.shape[1] == Cin and not kw.get("pro") and (
+                ops.d2s_eligible(dy.shape[0], dy.shape[1], dy.shape[2], sp[0], sp[1], Cin, dy.shape[-1])
+                if len(sp) == 2 and w.dim() == 4 else
+                S2D_3D and len(sp) == 3 and w.dim() == 5 and ops.d2s_eligible(dy.shape[0], dy.shape[2], dy.shape[3], sp[1], sp[2],
+                                                                    Cin, dy.shape[-1], dy.shape[1], sp[0])):
+            # transposed stride-2 gather onto the depth-to-space view, on the halo kernel (3-D: 8 classes)
             return ops.conv(dy, Cin, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=sp,
                             s2d_tiled=self.wc.s2d(w, 2), **kw)
         return ops.conv(dy, Cin, self.wc.get(w, 1, Kpad, None), ks=3, stride=stride, pad=1, transposed=True,

@@ -298,30 +298,41 @@ def halo_eligible(N, Hs, Ho, Wo, K, ks=3, stride=1, pad=1, upsample=False, trans
             and halo_splits(N, Ho, Wo, K, Cin, ztaps) > 0)
 
 
-def s2d_eligible(N, Hs, Ws, Ho, Wo, K, C, ks) -> bool:
-    """Mirror of fmd_conv_s2d's applicability test (csrc/conv_halo9.hip): a 2-D stride-2 pad-1 3x3 / 4x4 forward
-    gather onto 16x16 output tiles, C % 32 == 0, K % 128 == 0, >= 128 workgroups."""
+def s2d_eligible(N, Hs, Ws, Ho, Wo, K, C, ks, Ds=0, Do=0) -> bool:
+    """Mirror of fmd_conv_s2d's applicability test (csrc/conv_halo9.hip): a stride-2 pad-1 3x3 / 4x4 forward
+    gather onto 16x16 output tiles, C % 32 == 0, K % 128 == 0, >= 128 workgroups.  3-D: ``Ds`` = 2 ``Do`` input /
+    output depths (stride 2 in depth too; the depth taps run as chunks)."""
+    d3 = Ds > 0 or Do > 0
+    if d3 and Ds != 2 * Do:
+        return False
+    Ni, No = N * (Ds if d3 else 1), N * (Do if d3 else 1)
     return (ks in (3, 4) and Hs == 2 * Ho and Ws == 2 * Wo and Ho % 16 == 0 and Wo % 16 == 0 and C % 32 == 0
-            and K % 128 == 0 and N * (Ho // 16) * (Wo // 16) * (K // 128) >= 128
-            and N * Hs * Ws * C < (1 << 31) and N * Ho * Wo * K < (1 << 31))
+            and K % 128 == 0 and No * (Ho // 16) * (Wo // 16) * (K // 128) >= 128
+            and Ni * Hs * Ws * C < (1 << 31) and No * Ho * Wo * K < (1 << 31))
 
 
-def d2s_eligible(N, Hs, Ws, Ho, Wo, K, C) -> bool:
-    """Mirror of fmd_conv_d2s's applicability test: the transposed gather of a 2-D stride-2 pad-1 3x3 conv from an
-    Hs x Ws gradient (multiples of 16) onto Ho = 2 Hs, Wo = 2 Ws, C % 32 == 0, K % 128 == 0, >= 128 workgroups."""
+def d2s_eligible(N, Hs, Ws, Ho, Wo, K, C, Ds=0, Do=0) -> bool:
+    """Mirror of fmd_conv_d2s's applicability test: the transposed gather of a stride-2 pad-1 3x3 conv from an
+    Hs x Ws gradient (multiples of 16) onto Ho = 2 Hs, Wo = 2 Ws, C % 32 == 0, K % 128 == 0, >= 128 workgroups.
+    3-D: ``Do`` = 2 ``Ds`` (8 output classes per tile)."""
+    d3 = Ds > 0 or Do > 0
+    if d3 and Do != 2 * Ds:
+        return False
+    Ni, No = N * (Ds if d3 else 1), N * (Do if d3 else 1)
     return (Ho == 2 * Hs and Wo == 2 * Ws and Hs % 16 == 0 and Ws % 16 == 0 and C % 32 == 0 and K % 128 == 0
-            and N * (Hs // 16) * (Ws // 16) * 4 * (K // 128) >= 128
-            and N * Hs * Ws * C < (1 << 31) and N * Ho * Wo * K < (1 << 31))
+            and Ni * (Hs // 16) * (Ws // 16) * (8 if d3 else 4) * (K // 128) >= 128
+            and Ni * Hs * Ws * C < (1 << 31) and No * Ho * Wo * K < (1 << 31))
 
 
 def s2d_tile_weights(w: torch.Tensor, mode: int, out=None) -> torch.Tensor:
-    """fp32 [K][C][ks][ks] -> fmd_conv_s2d / fmd_conv_d2s tiles (mode 0 stride-2 forward, 1 data gradient of a 3x3
-    conv on a nearest-x2 input, 2 stride-2 3x3 data gradient)."""
+    """fp32 [K][C][ks][ks] (3-D: [K][C][3][3][3]) -> fmd_conv_s2d / fmd_conv_d2s tiles (mode 0 stride-2 forward,
+    1 data gradient of a 3x3 conv on a nearest-x2 input, 2 stride-2 3x3 data gradient)."""
     K, Cc, ks = w.shape[0], w.shape[1], w.shape[2]
-    n = int(_lib.lib().fmd_s2d_tiled_size(K, Cc, mode))
+    dims = w.dim() - 2
+    n = int(_lib.lib().fmd_s2d_tiled_size_nd(K, Cc, mode, ks, dims))
     if out is None:
         out = torch.empty((n,), device=w.device, dtype=BF16)
-    _lib.call("fmd_s2d_tile_weights", _p(w.contiguous()), K, Cc, ks, mode, _p(out), stream())
+    _lib.call("fmd_s2d_tile_weights_nd", _p(w.contiguous()), K, Cc, ks, mode, dims, _p(out), stream())
     return out
 
 
@@ -405,13 +416,13 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
                                                    C0 + C1, pro is not None)
     d.force_generic = int(force_generic)
     if s2d_tiled is not None:   # stride-2 on the halo kernel: one launch, statistics in its epilogue
-        ok = (s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks) if not transposed else
-              (ks == 3 and pro is None and d2s_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1)))
-        if not ok or d3 or stride != 2 or pad != 1 or upsample or src2 is not None or out_f32 or gout is not None:
+        ok = (s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks, Ds, Do) if not transposed else
+              (ks == 3 and pro is None and d2s_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, Ds, Do)))
+        if not ok or stride != 2 or pad != 1 or upsample or src2 is not None or out_f32 or gout is not None:
             raise ValueError("conv: s2d_tiled given for a problem fmd_conv_s2d / fmd_conv_d2s does not take")
         d.wgt_tiled, d.splits = _p(s2d_tiled), 1
         st = None
-        if want_stats and (Ho * Wo) % 64 == 0:
+        if want_stats and (max(Do, 1) * Ho * Wo) % 64 == 0:
             slab = torch.empty((M // 64, K, 2), device=dev, dtype=F32)
             d.stats = _p(slab)
             st = Stats(slab, 64)

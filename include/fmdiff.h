@@ -151,14 +151,18 @@ int fmd_tile_weights_halo(const void* w, int32_t K, int32_t T, int32_t C, void* 
  * tensor) on the halo kernel (csrc/conv_halo9.hip).  Replaces the implicit GEMM of DownsampleND's conv
  * (src/nn/ops/upsampling.py:49-56) and the data gradient of UpsampleND's conv (upsampling.py:27-29).  Needs
  * d->wgt_tiled from fmd_s2d_tile_weights, Hs = 2 Ho, Ws = 2 Wo, Ho and Wo multiples of 16, (C0 + C1) % 32 == 0,
- * K % 128 == 0, >= 128 output tiles; d->accumulate adds into d->out.  Returns 1 when the problem does not qualify. */
+ * K % 128 == 0, >= 128 output tiles; d->accumulate adds into d->out.  3-D (d->Ds = 2 d->Do, stride 2 in depth too;
+ * weights from fmd_s2d_tile_weights_nd with dims 3): the depth taps run as chunks over full-resolution slices
+ * 2z + kz - 1 (Conv3d of DownsampleND; the 4x4x4 data gradient of UpsampleND's Conv3d).  Returns 1 when the problem
+ * does not qualify. */
 int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t s);
 /* The data gradient of a stride-2 pad-1 3x3 conv (the transposed gather of DownsampleND's conv,
  * src/nn/ops/upsampling.py:49-56) as a stride-1 2x2 conv from the low-resolution gradient onto the depth-to-space
  * view of the output (4 pixel classes x K channels, one class per 128-channel tile) on the halo kernel.  d as for
  * fmd_conv with transposed = 1: Ho = 2 Hs, Wo = 2 Ws, Hs and Ws multiples of 16, (C0 + C1) % 32 == 0, K % 128 == 0,
- * no prologue; d->wgt_tiled from fmd_s2d_tile_weights mode 2; d->accumulate adds into d->out.  Returns 1 when the
- * problem does not qualify. */
+ * no prologue; d->wgt_tiled from fmd_s2d_tile_weights mode 2; d->accumulate adds into d->out.  3-D (d->Do = 2 d->Ds,
+ * weights from fmd_s2d_tile_weights_nd with dims 3): 8 output classes (depth parity, a, b), the gradient slices z and
+ * z + 1 as chunks.  Returns 1 when the problem does not qualify. */
 int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t s);
 /* fp32 reference-layout conv weight [K][C][ks][ks] -> the halo tiles of fmd_conv_s2d / fmd_conv_d2s.  mode 0: the
  * stride-2 forward (rows K, ks 3 or 4); mode 1: the 4x4 data gradient of a 3x3 conv on a nearest-x2 input
@@ -166,6 +170,12 @@ int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t s);
  * inner K).  The inner channel count must be a multiple of 32. */
 int64_t fmd_s2d_tiled_size(int32_t K, int32_t C, int32_t mode);
 int fmd_s2d_tile_weights(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, void* out, fmd_stream_t s);
+/* The same for 2-D (dims 2, as above) or 3-D (dims 3) masters: [K][C][3][3][3] fp32 -> the 3-D tiles of
+ * fmd_conv_s2d / fmd_conv_d2s (mode 0: 3 depth taps x the 2-D chunks; mode 1: the 4 folded depth taps; mode 2: rows
+ * 8C class-major, 2 depth offsets). */
+int64_t fmd_s2d_tiled_size_nd(int32_t K, int32_t C, int32_t mode, int32_t ks, int32_t dims);
+int fmd_s2d_tile_weights_nd(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t dims, void* out,
+                            fmd_stream_t s);
 
 /* UNet output head: out = conv3x3(SiLU(a*h + b)) to K <= 8 channels, fp32 NHWC [N][H][W][8]
  * (channels >= K zero), replacing the final GroupNorm -> SiLU -> ConvND of

@@ -1448,3 +1448,68 @@ def test_d2s_halo_dgrad_vs_torch(case):
     got, _ = O.conv(dy.to(DEV), C, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=(H, W), out=out,
                     accumulate=case == "acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 2))
     _close(got, ref)
+
+
+@pytest.mark.parametrize("case", ["down", "down_pro_stats", "updgrad", "updgrad_acc", "d2s", "d2s_acc"])
+def test_s2d_d2s_halo_3d_vs_torch(case):
+    """3-D stride-2 convs on the halo kernel (csrc/conv_halo9.hip, depth taps as chunks) vs torch autograd of
+    F.conv3d on the bf16-rounded operands: down = DownsampleND's Conv3d(stride 2) forward (fmd_conv_s2d; the
+    _pro_stats case with a GroupNorm-affine + SiLU prologue and fused statistics); updgrad = the data gradient of
+    Conv3d(nearest_x2(x)) as the 4x4x4 stride-2 gather; d2s = the data gradient of the stride-2 Conv3d onto 8
+    output classes (fmd_conv_d2s).  The _acc cases add into an existing gradient.  Depth sizes cover both the
+    zero-padded first slice and the last."""
+    O = ops()
+    g = torch.Generator().manual_seed(90)
+    if case.startswith("down"):
+        N, D, H, W, C, K = 2, 8, 128, 128, 64, 128
+        assert O.s2d_eligible(N, H, W, H // 2, W // 2, K, C, 3, D, D // 2)
+        x = _rand_ndhwc(N, D, H, W, C, 91)
+        w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)
+        b = torch.randn(K, generator=g) * 0.1
+        xin, pro = _to_ncdhw(x), None
+        if case == "down_pro_stats":
+            pa, pb = torch.rand(N, C, generator=g) + 0.5, torch.randn(N, C, generator=g) * 0.2
+            pro = (pa.to(DEV), pb.to(DEV), True)
+            xin = F.silu(pa[:, :, None, None, None] * xin + pb[:, :, None, None, None]).to(torch.bfloat16).float()
+        got, st = O.conv(x.to(DEV), K, None, ks=3, stride=2, pad=1, bias=b.to(DEV), pro=pro,
+                         want_stats=case == "down_pro_stats", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 0))
+        ref = F.conv3d(xin, _bfw(w), b, stride=2, padding=1).permute(0, 2, 3, 4, 1)
+        _close(got, ref)
+        if st is not None:
+            gf = got.float().cpu()
+            sums = st.slab.view(N, -1, K, 2).sum(1).cpu()
+            torch.testing.assert_close(sums[..., 0], gf.sum((1, 2, 3)), rtol=5e-3, atol=5e-2)
+            torch.testing.assert_close(sums[..., 1], (gf * gf).sum((1, 2, 3)), rtol=5e-3, atol=5e-2)
+        return
+    if case.startswith("updgrad"):
+        N, D, H, W, Cin, K = 2, 4, 64, 64, 128, 64       # low-resolution x; dy at 2D x 2H x 2W
+        w = torch.randn(K, Cin, 3, 3, 3, generator=g) / math.sqrt(Cin * 27)
+        dy = _rand_ndhwc(N, 2 * D, 2 * H, 2 * W, K, 92)
+        xl = torch.zeros(N, Cin, D, H, W, requires_grad=True)
+        F.conv3d(F.interpolate(xl, scale_factor=2, mode="nearest"), _bfw(w), padding=1).backward(_to_ncdhw(dy))
+        ref = xl.grad.permute(0, 2, 3, 4, 1)
+        out = None
+        if case == "updgrad_acc":
+            prev = _rand_ndhwc(N, D, H, W, Cin, 93)
+            out = prev.to(DEV).clone()
+            ref = ref + prev.float()
+        assert O.s2d_eligible(N, 2 * H, 2 * W, H, W, Cin, K, 4, 2 * D, D)
+        got, _ = O.conv(dy.to(DEV), Cin, None, ks=4, stride=2, pad=1, out_hw_=(D, H, W), out=out,
+                        accumulate=case == "updgrad_acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 1))
+        _close(got, ref)
+        return
+    N, D, H, W, C, K = 1, 8, 64, 64, 128, 128            # x [N, C, D, H, W] -> y [N, K, D/2, H/2, W/2]
+    w = torch.randn(K, C, 3, 3, 3, generator=g) / math.sqrt(C * 27)
+    dy = _rand_ndhwc(N, D // 2, H // 2, W // 2, K, 94)
+    x = torch.zeros(N, C, D, H, W, requires_grad=True)
+    F.conv3d(x, _bfw(w), stride=2, padding=1).backward(_to_ncdhw(dy))
+    ref = x.grad.permute(0, 2, 3, 4, 1)
+    out = None
+    if case == "d2s_acc":
+        prev = _rand_ndhwc(N, D, H, W, C, 95)
+        out = prev.to(DEV).clone()
+        ref = ref + prev.float()
+    assert O.d2s_eligible(N, H // 2, W // 2, H, W, C, K, D // 2, D)
+    got, _ = O.conv(dy.to(DEV), C, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=(D, H, W), out=out,
+                    accumulate=case == "d2s_acc", s2d_tiled=O.s2d_tile_weights(w.to(DEV), 2))
+    _close(got, ref)
