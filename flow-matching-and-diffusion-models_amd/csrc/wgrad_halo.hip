@@ -16,6 +16,13 @@
 // MFMAs run; one barrier per tile.  Partial sums go to a split-K slab reduced by
 // wgrad_reduce (csrc/wgrad.hip), which writes the reference [K][C][3][3] layout.
 //
+// S2D (stride 2): a workgroup's input chunk is one space-to-depth plane (a, b) of the input (pixels (2y + a, 2x + b),
+// staged at the output's resolution into the same 10x18 halo) and a 64-channel block; the plane meets only the taps
+// ky = 1 (a = 0) or ky in {0, 2} (a = 1) at halo rows {0} / {-1, 0}, columns alike, so the four planes compute the
+// 9 taps exactly once between them (1, 2, 2, 4 per plane; the tap loop is instantiated per plane shape).  2-D only:
+// on config E's 3-D downsamples the per-plane workgroups (a tile's dY staged once per plane and depth tap, 1-4 taps
+// of MFMAs per staging, unequal plane loads) measured slower than the generic kernel.
+//
 // 3-D (3x3x3): tiles run over the N*D output slices and a workgroup's input chunk is a (depth tap kz,
 // 64-channel block) pair staging slice z + kz - 1 (zeros outside the sample, >> 1 under nearest-x2); its
 // 9 accumulated taps land at taps kz*9 .. kz*9+8 of a 27-tap slab, so wgrad_reduce writes [K][C][3][3][3].
@@ -59,8 +66,10 @@ struct HWArgs {
                                    // slice z + kz - 1 (stored slice >> 1 under nearest-x2; dsrc = stored depth)
 };
 
-// PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU
-template <int PRO>
+template <int V> struct IC { static constexpr int value = V; };
+
+// PRO: 0 = raw input, 1 = GroupNorm affine, 2 = affine + SiLU; S2D: stride 2 (planes as chunks)
+template <int PRO, bool S2D = false>
 __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   __shared__ __attribute__((aligned(16))) bf16r lds[2 * XBUF + 2 * DBUF];
   bf16r* xb = lds;
@@ -76,9 +85,12 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   const int tci = b % A.nci; b /= A.nci;
   const int tco = b % A.ntc; b /= A.ntc;
   const int split = b;
-  const int kz = A.depth ? tci / A.ncc : 0;            // 3-D: depth tap of this workgroup's input chunk
+  // input chunk: stride 1 tci = kz*ncc + cb (3-D) | cb; S2D (2-D) tci = plane*ncc + cb
+  const int cgrp = tci / A.ncc;
+  const int pl = S2D ? cgrp : 0, pa_ = pl >> 1, pb_ = pl & 1;
+  const int kz = A.depth ? cgrp : 0;   // 3-D: depth tap of this workgroup's input chunk
   const int zsh = A.depth ? kz - 1 : 0;
-  const int co0 = tco * WCO, ci0 = (A.depth ? tci - kz * A.ncc : tci) * WCI;
+  const int co0 = tco * WCO, ci0 = (tci - cgrp * A.ncc) * WCI;
   const int T = A.depth ? 27 : 9;
   const int t0 = split * A.per_split, t1 = min(A.ntiles, t0 + A.per_split);
   const bool do_bias = d.db != nullptr && tci == 0;
@@ -131,7 +143,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       // stored low-resolution pixel, so the LDS image is the same as without it
       const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
       const bool valid = act && zok && y >= 0 && y < d.Ho && x >= 0 && x < d.Wo;
-      const int sy = d.upsample ? y >> 1 : y, sx = d.upsample ? x >> 1 : x;
+      const int sy = S2D ? 2 * y + pa_ : d.upsample ? y >> 1 : y, sx = S2D ? 2 * x + pb_ : d.upsample ? x >> 1 : x;
       const int pix = valid ? (srcsl * d.Hs + sy) * d.Ws + sx : 0;
       rx[k] = WDBG(1) ? u32x4{0u, 0u, 0u, 0u} : *(const u32x4*)(xsrc + (size_t)pix * xcs);
       xo[k] = !act ? -1 : ((kx8 * XPAD + pos) * 8) | (valid ? 0 : (1 << 30));
@@ -213,6 +225,29 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
       for (int i = 0; i < 4; ++i) acc[i][tap] = mfma16(af[ks & 1][i], bq[sl % 3], acc[i][tap]);
     }
   };
+  // S2D: the plane's NTY x NTX taps at halo rows hy0 + jy, columns hx0 + jx (accumulator slot jy * NTX + jx)
+  const int hy0 = pa_ ? 0 : 1, hx0 = pb_ ? 0 : 1;
+  auto compute_s2d = [&](int buf, auto nty, auto ntx) {
+    constexpr int NTY = decltype(nty)::value, NTX = decltype(ntx)::value, NTP = NTY * NTX, NS = 4 * NTP;
+    bf16x8 af[2][4], bq[3];
+    auto readB = [&](int sl) {
+      const int ks = sl / NTP, t = sl % NTP, jy = t / NTX, jx = t % NTX;
+      const bf16r* p = bbase + buf * XBUF + ((2 * ks + hy0 + jy) * HR + hx0 + jx) * 8;
+      const s16x4 lo = ds_read_tr16(p), hi = ds_read_tr16(p + 4 * 8);
+      bq[sl % 3] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    readA(buf, 0, af[0]);
+    readB(0);
+    if (NS > 1) readB(1);
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+      const int ks = sl / NTP, t = sl % NTP;
+      if (t == NTP / 2 && ks < 3) readA(buf, ks + 1, af[(ks + 1) & 1]);
+      if (sl + 2 < NS) readB(sl + 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][t] = mfma16(af[ks & 1][i], bq[sl % 3], acc[i][t]);
+    }
+  };
   // bias partials (workgroups of the first cin block): each wave sums k-step wci's 32 pixels of its 64 couts, so
   // the four cin waves of a cout half cover the tile
   auto bias_sums = [&](int buf) {
@@ -240,7 +275,13 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
         load_tile(t + 1);
         dma_dy(t + 1, buf ^ 1);
       }
-      if (!WDBG(8)) compute(buf);
+      if (!WDBG(8)) {
+        if (!S2D) compute(buf);
+        else if (pl == 0) compute_s2d(buf, IC<1>(), IC<1>());
+        else if (pl == 1) compute_s2d(buf, IC<1>(), IC<2>());
+        else if (pl == 2) compute_s2d(buf, IC<2>(), IC<1>());
+        else compute_s2d(buf, IC<2>(), IC<2>());
+      }
       if (do_bias) bias_sums(buf);
       if (more) store_tile(buf ^ 1);
       if (!WDBG(16)) {
@@ -255,16 +296,22 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
   // ---- partial slab ws[split][co][tap][ci] (wgrad_reduce's layout; 3-D tap = kz*9 + ky*3 + kx)
   const size_t per = (size_t)d.K * T * A.C;
   float* ws = d.ws + (size_t)split * per;
+  // S2D: slot jy * NTX + jx of plane (a, b) is tap (ky, kx) = (a ? 2 jy : 1, b ? 2 jx : 1)
+  const int ntx = pb_ ? 2 : 1, nts = (pa_ ? 2 : 1) * ntx;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int slot = 0; slot < (S2D ? 4 : 9); ++slot) {
+      if (S2D && slot >= nts) continue;
+      const int jy = slot / ntx, jx = slot - jy * ntx;
+      const int tap = !S2D ? slot : (pa_ ? 2 * jy : 1) * 3 + (pb_ ? 2 * jx : 1);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wco * 64 + 16 * i + 4 * lq + r;
         const int ci = ci0 + wci * 16 + l16;
-        ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[i][tap][r];
+        ws[((size_t)co * T + kz * 9 + tap) * A.C + ci] = acc[i][slot][r];
       }
+    }
   if (do_bias) {
     // lanes of the 4 pixel groups, then the 4 cin-waves (each summed one k-step) of a cout half
     float* red = (float*)lds;    // [4 wci][128 co] floats; the tiles are done
@@ -288,14 +335,17 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const HWArgs A) {
 
 }  // namespace
 
-// 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
+// 3x3 / stride 1 / pad 1 (optionally on the nearest-x2 upsample of src) or 2-D stride 2 / pad 1 (Hs = 2 Ho,
+// Ws = 2 Wo), K % 128 == 0, C % 64 == 0, Ho % 8 == 0, Wo % 16 == 0.
 // Returns 1 (nothing launched) when the problem does not qualify.  d->splits = pixel-tile splits.
 extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
-  if (d->ks != 3 || d->stride != 1 || d->pad != 1) return 1;
+  const bool s2 = d->stride == 2;   // S2D (2-D): the input's space-to-depth planes as chunks
+  if (d->ks != 3 || (d->stride != 1 && !s2) || d->pad != 1 || (s2 && d->upsample)) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;
-  if (d3 && d->Do != (d->upsample ? 2 * d->Ds : d->Ds)) return 1;   // 3-D: stride-1 3x3x3 (nearest-x2)
+  if (d3 && (s2 || d->Do != (d->upsample ? 2 * d->Ds : d->Ds))) return 1;   // 3-D: stride-1 3x3x3 (nearest-x2)
   const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
-  if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
+  if (s2 ? (d->Hs != 2 * d->Ho || d->Ws != 2 * d->Wo)
+         : d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (d->Ho % WTH || d->Wo % WTW) return 1;
   const int C = d->C0 + d->C1;
   if (d->K % WCO || C % WCI || (d->C0 % 8) || !d->ws) return 1;
@@ -313,7 +363,7 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   A.depth = d3 ? d->Do : 0;
   A.dsrc = d3 ? d->Ds : 0;
   A.ncc = C / WCI;
-  A.nci = d3 ? 3 * A.ncc : A.ncc;
+  A.nci = (d3 ? 3 : s2 ? 4 : 1) * A.ncc;
   A.splits = d->splits > 1 ? d->splits : 1;
   A.per_split = (A.ntiles + A.splits - 1) / A.splits;
 #ifdef FMD_HALO_DBG
@@ -324,7 +374,11 @@ extern "C" int fmd_wgrad_halo(const fmd_wgrad_desc* d, fmd_stream_t stream) {
   const int nwg = A.ntc * A.nci * A.splits;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
   hipStream_t st = (hipStream_t)stream;
-  if (pro == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(nwg), dim3(NT), 0, st, A);
+  if (s2) {
+    if (pro == 2) hipLaunchKernelGGL((wgrad_halo_kernel<2, true>), dim3(nwg), dim3(NT), 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, true>), dim3(nwg), dim3(NT), 0, st, A);
+    else hipLaunchKernelGGL((wgrad_halo_kernel<0, true>), dim3(nwg), dim3(NT), 0, st, A);
+  } else if (pro == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, dim3(nwg), dim3(NT), 0, st, A);
   else if (pro == 1) hipLaunchKernelGGL(wgrad_halo_kernel<1>, dim3(nwg), dim3(NT), 0, st, A);
   else hipLaunchKernelGGL(wgrad_halo_kernel<0>, dim3(nwg), dim3(NT), 0, st, A);
   return (int)hipGetLastError();

@@ -569,12 +569,17 @@ WGRAD_HALO_WG = tuning.get("WGRAD_HALO_WG") or NUM_CU
 # WGRAD_GEN_SLAB_MB)
 WGRAD_SLAB_MB = tuning.get("WGRAD_SLAB_MB")
 WGRAD_GEN_SLAB_MB = tuning.get("WGRAD_GEN_SLAB_MB")
+WGRAD_S2D = bool(tuning.get("WGRAD_S2D"))
 
 
 def wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, C, C0, ks=3, stride=1, pad=1, upsample=False, ldy=None) -> bool:
-    """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip)."""
-    return (ks == 3 and stride == 1 and pad == 1 and (Ho == 2 * Hs and Wo == 2 * Ws if upsample else
-                                                      Ho == Hs and Wo == Ws) and Ho % 8 == 0
+    """Mirror of fmd_wgrad_halo's applicability test (csrc/wgrad_halo.hip): 3x3 pad 1, stride 1 (optionally on a
+    nearest-x2 input) or 2-D stride 2 (the space-to-depth planes as chunks; 3-D stride 2 stays generic)."""
+    if stride == 2:
+        geo = WGRAD_S2D and not upsample and Hs == 2 * Ho and Ws == 2 * Wo
+    else:
+        geo = stride == 1 and (Ho == 2 * Hs and Wo == 2 * Ws if upsample else Ho == Hs and Wo == Ws)
+    return (ks == 3 and pad == 1 and geo and Ho % 8 == 0
             and Wo % 16 == 0 and K % 128 == 0 and C % 64 == 0 and C0 % 8 == 0 and (ldy or K) % 8 == 0)
 
 
@@ -617,13 +622,13 @@ def wgrad(src0, dy, dw, *, src1=None, ks=3, stride=1, pad=1, upsample=False, pro
     d.dy, d.ldy, d.dw, d.db, d.accumulate = dy.data_ptr() + 2 * dy_offset, ldy, _p(dw), _p(db), int(accumulate)
     d.force_generic = int(force_generic)
     if splits is None:
-        if (not force_generic and (not d3 or Do == (2 * Ds if upsample else Ds)) and
+        if (not force_generic and (not d3 or (stride == 1 and Do == (2 * Ds if upsample else Ds))) and
                 wgrad_halo_eligible(Hs, Ws, Ho, Wo, K, Ct, C0, ks, stride, pad, upsample, ldy)):
-            # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk [x depth tap], pixel-tile
-            # split); partial slabs capped at ~96 MB (their write + reduce read)
+            # halo kernel: one workgroup per CU over (cout tile, 64-cin chunk [x depth tap | x stride-2 plane],
+            # pixel-tile split); partial slabs capped at ~96 MB (their write + reduce read)
             zt = 3 if d3 else 1
             tiles = N * max(Do, 1) * (Ho // 8) * (Wo // 16)
-            base = (K // 128) * (Ct // 64) * zt
+            base = (K // 128) * (Ct // 64) * zt * (4 if stride == 2 else 1)
             splits = max(1, min(tiles, -(-WGRAD_HALO_WG // base), (WGRAD_SLAB_MB << 20) // (K * Ct * 36 * zt)))
         else:
             # narrow inputs (Ct < 128, T > 1) tile the flattened (tap, cin) pairs (csrc/wgrad.hip make_args

@@ -21,6 +21,8 @@ TABLE = {
     "S2D_HALO": (1, "stride-2 3x3 forwards / nearest-x2 data gradients on the space-to-depth halo kernel"),
     "S2D_3D": (1, "3-D: the same stride-2 modes with the depth taps as chunks (0: generic implicit GEMM, and the "
                   "nearest-x2 data gradient at full resolution + 2x2x2 box sum)"),
+    "WGRAD_S2D": (1, "stride-2 3x3 (3x3x3) weight gradients on the halo weight-gradient kernel (space-to-depth planes "
+                     "as chunks; 0: the generic weight-gradient kernel)"),
     "POINT_1X1": (1, "ResBlock 3x3 convs on 1x1 images as their centre tap"),
     "GN_FUSED": (1, "small levels: GroupNorm statistics + affine + SiLU operand in one launch"),
     "CONV_GN": (1, "split-K conv1 -> GroupNorm-2 in the split combine (fmd_conv_gn)"),

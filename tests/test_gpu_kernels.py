@@ -344,6 +344,46 @@ def test_wgrad_halo_vs_torch(case):
     torch.testing.assert_close(db.cpu(), bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("case", ["plain", "pro_concat"])
+def test_wgrad_halo_stride2_vs_torch(case):
+    """Halo weight gradient of a 2-D stride-2 3x3 conv (the space-to-depth planes as chunks: DownsampleND's conv,
+    csrc/wgrad_halo.hip S2D) vs torch autograd on the bf16-rounded operands, and vs the generic kernel on the same
+    inputs; the second case with a GN+SiLU prologue over a two-source concat."""
+    O = ops()
+    g = torch.Generator().manual_seed(97)
+    N, H, W, C0, K = 4, 64, 64, 64, 128
+    C1 = 64 if case == "pro_concat" else 0
+    x0 = _rand_nhwc(N, H, W, C0, 98)
+    x1 = _rand_nhwc(N, H, W, C1, 99) if C1 else None
+    x = _to_nchw(torch.cat([x0, x1], -1) if C1 else x0)
+    C = C0 + C1
+    pro = None
+    if case == "pro_concat":
+        a = torch.rand(N, C, generator=g) + 0.5
+        b = torch.randn(N, C, generator=g) * 0.2
+        pro = (a.to(DEV), b.to(DEV), True)
+        x = F.silu(x * a[:, :, None, None] + b[:, :, None, None]).to(torch.bfloat16).float()
+    w = (torch.randn(K, C, 3, 3, generator=g) / math.sqrt(C * 9)).requires_grad_()
+    bias = torch.zeros(K, requires_grad=True)
+    y = F.conv2d(x, w, bias, stride=2, padding=1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(DEV)
+    assert O.wgrad_halo_eligible(H, W, H // 2, W // 2, K, C, C0, 3, 2)
+    res = []
+    for generic in (False, True):
+        dw = torch.zeros(K, C, 3, 3, device=DEV)
+        db = torch.zeros(K, device=DEV)
+        O.wgrad(x0.to(DEV), dyn, dw, src1=x1.to(DEV) if C1 else None, pro=pro, ks=3, stride=2, pad=1, db=db,
+                force_generic=generic)
+        res.append((dw.cpu(), db.cpu()))
+    for dw, db in res:
+        torch.testing.assert_close(dw, w.grad, rtol=2e-2, atol=2e-2 * w.grad.abs().max().item())
+        torch.testing.assert_close(db, bias.grad, rtol=1e-3, atol=1e-3 * bias.grad.abs().max().item())
+    rel = ((res[0][0] - res[1][0]).norm() / res[1][0].norm()).item()
+    assert rel < 5e-3, rel
+
+
 @pytest.mark.parametrize("C,rows_img,N", [(128, 32768, 1), (384, 4096, 2), (1030, 512, 1), (6, 256, 3)])
 def test_stats_fold(C, rows_img, N):
     """fmd_stats_fold: 128 consecutive slab rows summed (row-lane chains + fixed-order lane combine) vs torch."""
