@@ -120,6 +120,18 @@ __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const f
   const int c_begin = g * Cg;
   const int E0 = HW / rows0;
   const int E1 = C1 ? HW / rows1 : 0;
+  // the affine inputs of this thread's channel, loaded before the slab reduction (their latency under its loads
+  // instead of after the block's final barrier)
+  float gm = 1.f, bt = 0.f, es = 1.f, esh = 0.f;
+  if ((int)threadIdx.x < Cg) {
+    const int c = c_begin + threadIdx.x;
+    if (gamma) gm = gamma[c];
+    if (beta) bt = beta[c];
+    if (emb_mode == 1) {
+      es = 1.f + emb[(size_t)n * emb_stride + c];
+      esh = emb[(size_t)n * emb_stride + C + c];
+    }
+  }
   double s1 = 0.0, s2 = 0.0;
   const bool in0 = c_begin + Cg <= C0, in1 = c_begin >= C0;
   if ((in0 || in1) && (Cg & 1) == 0) {
@@ -197,16 +209,21 @@ __global__ void gn_prep_kernel(const float* __restrict__ st0, int rows0, const f
   const float meanf = (float)mean;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   if (threadIdx.x == 0 && mr) { mr[((size_t)n * G + g) * 2] = meanf; mr[((size_t)n * G + g) * 2 + 1] = rstd; }
-  for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
+  for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {   // (channels past the block size: loaded here)
     const int c = c_begin + cl;
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    if (cl >= (int)blockDim.x) {
+      gm = gamma ? gamma[c] : 1.f;
+      bt = beta ? beta[c] : 0.f;
+      if (emb_mode == 1) {
+        es = 1.f + emb[(size_t)n * emb_stride + c];
+        esh = emb[(size_t)n * emb_stride + C + c];
+      }
+    }
     float av = rstd * gm;
     float bv = bt - meanf * av;
     if (emb_mode == 1) {
-      const float s = 1.f + emb[(size_t)n * emb_stride + c];
-      const float sh = emb[(size_t)n * emb_stride + C + c];
-      av *= s;
-      bv = bv * s + sh;
+      av *= es;
+      bv = bv * es + esh;
     }
     a[(size_t)n * C + c] = av;
     b[(size_t)n * C + c] = bv;
