@@ -38,10 +38,10 @@ constexpr bool H9_SCHED = FMD_H9_SCHED;   // v9b: pinned read/MFMA interleave of
 #define FMD_H9_LAG 3   // taps between a staging round's load and its transform (2: 22.94 / 23.00 vs 3: 22.89 / 22.89 ms per train step)
 #endif
 
-template <bool UP>
+template <bool UP, int THT = TH>
 struct G9 {
   static constexpr int HROW = UP ? TW / 2 + 2 : TW + 2;           // halo row (positions)
-  static constexpr int HPOS = UP ? (TH / 2 + 2) * HROW : (TH + 2) * HROW;
+  static constexpr int HPOS = UP ? (THT / 2 + 2) * HROW : (THT + 2) * HROW;
   static constexpr int HPOSP = (HPOS + 7) / 8 * 8;                 // positions rounded to 8-position pieces rows
   static constexpr int HPAD = (HPOSP + 15) / 16 * 16;              // plane stride == 0 mod 16 bank slots
   static constexpr int HBUF = KC * HPAD * 16;                      // bytes per halo buffer
@@ -97,10 +97,15 @@ FMD_DEV void fence8_(float (&y)[8]) {
 // slices and chunk = (depth tap kz < ks, plane, block) stages full-resolution slice 2z + kz - 1 (zeros outside the
 // sample).  D2S: images are the N*Ds gradient slices, the output classes are 8 (depth parity, a, b; class-major) and
 // chunk = (depth offset dz, block) stages gradient slice z + dz; class (c, a, b) writes full-resolution slice 2z + c.
-template <bool UP, int PRO, int MODE = 0>
+// THT: tile rows (16, or 8 for grids that would otherwise leave CUs with one workgroup or one round: twice the
+// workgroups, half the accumulators; plain 3x3 / nearest-x2 only)
+template <bool UP, int PRO, int MODE = 0, int THT = TH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
-  using G = G9<UP>;
+  static_assert(THT == TH || (THT == 8 && MODE == 0), "8-row tiles: plain / nearest-x2 gathers only");
+  using G = G9<UP, THT>;
+  constexpr int NPB = THT / 2;               // 32-pixel blocks (2 rows) per wave
+  constexpr int OUT_T = THT * TW * BCO * 2;
   constexpr int HROW = G::HROW, HPAD = G::HPAD, HBUF = G::HBUF, NR = G::NR;
   constexpr bool S2D = MODE == 1, D2S = MODE == 2;
   static_assert(!(MODE && UP), "stride-2 modes are not nearest-x2 gathers");
@@ -110,7 +115,7 @@ void conv3x3_halo9b(const HArgs A) {
   constexpr int SL = RPT * LAG;              // staging register slots (rounds in flight)
   constexpr int RB = MODE ? 4 : 3;           // B-fragment ring (NTAP % RB == 0 keeps its phase per chunk)
   static_assert(NTAP % RB == 0 && (NR + RPT - 1) / RPT + LAG <= NTAP, "chunk pipeline");
-  constexpr int SM_COEF = 2 * HBUF > OUT_TILE ? 2 * HBUF : OUT_TILE;
+  constexpr int SM_COEF = 2 * HBUF > OUT_T ? 2 * HBUF : OUT_T;
   constexpr int ZCOEF = 2 * CMAX;   // 8 zero coefficients: the affine of a chunk's invalid channels (-> SiLU(0) = 0)
   constexpr int SM_EPI = SM_COEF + (2 * CMAX + 8) * 4;
   constexpr int SM_BYTES = SM_EPI + 3 * BCO * 4;
@@ -131,7 +136,7 @@ void conv3x3_halo9b(const HArgs A) {
   const int tin = tile - n * per_img;
   const int smp = A.depth ? n / A.depth : n;
   const int zz = A.depth ? n - smp * A.depth : 0;
-  const int ty0 = (tin / A.tiles_x) * TH, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
+  const int ty0 = (tin / A.tiles_x) * THT, tx0 = (tin - (tin / A.tiles_x) * A.tiles_x) * TW;
   // D2S: cout tile tco = (output class, 128-cout block), class-major
   const int ncob = D2S ? d.K / BCO : 1;
   const int ocls = D2S ? tco / ncob : 0;
@@ -336,9 +341,9 @@ void conv3x3_halo9b(const HArgs A) {
               : abase + (s * 2 * HPAD + (2 * pb + ky) * HROW + kx) * 16;
   };
 
-  f32x16 acc[8];
+  f32x16 acc[NPB];
 #pragma unroll
-  for (int pb = 0; pb < 8; ++pb)
+  for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[pb][e] = 0.f;
 
@@ -346,16 +351,17 @@ void conv3x3_halo9b(const HArgs A) {
   // groups ahead of their MFMAs (sched_group_barrier: 8 reads, then 4 MFMAs + 4 reads per group), so each group's
   // LDS latency hides under the previous group's 4 x 32 MFMA cycles instead of every MFMA waiting on its read
   auto tap_mma = [&](int tap, int hb, const bf16x8 (&bq)[2]) {
-    bf16x8 af[16];
+    constexpr int NG = NPB / 4;   // groups of 4 pixel blocks per k-half
+    bf16x8 af[2 * NPB];
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 2 * NG; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[4 * g + i] = *(const bf16x8*)(smem + hb + aoff(tap, g >> 1, 4 * (g & 1) + i));
+      for (int i = 0; i < 4; ++i) af[4 * g + i] = *(const bf16x8*)(smem + hb + aoff(tap, g / NG, 4 * (g % NG) + i));
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 2 * NG; ++g)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[4 * (g & 1) + i] = mfma32(af[4 * g + i], bq[g >> 1], acc[4 * (g & 1) + i]);
-    if constexpr (H9_SCHED) {
+      for (int i = 0; i < 4; ++i) acc[4 * (g % NG) + i] = mfma32(af[4 * g + i], bq[g / NG], acc[4 * (g % NG) + i]);
+    if constexpr (H9_SCHED && NPB == 8) {
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -370,9 +376,9 @@ void conv3x3_halo9b(const HArgs A) {
     setup(ch);
     u32x4 sv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *(const u32x4*)(sok ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2);
+    for (int q = 0; q < THT / 4; ++q) sv[q] = *(const u32x4*)(sok ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < THT / 4; ++q)
       *(u32x4*)(smem + buf + s2dst0 + q * 72 * 16) = sok ? sv[q] : u32x4{0u, 0u, 0u, 0u};
   };
 
@@ -388,7 +394,7 @@ void conv3x3_halo9b(const HArgs A) {
   if (A.splits <= 1) {   // the summed bias is the accumulators' start value
     const float bv = epi[32 * wid + r];
 #pragma unroll
-    for (int pb = 0; pb < 8; ++pb)
+    for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[pb][e] = bv;
   }
@@ -475,10 +481,10 @@ void conv3x3_halo9b(const HArgs A) {
     const bool more = i + 1 < n_seg2;
     setup(more ? ch + 1 : -1);
     loadB(bq[2], min(T1 + i + 2, last2));
-    u32x4 sv[4];
-    int so[4];
+    u32x4 sv[THT / 4];
+    int so[THT / 4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < THT / 4; ++q) {
       const bool valid = more && sok;
       const bf16r* src = valid ? sbase + (size_t)(s2pix0 + 4 * q * d.Wo) * scs : s2;
       sv[q] = *(const u32x4*)src;
@@ -486,7 +492,7 @@ void conv3x3_halo9b(const HArgs A) {
     }
     tap_mma(4, (ch & 1) * HBUF, bq[0]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < THT / 4; ++q) {
       u32x4 v = sv[q];
       if (so[q] & ZFLAG) v = u32x4{0u, 0u, 0u, 0u};
       *(u32x4*)(smem + ((ch + 1) & 1) * HBUF + (so[q] & ~ZFLAG)) = v;
@@ -512,7 +518,7 @@ void conv3x3_halo9b(const HArgs A) {
     const int co = co0 + 32 * wid + r;
     if (co < K) {
 #pragma unroll
-      for (int pb = 0; pb < 8; ++pb)
+      for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int pi = pixl(pb, (e & 3) + 8 * (e >> 2) + 4 * hh);
@@ -553,7 +559,7 @@ void conv3x3_halo9b(const HArgs A) {
   const float ea = epi[BCO + cl + r], eb = epi[2 * BCO + cl + r];
   float st1 = 0.f, st2 = 0.f;
 #pragma unroll
-  for (int pb = 0; pb < 8; ++pb) {
+  for (int pb = 0; pb < NPB; ++pb) {
     const int pi_l = pixl(pb, r);
     f32x16 v = acc[pb];
     f32x16 xc;
@@ -564,7 +570,7 @@ void conv3x3_halo9b(const HArgs A) {
         *(u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16)) = sv[pb & 1][j];
       }
       __syncthreads();
-      if (pb + 2 < 8) {
+      if (pb + 2 < NPB) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) sv[pb & 1][j] = *(const u32x4*)side_piece(2 * pb + 4 + j);
       }
@@ -618,7 +624,7 @@ void conv3x3_halo9b(const HArgs A) {
       *(u32x2*)(tileb + pi_l * 256 + (((c >> 3) ^ (pi_l & 15)) * 16) + (c & 7) * 2) = o;
     }
     if (stats && (pb & 1)) {   // one statistics row per 64 pixels (= pixel blocks 2k, 2k+1: 4 tile rows)
-      const int srow = (D2S ? tile * (A.depth ? 8 : 4) + ocls : tile) * 4 + (pb >> 1);
+      const int srow = (D2S ? tile * (A.depth ? 8 : 4) + ocls : tile) * (THT * TW / 64) + (pb >> 1);
       const float a = st1 + __shfl_xor(st1, 32, 64);
       const float q = st2 + __shfl_xor(st2, 32, 64);
       if (hh == 0) {
@@ -632,7 +638,7 @@ void conv3x3_halo9b(const HArgs A) {
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < TH * TW * BCO / 8 / NT9; ++k) {
+  for (int k = 0; k < THT * TW * BCO / 8 / NT9; ++k) {
     const int q = tid + NT9 * k, pi = q >> 4, c16 = q & 15;
     *(u32x4*)((bf16r*)d.out + (size_t)opix(pi) * K + co0 + c16 * 8) =
         *(const u32x4*)(tileb + pi * 256 + ((c16 ^ (pi & 15)) * 16));
@@ -641,26 +647,48 @@ void conv3x3_halo9b(const HArgs A) {
 
 }  // namespace
 
+namespace {
+// grids of fewer workgroups than this (16-row tiles x splits) run 8-row tiles: at 128^2 / 64^2 a 16-row grid is one
+// round of 512 (or 256) workgroups whose prologues and epilogues all coincide (0 = never)
+int g_th8_max_wg = 1024;
+
+template <int THT>
+int halo9_go(const HArgs& A, int pro, fmd_stream_t stream) {
+  const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
+  const dim3 g(nwg, A.splits);
+  const dim3 blk(NT9);
+  hipStream_t st = (hipStream_t)stream;
+  if (A.d.upsample) {
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<true, 2, 0, THT>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<true, 1, 0, THT>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo9b<true, 0, 0, THT>), g, blk, 0, st, A);
+  } else {
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, 0, THT>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, 0, THT>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 0, THT>), g, blk, 0, st, A);
+  }
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int fmd_halo_set_th8_max_workgroups(int32_t n) {
+  g_th8_max_wg = n < 0 ? 0 : n;
+  return 0;
+}
+
 int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const fmd_conv_desc* d = &A.d;
   if (d->gout) return 1;
   if (d->upsample && d->src2) return 1;
   if (A.splits <= 1 && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
   if (A.splits > 1 && (d->out_f32 || d->accumulate)) return 1;
-  const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
-  const dim3 g(nwg, A.splits);
-  const dim3 blk(NT9);
-  hipStream_t st = (hipStream_t)stream;
-  if (d->upsample) {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<true, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<true, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo9b<true, 0>), g, blk, 0, st, A);
-  } else {
-    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2>), g, blk, 0, st, A);
-    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1>), g, blk, 0, st, A);
-    else hipLaunchKernelGGL((conv3x3_halo9b<false, 0>), g, blk, 0, st, A);
+  const long long nwg16 = (long long)A.d.N * A.tiles_x * A.tiles_y * A.ntc * A.splits;
+  if (nwg16 < g_th8_max_wg && d->Ho % 8 == 0) {
+    HArgs A8 = A;
+    A8.tiles_y = d->Ho / 8;
+    return halo9_go<8>(A8, pro, stream);
   }
-  return (int)hipGetLastError();
+  return halo9_go<TH>(A, pro, stream);
 }
 
 // ---------------------------------------------------------------------------------------------------------------

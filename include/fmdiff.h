@@ -138,6 +138,10 @@ int fmd_conv_gn(const fmd_conv_desc* d, const fmd_gn_out_desc* g, fmd_stream_t s
  * (default 32; fewer go to the implicit GEMM).  The Python side applies its tuning table's HALO_MIN_WG through it
  * (fmdiff/runtime/tuning.py); the host's halo_splits mirror reads the same table entry. */
 int fmd_halo_set_min_workgroups(int32_t n);
+/* Halo-conv grids with fewer workgroups than n (16-row tiles x cout tiles x splits; default 1024) run 8-row tiles
+ * instead (twice the workgroups: the 128^2 / 64^2 levels would otherwise be one lock-step round); 0 = never.  A
+ * tuning hook (tuning table HALO_TH8_MAX_WG). */
+int fmd_halo_set_th8_max_workgroups(int32_t n);
 /* Fewest channels per combine block of fmd_conv_gn (4, 8, 16, 32 or 64; default 4):
  * a block owns max(cb, K / G) channels = whole groups.  Returns -1 for any other value.  A tuning hook; the host's
  * conv_gn_eligible mirror reads ops.CONV_GN_CB. */

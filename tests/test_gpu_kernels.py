@@ -697,6 +697,60 @@ def test_halo_conv_matches_generic(case):
         torch.testing.assert_close(ta, tb, rtol=5e-3, atol=3e-2)
 
 
+@pytest.mark.parametrize("case", ["pro_stats", "resid", "upsample_pro", "skip_seg2", "dgrad_ep", "split_k", "depth3d"])
+def test_halo_conv_8_row_tiles_match_16_row_tiles(case):
+    """conv3x3_halo9b with 8-row tiles (the default for grids under 1024 workgroups, fmd_halo_set_th8_max_workgroups)
+    against the 16-row form on the same problem: outputs bit-identical (same per-pixel summation order), statistics
+    equal as per-sample totals (their rows are the same 64-pixel blocks in another order)."""
+    from fmdiff import _lib
+    O = ops()
+    L = _lib.lib()
+    N, H, W, C0, K = 8, 64, 64, 64, 128
+    d3 = case == "depth3d"
+    up = case == "upsample_pro"
+    Hs, Ws = (H // 2, W // 2) if up else (H, W)
+    if d3:
+        N, D, H, W = 2, 8, 32, 32
+        Hs, Ws = H, W
+        x0 = _rand_ndhwc(N, D, H, W, C0, 41).to(DEV)
+        wf = (torch.randn(K, C0, 3, 3, 3) / math.sqrt(C0 * 27)).to(DEV)
+    else:
+        x0 = _rand_nhwc(N, Hs, Ws, C0, 41).to(DEV)
+    kw = dict(bias=(torch.randn(K) * 0.1).to(DEV))
+    if case in ("pro_stats", "upsample_pro", "split_k"):
+        kw["pro"] = ((torch.rand(N, C0) + 0.5).to(DEV), (torch.randn(N, C0) * 0.2).to(DEV), True)
+    if case == "resid":
+        kw["resid"] = _rand_nhwc(N, H, W, K, 42).to(DEV)
+    if case == "skip_seg2":
+        kw.update(src2=_rand_nhwc(N, H, W, 96, 43).to(DEV), src3=_rand_nhwc(N, H, W, 32, 44).to(DEV),
+                  wgt2=O.prep_weights(_w(K, 128, 1, 45).to(DEV), 0), bias2=(torch.randn(K) * 0.1).to(DEV))
+    if case == "dgrad_ep":
+        kw["ep"] = (_rand_nhwc(N, H, W, K, 46).to(DEV), None, (torch.rand(N, K) + 0.5).to(DEV),
+                    (torch.randn(N, K) * 0.2).to(DEV))
+    if case == "split_k":
+        kw["splits"] = 2
+    want = case in ("pro_stats", "upsample_pro", "dgrad_ep", "depth3d")
+    res = []
+    try:
+        for lim in (1 << 30, 0):   # 8-row tiles for every grid, then never
+            L.fmd_halo_set_th8_max_workgroups(lim)
+            if d3:
+                from fmdiff.runtime.engine import WeightCache
+                out, st = O.conv(x0, K, None, ks=3, want_stats=want, wgt_tiled=WeightCache().dtiled(wf, 0), **kw)
+            else:
+                w = O.prep_weights(_w(K, C0, 3, 47).to(DEV), 0)
+                out, st = O.conv(x0, K, w, upsample=up, want_stats=want, **kw)
+            torch.cuda.synchronize()
+            res.append((out.clone(), None if st is None else st.slab.clone()))
+    finally:
+        L.fmd_halo_set_th8_max_workgroups(1024)
+    assert torch.equal(res[0][0], res[1][0])
+    if want:
+        ta = res[0][1].double().view(N, -1, K, 2).sum(1)
+        tb = res[1][1].double().view(N, -1, K, 2).sum(1)
+        torch.testing.assert_close(ta, tb, rtol=1e-6, atol=1e-4)
+
+
 @pytest.mark.parametrize("case", ["fwd_pro_stats", "dgrad_ep_stats"])
 def test_halo_conv_bench_problem_vs_torch(case):
     """The bench's roofline kernel on the bench's own problem -- non-split conv3x3_halo at 8x256^2, 128 -> 128
