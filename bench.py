@@ -71,8 +71,8 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.conv(x, K, w, pro=(a, b, True), bias=bias, out=out, want_stats=True, wgt_tiled=wt)
-        kernel = "conv3x3_halo9b<false, 2, 0> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)"
-        kid = ["conv3x3_halo9b<false, 2, 0>"]
+        kernel = "conv3x3_halo9b<false, 2, 0, 16> (GN+SiLU prologue, 3x3, 8x256x256x128->128, fused stats)"
+        kid = ["conv3x3_halo9b<false, 2, 0, 16>"]
     elif prob == "dgrad":
         w = ops.prep_weights(wf, 3)
         wt = ops.tile_weights(w)
@@ -80,9 +80,9 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.conv(dy, C, w, out=out, want_stats=True, ep=(x, None, a, b), wgt_tiled=wt)
-        kernel = ("conv3x3_halo9b<false, 0, 0> data gradient (flipped taps, SiLU' + GN-backward-sums epilogue, "
+        kernel = ("conv3x3_halo9b<false, 0, 0, 16> data gradient (flipped taps, SiLU' + GN-backward-sums epilogue, "
                   "8x256x256x128->128)")
-        kid = ["conv3x3_halo9b<false, 0, 0>"]
+        kid = ["conv3x3_halo9b<false, 0, 0, 16>"]
     else:
         dy = torch.randn(N, H, W, K, device=dev, generator=g).to(torch.bfloat16)
         dw = torch.zeros(K, C, 3, 3, device=dev)
@@ -90,8 +90,8 @@ def conv_roofline(dev, iters=20, prob="fwd"):
 
         def fn():
             ops.wgrad(x, dy, dw, pro=(a, b, True), db=db)
-        kernel = "wgrad_halo_kernel<2> + wgrad_reduce2 (GN+SiLU recomputed, 8x256x256x128->128x3x3, fp32 dW)"
-        kid = ["wgrad_halo_kernel<2>", "wgrad_reduce2"]
+        kernel = "wgrad_halo_kernel<2, false> + wgrad_reduce2 (GN+SiLU recomputed, 8x256x256x128->128x3x3, fp32 dW)"
+        kid = ["wgrad_halo_kernel<2, false>", "wgrad_reduce2"]
     for _ in range(3):
         fn()
     # In the train step the 134 MB input arrives cold (written by an earlier kernel, evicted by the ones

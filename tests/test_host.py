@@ -264,13 +264,14 @@ def test_bench_pmc_traffic_matches_timed_kernel_only():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    fwd = bench.pmc_traffic("conv3x3_halo9b<false, 2, 0>")
+    fwd = bench.pmc_traffic("conv3x3_halo9b<false, 2, 0, 16>")
     assert fwd is not None and fwd["file"].startswith("profiles/r5_")
     assert 2.5e8 < fwd["bytes"] < 4e8   # ~1.05x the 276.8 MB algorithmic bytes of the 8x256^2x128 problem
-    wg = bench.pmc_traffic(["wgrad_reduce2", "wgrad_halo_kernel<2>"])   # order-free set of kernels
+    wg = bench.pmc_traffic(["wgrad_reduce2", "wgrad_halo_kernel<2, false>"])   # order-free set of kernels
     assert wg is not None and wg["file"].endswith("r5_wgrad_traffic.json")
     assert bench.pmc_traffic("conv3x3_halo<false, 2, false>") is None   # round 3's kernel: not the timed one
-    assert bench.pmc_traffic(["wgrad_halo_kernel<2>"]) is None          # a subset is not the timed pair
+    assert bench.pmc_traffic(["wgrad_halo_kernel<2, false>"]) is None   # a subset is not the timed pair
+    assert bench.pmc_traffic("conv3x3_halo9b<false, 2, 0, 8>") is None   # the 8-row instance: not the timed one
 
 
 def test_tuning_table_and_override(monkeypatch):

@@ -39,13 +39,13 @@ def main():
         j = json.loads(line)
         bench = {"fwd": j["roofline"]["kernel_ms"] * 1e3, "dgrad": j["roofline_backward"]["dgrad"]["kernel_ms"] * 1e3,
                  "wgrad": j["roofline_backward"]["wgrad"]["kernel_ms"] * 1e3}
-    for prob, kname in (("fwd", "conv3x3_halo9b<false, 2, 0>"), ("dgrad", "conv3x3_halo9b<false, 0, 0>")):
+    for prob, kname in (("fwd", "conv3x3_halo9b<false, 2, 0, 16>"), ("dgrad", "conv3x3_halo9b<false, 0, 0, 16>")):
         sel = [r for r in rows if r["name"] == kname and int(r["Grid_Size_X"]) == 2048 * 256 and r["Grid_Size_Y"] == "1"]
         d = [r["us"] for r in sel[-a.n:]]
         ev = f", bench.py HIP events {bench[prob]:.1f} us" if prob in bench else ""
         print(f"{prob:6s} {kname} (8x256x256x128->128) last {len(d)} launches: mean {sum(d) / len(d):.1f} us "
               f"({GF / (sum(d) / len(d)) * 1e3:.0f} TF/s), min {min(d):.1f}, max {max(d):.1f}{ev}")
-    idx = [i for i, r in enumerate(rows) if r["name"] == "wgrad_halo_kernel<2>"]
+    idx = [i for i, r in enumerate(rows) if r["name"] == "wgrad_halo_kernel<2, false>"]
     grid = rows[idx[-1]]["Grid_Size_X"]
     idx = [i for i in idx if rows[i]["Grid_Size_X"] == grid][-a.n:]
     kern, red = [], []
@@ -55,7 +55,7 @@ def main():
         red.append(nxt["us"] if nxt else 0.0)
     tot = [k + r for k, r in zip(kern, red)]
     ev = f", bench.py HIP events {bench['wgrad']:.1f} us" if "wgrad" in bench else ""
-    print(f"wgrad  wgrad_halo_kernel<2> + wgrad_reduce2 last {len(tot)}: kernel mean {sum(kern) / len(kern):.1f} us, "
+    print(f"wgrad  wgrad_halo_kernel<2, false> + wgrad_reduce2 last {len(tot)}: kernel mean {sum(kern) / len(kern):.1f} us, "
           f"reduce mean {sum(red) / len(red):.1f} us, sum {sum(tot) / len(tot):.1f} us "
           f"({GF / (sum(tot) / len(tot)) * 1e3:.0f} TF/s){ev}")
 
