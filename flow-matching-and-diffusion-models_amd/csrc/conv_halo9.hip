@@ -98,11 +98,11 @@ FMD_DEV void fence8_(float (&y)[8]) {
 // sample).  D2S: images are the N*Ds gradient slices, the output classes are 8 (depth parity, a, b; class-major) and
 // chunk = (depth offset dz, block) stages gradient slice z + dz; class (c, a, b) writes full-resolution slice 2z + c.
 // THT: tile rows (16, or 8 for grids that would otherwise leave CUs with one workgroup or one round: twice the
-// workgroups, half the accumulators; plain 3x3 / nearest-x2 only)
+// workgroups, half the accumulators)
 template <bool UP, int PRO, int MODE = 0, int THT = TH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
-  static_assert(THT == TH || (THT == 8 && MODE == 0), "8-row tiles: plain / nearest-x2 gathers only");
+  static_assert(THT == TH || THT == 8, "16- or 8-row tiles");
   using G = G9<UP, THT>;
   constexpr int NPB = THT / 2;               // 32-pixel blocks (2 rows) per wave
   constexpr int OUT_T = THT * TW * BCO * 2;
@@ -827,8 +827,16 @@ extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;
   const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
-  const dim3 g(nwg), blk(NT9);
   hipStream_t st = (hipStream_t)stream;
+  if (nwg < g_th8_max_wg) {   // 8-row tiles on a one-round grid (as halo9_launch)
+    A.tiles_y = d->Ho / 8;
+    const dim3 g(2 * nwg), blk(NT9);
+    if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, 1, 8>), g, blk, 0, st, A);
+    else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, 1, 8>), g, blk, 0, st, A);
+    else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 1, 8>), g, blk, 0, st, A);
+    return (int)hipGetLastError();
+  }
+  const dim3 g(nwg), blk(NT9);
   if (pro == 2) hipLaunchKernelGGL((conv3x3_halo9b<false, 2, 1>), g, blk, 0, st, A);
   else if (pro == 1) hipLaunchKernelGGL((conv3x3_halo9b<false, 1, 1>), g, blk, 0, st, A);
   else hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 1>), g, blk, 0, st, A);
@@ -873,6 +881,11 @@ extern "C" int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t stream) {
   A.dbg = 0;
   const int nwg = A.d.N * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg < 128) return 1;
+  if (nwg < g_th8_max_wg) {   // 8-row tiles on a one-round grid (as halo9_launch)
+    A.tiles_y = d->Hs / 8;
+    hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 2, 8>), dim3(2 * nwg), dim3(NT9), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((conv3x3_halo9b<false, 0, 2>), dim3(nwg), dim3(NT9), 0, (hipStream_t)stream, A);
   return (int)hipGetLastError();
 }

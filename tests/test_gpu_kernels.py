@@ -751,6 +751,63 @@ def test_halo_conv_8_row_tiles_match_16_row_tiles(case):
         torch.testing.assert_close(ta, tb, rtol=1e-6, atol=1e-4)
 
 
+@pytest.mark.parametrize("case", ["s2d_pro_stats", "s2d_updgrad", "d2s", "s2d_3d", "d2s_3d"])
+def test_halo_stride2_8_row_tiles_match_16_row_tiles(case):
+    """fmd_conv_s2d / fmd_conv_d2s with 8-row tiles (grids under 1024 workgroups) against the 16-row form on the same
+    problem: outputs bit-identical, statistics equal as per-sample totals."""
+    from fmdiff import _lib
+    O = ops()
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(101)
+    d3 = case.endswith("_3d")
+    kw = {}
+    if case.startswith("s2d_pro") or case == "s2d_3d":
+        N, C, K = (2 if d3 else 8), 64, 128
+        sp = (8, 128, 128) if d3 else (128, 128)
+        x = (_rand_ndhwc(N, *sp, C, 102) if d3 else _rand_nhwc(N, *sp, C, 102)).to(DEV)
+        w = torch.randn(K, C, *([3] * len(sp)), generator=g) / math.sqrt(C * 27)
+        tiled = O.s2d_tile_weights(w.to(DEV), 0)
+        if not d3:
+            kw["pro"] = ((torch.rand(N, C, generator=g) + 0.5).to(DEV), (torch.randn(N, C, generator=g) * 0.2).to(DEV),
+                         True)
+
+        def run():
+            return O.conv(x, K, None, ks=3, stride=2, pad=1, bias=(torch.ones(K) * 0.1).to(DEV), want_stats=True,
+                          s2d_tiled=tiled, **kw)
+    elif case == "s2d_updgrad":
+        N, Cin, K, Hl = 8, 128, 64, 64
+        w = torch.randn(K, Cin, 3, 3, generator=g) / math.sqrt(Cin * 9)
+        dy = _rand_nhwc(N, 2 * Hl, 2 * Hl, K, 103).to(DEV)
+        tiled = O.s2d_tile_weights(w.to(DEV), 1)
+
+        def run():
+            return O.conv(dy, Cin, None, ks=4, stride=2, pad=1, out_hw_=(Hl, Hl), s2d_tiled=tiled)
+    else:
+        N, C, K = (1 if d3 else 8), 128, 128
+        sp = (8, 64, 64) if d3 else (64, 64)
+        w = torch.randn(K, C, *([3] * len(sp)), generator=g) / math.sqrt(C * 27)
+        dy = (_rand_ndhwc(N, *[v // 2 for v in sp], K, 104) if d3 else _rand_nhwc(N, *[v // 2 for v in sp], K, 104)).to(DEV)
+        tiled = O.s2d_tile_weights(w.to(DEV), 2)
+
+        def run():
+            return O.conv(dy, C, None, ks=3, stride=2, pad=1, transposed=True, out_hw_=sp, s2d_tiled=tiled)
+    res = []
+    try:
+        for lim in (1 << 30, 0):
+            L.fmd_halo_set_th8_max_workgroups(lim)
+            out, st = run()
+            torch.cuda.synchronize()
+            res.append((out.clone(), None if st is None else st.slab.clone()))
+    finally:
+        L.fmd_halo_set_th8_max_workgroups(1024)
+    assert torch.equal(res[0][0], res[1][0])
+    if res[0][1] is not None:
+        Kk = res[0][0].shape[-1]
+        ta = res[0][1].double().view(N, -1, Kk, 2).sum(1)
+        tb = res[1][1].double().view(N, -1, Kk, 2).sum(1)
+        torch.testing.assert_close(ta, tb, rtol=1e-6, atol=1e-4)
+
+
 @pytest.mark.parametrize("case", ["fwd_pro_stats", "dgrad_ep_stats"])
 def test_halo_conv_bench_problem_vs_torch(case):
     """The bench's roofline kernel on the bench's own problem -- non-split conv3x3_halo at 8x256^2, 128 -> 128
