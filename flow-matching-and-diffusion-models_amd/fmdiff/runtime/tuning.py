@@ -21,8 +21,9 @@ TABLE = {
     "S2D_HALO": (1, "stride-2 3x3 forwards / nearest-x2 data gradients on the space-to-depth halo kernel"),
     "S2D_3D": (1, "3-D: the same stride-2 modes with the depth taps as chunks (0: generic implicit GEMM, and the "
                   "nearest-x2 data gradient at full resolution + 2x2x2 box sum)"),
-    "WGRAD_S2D": (1, "stride-2 3x3 (3x3x3) weight gradients on the halo weight-gradient kernel (space-to-depth planes "
-                     "as chunks; 0: the generic weight-gradient kernel)"),
+    "WGRAD_S2D": (1, "2-D stride-2 3x3 weight gradients on the halo weight-gradient kernel (space-to-depth planes as "
+                     "chunks; 0: the generic weight-gradient kernel).  2-D only: 3-D stride-2 weight gradients always "
+                     "run on the generic kernel (fmd_wgrad_halo rejects them)"),
     "POINT_1X1": (1, "ResBlock 3x3 convs on 1x1 images as their centre tap"),
     "GN_FUSED": (1, "small levels: GroupNorm statistics + affine + SiLU operand in one launch"),
     "CONV_GN": (1, "split-K conv1 -> GroupNorm-2 in the split combine (fmd_conv_gn)"),
@@ -45,6 +46,23 @@ TABLE = {
     "WGRAD_GEN_SLAB_MB": (48, "generic weight gradient: split-K slab cap (MB)"),
 }
 
+# the per-switch environment variables this table replaced in round 5 (and earlier retired switches): setting one
+# would silently measure the default, so it raises instead
+RETIRED = sorted({f"FMD_{k}" for k in TABLE} | {
+    "FMD_HALO9", "FMD_HALO10", "FMD_WGRAD9", "FMD_WGRAD_REDUCE", "FMD_WGRAD_REDUCE1", "FMD_WGRAD_PIPE", "FMD_WGRAD_KS",
+    "FMD_SPLITK_FUSE", "FMD_WRED_BATCH", "FMD_SIDE_WGRAD", "FMD_MAT_PRO", "FMD_GOUT", "FMD_CONV_LOG", "FMD_X"})
+
+
+def check_environment(env=None) -> None:
+    """Raise if a retired per-switch FMD_* variable is set (use FMD_TUNE=NAME=value instead)."""
+    env = os.environ if env is None else env
+    stale = [k for k in RETIRED if k in env]
+    if stale:
+        raise ValueError(f"retired environment switch(es) {', '.join(stale)}: the runtime no longer reads them; use "
+                         f"FMD_TUNE=\"NAME=value,...\" with the names of fmdiff/runtime/tuning.py TABLE")
+
+
+check_environment()
 _over = {}
 for _item in filter(None, (s.strip() for s in os.environ.get("FMD_TUNE", "").split(","))):
     _k, _, _v = _item.partition("=")

@@ -155,7 +155,10 @@ def test_config_e_full_size_halo_path_vs_generic_path(golden_e, monkeypatch):
     res = {}
     for path in ("halo", "generic"):
         if path == "generic":
+            # every conv on the generic implicit GEMM: the depth-tap halo convs AND the 3-D stride-2 s2d / d2s halo
+            # modes (DownsampleND forward, its data gradient, the nearest-x2 data gradient)
             monkeypatch.setattr(E, "DEPTH_HALO", False)
+            monkeypatch.setattr(E, "S2D_3D", False)
             wgrad = ops.wgrad
 
             def wgrad_generic(*a, **k):

@@ -287,6 +287,14 @@ def test_tuning_table_and_override(monkeypatch):
         monkeypatch.setenv("FMD_TUNE", "HALO_MIN_WGS=64")
         with pytest.raises(ValueError):
             importlib.reload(tuning)
+        monkeypatch.delenv("FMD_TUNE")
+        # a retired per-switch variable (round-4 A/B scripts set these) raises instead of measuring the default
+        for stale in ("FMD_HALO_MIN_WG", "FMD_WGRAD_REDUCE", "FMD_HALO9"):
+            monkeypatch.setenv(stale, "1")
+            with pytest.raises(ValueError, match=stale):
+                importlib.reload(tuning)
+            monkeypatch.delenv(stale)
+        tuning.check_environment({"FMD_LIB": "x", "FMD_TUNE": ""})   # the two live variables pass
     finally:
         monkeypatch.delenv("FMD_TUNE", raising=False)
         importlib.reload(tuning)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box helper: A/B of train-step env switches.  usage: AB="FMD_X=0 FMD_X=1 ..." bash tools/ab_env.sh
+# GPU-box helper: A/B of train-step env switches.  usage: AB="FMD_TUNE=HALO_MIN_WG=32 FMD_TUNE=HALO_MIN_WG=64 ..." bash tools/ab_env.sh
 # Runs the wgrad / train-step GPU tests once, then one bench per setting (train only, no CPU baseline).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box helper: config D probe per env setting.  usage: AB="FMD_X=0 FMD_X=1" bash tools/ab_latent.sh
+# GPU-box helper: config D probe per env setting.  usage: AB="FMD_TUNE=CONV_GN=0 FMD_TUNE=CONV_GN=1" bash tools/ab_latent.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box helper: rocprofv3 kernel traces of a short train bench under two env settings (this tree).
-# usage: A="FMD_X=1" B="FMD_X=0" bash tools/ab_prof_env.sh   -> gpurun_out/abpe_A, gpurun_out/abpe_B
+# usage: A="FMD_TUNE=CONV_GN=1" B="FMD_TUNE=CONV_GN=0" bash tools/ab_prof_env.sh   -> gpurun_out/abpe_A, gpurun_out/abpe_B
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box helper: rocprofv3 kernel stats of the config D probe under two env settings.
-# usage: A="FMD_X=1" B="FMD_X=0" bash tools/ab_prof_latent.sh   -> gpurun_out/abpl_A, gpurun_out/abpl_B
+# usage: A="FMD_TUNE=CONV_GN=1" B="FMD_TUNE=CONV_GN=0" bash tools/ab_prof_latent.sh   -> gpurun_out/abpl_A, gpurun_out/abpl_B
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
