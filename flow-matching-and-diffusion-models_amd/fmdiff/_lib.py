@@ -56,6 +56,18 @@ class GnOutDesc(C.Structure):
                 ("emb_mode", i32), ("silu", i32), ("a", p), ("b", p), ("mean_rstd", p), ("t", p)]
 
 
+class ConvSmallDesc(C.Structure):
+    """Mirror of ``fmd_conv_small_desc``."""
+    _fields_ = [
+        ("N", i32), ("Hs", i32), ("Ws", i32), ("C0", i32), ("C1", i32), ("Ho", i32), ("Wo", i32), ("K", i32),
+        ("mode", i32), ("src0", p), ("src1", p), ("wgt", p), ("st0", p), ("rows0", i32), ("st1", p), ("rows1", i32),
+        ("G", i32), ("eps", f32), ("gamma", p), ("beta", p), ("emb", p), ("emb_stride", i32), ("silu", i32),
+        ("src2", p), ("src3", p), ("C2", i32), ("C3", i32), ("wgt2", p), ("bias", p), ("bias2", p), ("bias_nc", p),
+        ("bias_nc_stride", i32), ("resid", p),
+        ("out", p), ("stats", p), ("part", p), ("part_bytes", i64), ("tickets", p), ("n_tickets", i32), ("split", i32),
+    ]
+
+
 LINCOMB_MAX = 6   # FMD_LINCOMB_MAX
 
 
@@ -94,6 +106,9 @@ SIGNATURES = {
     "fmd_tile_weights_halo": [p, i32, i32, i32, p, p],
     "fmd_conv_s2d": [C.POINTER(ConvDesc), p],
     "fmd_conv_d2s": [C.POINTER(ConvDesc), p],
+    "fmd_conv_small_plan": [C.POINTER(ConvSmallDesc)],
+    "fmd_conv_small_split": [C.POINTER(ConvSmallDesc)],
+    "fmd_conv_small": [C.POINTER(ConvSmallDesc), p],
     "fmd_s2d_tiled_size": [i32, i32, i32],
     "fmd_s2d_tile_weights": [p, i32, i32, i32, i32, p, p],
     "fmd_s2d_tiled_size_nd": [i32, i32, i32, i32, i32],

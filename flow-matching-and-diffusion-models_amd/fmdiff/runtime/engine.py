@@ -381,6 +381,14 @@ class UNetEngine:
         _check_conv(conv, 3, stride, 1)
         Cin = x.C
         N_, sp = x.t.shape[0], tuple(x.t.shape[1:-1])
+        if (ctx.tape is None and len(sp) == 2 and not self.dims1 and conv.weight.dim() == 4 and
+                conv.weight.shape[1] == Cin):
+            # forward only, small level: one launch with the output statistics (fmd_conv_small)
+            mode = "s2" if stride == 2 else "up" if upsample else "s1"
+            if ops.conv_small_ok(tuple(x.t.shape), conv.out_channels, mode=mode):
+                out, st = ops.conv_small(x.t, conv.out_channels, self.wc.get(conv.weight, 0), mode=mode,
+                                         bias=conv.bias)
+                return Act(out, st)
         Ho_ = ops.out_hw(sp[0], 3, stride, 1, upsample)
         if len(sp) == 2:
             halo = stride == 1 and ops.halo_eligible(N_, sp[0], Ho_, ops.out_hw(sp[1], 3, stride, 1, upsample),
@@ -604,6 +612,10 @@ class UNetEngine:
             es = eo.shape[1]
         else:   # the embedding projection feeds nothing (or the block has none: VAE ResBlocks)
             eo, es = None, 0
+        if ctx.tape is None and not drop and len(sp) == 2 and not self.dims1:
+            o = self._res_block_small(m, x0, x1, eo, es, ss, add)
+            if o is not None:
+                return o
         halo1 = self._halo_ok(N, sp, Cout, Cin, pro=True)
         mat1 = _materialise(halo1, x1, Cin, HW, len(sp) == 3)
         if mat1 and not halo1:   # without the fused prologue the halo kernel's affine-table limit is moot
@@ -740,6 +752,55 @@ class UNetEngine:
                                in_silu=m.emb_activation_before_proj)
         ctx.tape.append(bwd)
         return o
+
+    def _res_block_small(self, m: ResBlockND, x0: Act, x1: Optional[Act], eo, es, ss: bool, add: bool):
+        """Forward-only ResBlockND on a small level in TWO launches (fmd_conv_small, csrc/conv_small.hip): conv1 folds
+        GroupNorm-1 from the inputs' statistics slabs, applies it + SiLU while staging, adds the conv bias and the
+        time-embedding (add form); conv2 folds GroupNorm-2 (+ the scale-shift embedding) from conv1's statistics and
+        adds its bias and the identity residual or the 1x1 skip conv over the block input.  Both emit the statistics
+        of their outputs for the next GroupNorm.  Reference: residual.py:84-120.  Returns None (caller takes the
+        general path) when either conv does not qualify."""
+        N, H, W, C0 = x0.t.shape
+        C1 = x1.C if x1 is not None else 0
+        Cout = m.out_channels
+        c1, c2 = m.conv1.conv, m.conv2.conv
+        if c1.weight.dim() != 4 or c2.weight.dim() != 4:
+            return None
+        _check_conv(c1, 3, 1, 1)
+        _check_conv(c2, 3, 1, 1)
+        point = POINT_1X1 and (H, W) == (1, 1)
+        mode = "point" if point else "s1"
+        g1, g2 = m.norm1, m.norm2
+        sk = m.skip_connection
+        ident = isinstance(sk, Identity)
+        if ident and x1 is not None:
+            raise ValueError("identity skip with concatenated input")
+        if not ident:
+            _check_conv(sk.conv, 1, 1, 0)
+        rows = 64 if (H * W) % 64 == 0 else H * W   # the slab rows fmd_channel_stats / fmd_conv_small write
+
+        def probe(a):
+            return a.stats if a.stats is not None else ops.Stats(None, rows)
+        gn1 = dict(st0=probe(x0), st1=probe(x1) if x1 is not None else None, groups=g1.num_groups, eps=g1.eps)
+        gn2 = dict(st0=ops.Stats(None, rows), groups=g2.num_groups, eps=g2.eps, emb=eo if ss else None,
+                   emb_stride=es if ss else 0)
+        if not (ops.conv_small_ok((N, H, W, C0), Cout, C1=C1, mode=mode, gn=gn1) and
+                ops.conv_small_ok((N, H, W, Cout), Cout, mode=mode, gn=gn2, skip=None if ident else (C0, C1))):
+            return None
+        gn1.update(st0=_stats(x0), st1=_stats(x1), gamma=g1.weight, beta=g1.bias)
+        w1 = self.wc.get(self.wc.center(c1.weight), 0) if point else self.wc.get(c1.weight, 0)
+        h, hst = ops.conv_small(x0.t, Cout, w1, src1=x1.t if x1 is not None else None, mode=mode, gn=gn1,
+                                bias=c1.bias, bias_nc=eo if add else None)
+        gn2.update(st0=hst, gamma=g2.weight, beta=g2.bias)
+        w2 = self.wc.get(self.wc.center(c2.weight), 0) if point else self.wc.get(c2.weight, 0)
+        kw = {}
+        if ident:
+            kw["resid"] = x0.t
+        else:
+            kw.update(src2=x0.t, src3=x1.t if x1 is not None else None, skip_wgt=self.wc.get(sk.conv.weight, 0),
+                      bias2=sk.conv.bias)
+        out, ost = ops.conv_small(h, Cout, w2, mode=mode, gn=gn2, bias=c2.bias, **kw)
+        return Act(out, ost)
 
     def _dropout_seed(self, m, ctx: Ctx, dev):
         """(device seed counter, per-block salt) for ResBlockND dropout; the counter advances once per forward

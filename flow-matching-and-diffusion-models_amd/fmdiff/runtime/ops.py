@@ -487,6 +487,123 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     return out, st
 
 
+CONV_SMALL_MODES = {"s1": 0, "s2": 1, "up": 2, "point": 3}
+# forward-only small levels in one launch per conv (fmd_conv_small, runtime/tuning.py SMALL_CONV / SMALL_CONV_MAX_HW)
+SMALL_CONV = bool(tuning.get("SMALL_CONV"))
+SMALL_CONV_MAX_HW = tuning.get("SMALL_CONV_MAX_HW")
+SMALL_CONV_SPLIT = tuning.get("SMALL_CONV_SPLIT")
+# the in-launch combine of a split reduction: fp32 partial tiles + arrival tickets, one set per (device, stream) --
+# launches on one stream serialise, so they can share it; the tickets start at zero and every launch leaves them so
+SMALL_PART_BYTES = 8 << 20
+SMALL_TICKETS = 4096
+_small_ws = {}
+
+
+def _small_workspace(dev):
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    ws = _small_ws.get(key)
+    if ws is None:
+        ws = (torch.empty(SMALL_PART_BYTES // 4, device=dev, dtype=F32),
+              torch.zeros(SMALL_TICKETS, device=dev, dtype=torch.int32))
+        _small_ws[key] = ws
+    return ws
+
+
+def _conv_small_desc(shape0, C1, K, mode, gn, skip, ptrs, split=None):
+    """fmd_conv_small_desc for input shape ``shape0`` = (N, Hs, Ws, C0) (+ C1 concat channels).  ``ptrs``: dict of
+    device pointers (a host-only plan query passes placeholders)."""
+    from .._lib import ConvSmallDesc
+    N, Hs, Ws, C0 = shape0
+    m = CONV_SMALL_MODES[mode]
+    Ho, Wo = (Hs // 2, Ws // 2) if m == 1 else (2 * Hs, 2 * Ws) if m == 2 else (Hs, Ws)
+    d = ConvSmallDesc()
+    d.N, d.Hs, d.Ws, d.C0, d.C1, d.Ho, d.Wo, d.K, d.mode = N, Hs, Ws, C0, C1, Ho, Wo, K, m
+    d.src0, d.src1, d.wgt, d.out = ptrs["src0"], ptrs.get("src1"), ptrs["wgt"], ptrs["out"]
+    if gn is not None:
+        d.st0, d.rows0 = ptrs["st0"], gn["st0"].rows
+        if gn.get("st1") is not None:
+            d.st1, d.rows1 = ptrs["st1"], gn["st1"].rows
+        d.G, d.eps = gn["groups"], float(gn["eps"])
+        d.gamma, d.beta, d.emb = ptrs.get("gamma"), ptrs.get("beta"), ptrs.get("emb")
+        emb = gn.get("emb")
+        d.emb_stride = (gn.get("emb_stride") or emb.shape[-1]) if emb is not None else 0
+        d.silu = int(gn.get("silu", True))
+    if skip:   # (C2, C3): channels of the raw 1x1-segment sources at the output pixels
+        d.C2, d.C3 = skip
+        d.src2, d.src3, d.wgt2 = ptrs["src2"], ptrs.get("src3"), ptrs["wgt2"]
+    d.split = SMALL_CONV_SPLIT if split is None else split
+    if d.split != 1:
+        d.part, d.part_bytes, d.tickets, d.n_tickets = ptrs["part"], SMALL_PART_BYTES, ptrs["tickets"], SMALL_TICKETS
+    return d, (N, Ho, Wo)
+
+
+def _conv_small_query(fn, shape0, K, C1, mode, gn, skip, split):
+    fake = dict(src0=16, src1=16 if C1 else None, wgt=16, out=16, st0=16, st1=16, wgt2=16, src2=16,
+                src3=16 if skip and skip[1] else None, part=16, tickets=16)
+    d, _ = _conv_small_desc(tuple(shape0), C1, K, mode, gn, skip, fake, split)
+    return int(getattr(_lib.lib(), fn)(C.byref(d)))
+
+
+def conv_small_ok(shape0, K, *, C1=0, mode="s1", gn=None, skip=None, split=None) -> bool:
+    """Whether fmd_conv_small takes the problem on input shape ``shape0`` = (N, Hs, Ws, C0) (fmd_conv_small_plan:
+    geometry, channel counts, one CU's LDS; a host-side query, nothing is launched), within the SMALL_CONV switches.
+    ``skip``: (C2, C3) channels of a 1x1 segment's sources, or None.  ``split``: parts of the reduction (None:
+    SMALL_CONV_SPLIT; 0 the plan's choice, 1 none)."""
+    if not SMALL_CONV or len(shape0) != 4 or K % 16:
+        return False
+    m = CONV_SMALL_MODES[mode]
+    HWo = shape0[1] * shape0[2] * (4 if m == 2 else 1) // (4 if m == 1 else 1)
+    if HWo > SMALL_CONV_MAX_HW:
+        return False
+    return _conv_small_query("fmd_conv_small_plan", shape0, K, C1, mode, gn, skip, split) > 0
+
+
+def conv_small_split(shape0, K, *, C1=0, mode="s1", gn=None, skip=None, split=None) -> int:
+    """The parts fmd_conv_small splits the reduction of this problem into (fmd_conv_small_split; host-side)."""
+    return _conv_small_query("fmd_conv_small_split", shape0, K, C1, mode, gn, skip, split)
+
+
+def conv_small(src0, K, wgt, *, src1=None, mode="s1", gn=None, src2=None, src3=None, skip_wgt=None, bias=None,
+               bias2=None, bias_nc=None, resid=None, out=None, want_stats=True,
+               split=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+    """One-launch small-level conv (fmd_conv_small, csrc/conv_small.hip; forward only).
+
+    ``mode``: "s1" 3x3 stride 1, "s2" 3x3 stride 2 (DownsampleND), "up" nearest-x2 + 3x3 (UpsampleND), "point" 1x1
+    (the centre tap of a 3x3 on 1x1 images).  ``wgt``: fmd_prep_weights mode-0 layout [K][T][C0 + C1].
+    ``gn``: GroupNorm(+scale/shift)+SiLU prologue folded from the inputs' statistics:
+    dict(st0=Stats, st1=Stats or None, groups, eps, gamma, beta[, emb, emb_stride, silu]).  ``src2`` | ``src3``,
+    ``skip_wgt`` (bf16 [K][1][C2 + C3]): a 1x1 conv over raw tensors at the output resolution (the ResBlock skip
+    connection over the block input).  ``bias_nc``: [N][>=K] per-sample bias
+    (row stride taken from the tensor).  Returns (out, Stats of the bf16 output: 64-pixel rows, or one row per
+    image when Ho*Wo < 64).  ``split``: parts of the reduction, combined inside the launch (None: SMALL_CONV_SPLIT;
+    0 the plan's choice -- enough workgroups for the chip --, 1 none, 2..16 forced)."""
+    _need_cuda(src0, "conv_small")
+    C1 = src1.shape[-1] if src1 is not None else 0
+    ptrs = dict(src0=_p(src0), src1=_p(src1), wgt=_p(wgt), out=_p(out), wgt2=_p(skip_wgt), src2=_p(src2),
+                src3=_p(src3))
+    if gn is not None:
+        ptrs.update(st0=_p(gn["st0"].slab), st1=_p(gn["st1"].slab) if gn.get("st1") is not None else None,
+                    gamma=_p(gn.get("gamma")), beta=_p(gn.get("beta")), emb=_p(gn.get("emb")))
+    skip = (src2.shape[-1], src3.shape[-1] if src3 is not None else 0) if skip_wgt is not None else None
+    part, tickets = _small_workspace(src0.device)
+    ptrs.update(part=_p(part), tickets=_p(tickets))
+    d, (N, Ho, Wo) = _conv_small_desc(tuple(src0.shape), C1, K, mode, gn, skip, ptrs, split)
+    d.bias, d.bias2, d.resid = _p(bias), _p(bias2), _p(resid)
+    if bias_nc is not None:
+        d.bias_nc, d.bias_nc_stride = _p(bias_nc), bias_nc.stride(0)
+    if out is None:
+        out = torch.empty((N, Ho, Wo, K), device=src0.device, dtype=BF16)
+        d.out = _p(out)
+    st = None
+    if want_stats:
+        rows = 64 if (Ho * Wo) % 64 == 0 else Ho * Wo
+        slab = torch.empty((N * Ho * Wo // rows, K, 2), device=src0.device, dtype=F32)
+        d.stats = _p(slab)
+        st = Stats(slab, rows)
+    _lib.call("fmd_conv_small", C.byref(d), stream())
+    return out, st
+
+
 def conv_combine(ws, K, out_shape, *, bias=None, bias2=None, bias_nc=None, resid=None, ep=None, out=None,
                  accumulate=False, want_stats=False):
     """out (bf16, N-D ``out_shape`` = (N, *sp)) = sum of the fp32 slabs ws [S][M][K] + conv epilogue

@@ -181,6 +181,62 @@ int64_t fmd_s2d_tiled_size_nd(int32_t K, int32_t C, int32_t mode, int32_t ks, in
 int fmd_s2d_tile_weights_nd(const float* w, int32_t K, int32_t C, int32_t ks, int32_t mode, int32_t dims, void* out,
                             fmd_stream_t s);
 
+/* Small-level conv in ONE launch (csrc/conv_small.hip): the sampler's low-resolution levels, where the split-K
+ * implicit GEMM needed a combine launch and a GroupNorm launch beside every conv.  A workgroup owns up to 64 output
+ * pixels (64-pixel blocks of one image, or whole images when Ho*Wo < 64) x 16 output channels and the FULL reduction:
+ * the input rows its taps read (all C = C0 + C1 channels) are staged once in LDS with the GroupNorm affine
+ * (+ scale/shift) + SiLU applied -- the affine folded in-kernel from the producers' statistics slabs -- and eight
+ * waves split the 32-channel chunks, combining in LDS in a fixed order.  Replaces, per conv, ResBlockND's
+ * GroupNorm(+scale/shift)+SiLU -> ConvND 3x3 (src/nn/blocks/residual.py:84-120, normalization.py:11-19,
+ * convolution.py:8-54) with the time-embedding add, the 1x1 skip conv + residual add (residual.py:77-82, 120),
+ * DownsampleND's stride-2 conv and UpsampleND's nearest-x2 + conv (upsampling.py:8-62), and emits the per-channel
+ * statistics the next GroupNorm folds.  Forward only (no saved affine for a backward). */
+typedef struct fmd_conv_small_desc {
+  int32_t N, Hs, Ws, C0, C1; /* input bf16 NHWC [N][Hs][Ws][C0] (+ [N][Hs][Ws][C1], virtual concat) */
+  int32_t Ho, Wo, K;         /* output bf16 NHWC [N][Ho][Wo][K] */
+  int32_t mode;              /* 0: 3x3 stride 1 pad 1; 1: 3x3 stride 2 pad 1; 2: nearest-x2 gather, 3x3 s1 p1;
+                                3: 1x1 (the centre tap of a 3x3 on 1x1 images) */
+  const void* src0;
+  const void* src1;
+  const void* wgt;           /* bf16 [K][T][C0 + C1], T = 9 (modes 0-2) or 1: fmd_prep_weights mode 0 */
+  const float* st0;          /* GroupNorm prologue when non-NULL: statistics slab of src0 [N*Hs*Ws/rows0][C0][2] */
+  int32_t rows0;             /*   (sum, sum of squares per rows0-pixel block of one image) */
+  const float* st1;          /* ... of src1 (C1 > 0) */
+  int32_t rows1;
+  int32_t G;                 /* groups */
+  float eps;
+  const float* gamma;        /* [C0 + C1] or NULL */
+  const float* beta;
+  const float* emb;          /* scale-shift norm: [N][emb_stride] scale | shift, or NULL */
+  int32_t emb_stride;
+  int32_t silu;              /* SiLU after the affine */
+  const void* src2;          /* 1x1 segment (ResBlock skip conv) over raw (src2 | src3) at the OUTPUT pixels, */
+  const void* src3;          /*   bf16 [N][Ho][Wo][C2] (+ [N][Ho][Wo][C3]); C2 = 0: none (modes 0 and 3 only) */
+  int32_t C2, C3;
+  const void* wgt2;          /* bf16 [K][C2 + C3] */
+  const float* bias;         /* [K] or NULL */
+  const float* bias2;        /* [K] or NULL (skip-conv bias) */
+  const float* bias_nc;      /* per-sample bias [N][bias_nc_stride] (time-embedding add) or NULL */
+  int32_t bias_nc_stride;    /* 0: K */
+  const void* resid;         /* bf16 [N][Ho][Wo][K] or NULL */
+  void* out;
+  float* stats;              /* NULL or [N*Ho*Wo/srows][K][2] of the bf16 outputs, srows = 64 if Ho*Wo % 64 == 0
+                                else Ho*Wo (one row per image) */
+  float* part;               /* split of the reduction over input channels (grids smaller than the chip): fp32
+                                partial tiles, part_bytes bytes; NULL: no split */
+  int64_t part_bytes;
+  uint32_t* tickets;         /* [n_tickets] arrival counters of the in-launch combine: zero before first use, left
+                                zero by every completed launch; one set per stream (launches on it serialise) */
+  int32_t n_tickets;
+  int32_t split;             /* parts: 0 chosen by the plan (enough workgroups for the chip), 1 none, 2..16 forced */
+} fmd_conv_small_desc;
+/* LDS bytes the launch needs (> 0), or a negative code when the problem does not qualify (geometry, channel
+ * counts, or more than one CU's LDS). */
+int fmd_conv_small_plan(const fmd_conv_small_desc* d);
+/* The number of parts the plan splits the reduction into (>= 1), or the plan's negative code. */
+int fmd_conv_small_split(const fmd_conv_small_desc* d);
+int fmd_conv_small(const fmd_conv_small_desc* d, fmd_stream_t s);
+
 /* UNet output head: out = conv3x3(SiLU(a*h + b)) to K <= 8 channels, fp32 NHWC [N][H][W][8]
  * (channels >= K zero), replacing the final GroupNorm -> SiLU -> ConvND of
  * src/models/unet/unet.py:286-293 (unet_diffusers_nd.py conv_norm_out/conv_act/conv_out).

@@ -47,6 +47,7 @@ def test_struct_mirrors_match_header_field_order():
     src = open(HEADER).read()
     for cname, py in (("fmd_conv_desc", _lib.ConvDesc), ("fmd_wgrad_desc", _lib.WgradDesc),
                       ("fmd_gn_apply_desc", _lib.GnApplyDesc), ("fmd_gb_job", _lib.GbJob),
+                      ("fmd_conv_small_desc", _lib.ConvSmallDesc),
                       ("fmd_lincomb_desc", _lib.LincombDesc)):
         m = re.search(r"typedef\s+struct\s*(?:\w+\s*)?\{([^{}]*)\}\s*" + cname + r"\s*;", src, flags=re.S)
         assert m, cname

@@ -24,8 +24,10 @@ def _rel(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
-@pytest.mark.parametrize("use_graph", [True, False])
-def test_latent_flow_sample_vs_oracle_composition(use_graph):
+@pytest.mark.parametrize("use_graph,small_conv", [(True, False), (False, False), (True, True)])
+def test_latent_flow_sample_vs_oracle_composition(use_graph, small_conv, monkeypatch):
+    """small_conv: the sampler's no-tape UNet evaluations through fmd_conv_small where the plan takes the level
+    (runtime/ops.py SMALL_CONV), against the same oracle composition."""
     from fmdiff.models.generators import DiffusionUNetFactory
     from fmdiff.models.vae import AutoencoderKL
     from fmdiff.pipelines.latent import latent_flow_sample
@@ -35,6 +37,8 @@ def test_latent_flow_sample_vs_oracle_composition(use_graph):
     from oracle import train_step as OT
     from oracle import unet as U
     from oracle import vae as V
+    from fmdiff.runtime import ops
+    monkeypatch.setattr(ops, "SMALL_CONV", small_conv)
     G = torch.load(os.path.join(REPO, "tests", "golden", "vae_golden.pt"), weights_only=True)
     vcfg = json.loads(bytes(G["cfg_json"].tolist()).decode())
     with warnings.catch_warnings():
@@ -60,6 +64,6 @@ def test_latent_flow_sample_vs_oracle_composition(use_graph):
         lat = OT.sample(sd, spec, OS.FlowMatchEuler(1000, 1.0), steps, noise, cond=mode)
         ref = (V.decode(G["state"], vcfg, lat).clamp(-1.0, 1.0) + 1.0) * 0.5
     err = _rel(got, ref)
-    print(f"latent_flow_sample graph={use_graph}: decoded rel L2 {err:.3e}")
+    print(f"latent_flow_sample graph={use_graph} small_conv={small_conv}: decoded rel L2 {err:.3e}")
     assert got.shape == ref.shape
     assert err < 3e-2

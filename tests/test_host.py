@@ -299,3 +299,37 @@ def test_tuning_table_and_override(monkeypatch):
         monkeypatch.delenv("FMD_TUNE", raising=False)
         importlib.reload(tuning)
     assert not tuning._over
+
+
+def test_conv_small_plan_is_a_host_query(monkeypatch):
+    """fmd_conv_small_plan (csrc/conv_small.hip) decides eligibility on the host without a launch: the config-D latent
+    UNet's small-level problems are taken, out-of-range ones refused (LDS, channel multiples, tile geometry)."""
+    from fmdiff import _lib
+    from fmdiff.runtime import ops
+    try:
+        _lib.lib()
+    except (OSError, RuntimeError) as e:
+        pytest.skip(f"library not loadable here: {e}")
+    monkeypatch.setattr(ops, "SMALL_CONV", True)
+    st64, st16 = ops.Stats(None, 64), ops.Stats(None, 16)
+    gn = dict(st0=st64, st1=st64, groups=32, eps=1e-6)
+    assert ops.conv_small_ok((8, 16, 16, 256), 128, C1=128, gn=gn, skip=(256, 128))      # 16^2 decoder concat
+    assert ops.conv_small_ok((8, 4, 4, 512), 256, C1=256, gn=dict(gn, st0=st16, st1=st16), skip=(512, 256))
+    assert ops.conv_small_ok((8, 1, 1, 512), 512, C1=512, mode="point", gn=dict(gn, st0=ops.Stats(None, 1),
+                                                                                 st1=ops.Stats(None, 1)), skip=(512, 512))
+    assert ops.conv_small_ok((8, 32, 32, 128), 128, mode="s2")
+    assert not ops.conv_small_ok((8, 8, 8, 32), 64)          # C < 64
+    assert not ops.conv_small_ok((8, 8, 8, 64), 24)          # K % 16
+    assert not ops.conv_small_ok((8, 8, 12, 64), 64)         # Ho*Wo neither a multiple nor a divisor of 64
+    assert not ops.conv_small_ok((1, 16, 16, 2048), 64, split=1)   # more than one CU's LDS unsplit ...
+    assert ops.conv_small_ok((1, 16, 16, 2048), 64)               # ... fits as parts of the reduction
+    assert not ops.conv_small_ok((8, 64, 64, 128), 128)      # above SMALL_CONV_MAX_HW
+    # the in-launch split: parts until the grid has 256 workgroups, whole GroupNorm groups and >= 64 channels per
+    # part; none where the grid already fills the chip; forced values validated
+    gn2 = dict(gn, st0=ops.Stats(None, 4), st1=ops.Stats(None, 4))
+    assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=0) == 8        # 32 tiles -> 256
+    assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=1) == 1
+    assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=4) == 4
+    assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=3) < 0         # not a power of two
+    assert ops.conv_small_split((8, 32, 32, 128), 128, mode="s2", split=0) == 2             # 128 tiles -> 256
+    assert ops.conv_small_split((8, 16, 16, 128), 128, C1=128, gn=gn, skip=(128, 128), split=0) == 2
