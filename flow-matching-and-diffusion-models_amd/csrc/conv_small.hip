@@ -1,32 +1,42 @@
 // Small-level convolution in one launch (fmd_conv_small): the sampler's low-resolution UNet levels.
 //
-// Why: at 32^2 ... 1^2 a conv moves a few MB and its MFMA work is a few microseconds of one CU,
+// Why: at 16^2 ... 1^2 a conv moves a few MB and its MFMA work is a few microseconds of one CU,
 // so the split-K implicit GEMM of csrc/conv.hip spent its time at the ~5 us launch floor three or four times per conv
-// (main launch, split-K combine, GroupNorm statistics / affine, materialised GN+SiLU operand).  Here one workgroup
-// does a whole output tile with the FULL reduction and no separate GroupNorm pass:
+// (main launch, split-K combine, GroupNorm statistics / affine, materialised GN+SiLU operand).  Here one launch does
+// it all:
 //
 // * tile = up to 64 output pixels (a 64-pixel block of one image: 64 / Wo rows, or S whole images when Ho*Wo < 64)
-//   x 16 output channels; 512 threads = 8 waves, one workgroup per CU (LDS up to 160 KiB);
-// * prologue: the GroupNorm affine of every input channel of the tile's images is folded in-kernel from the
-//   producers' statistics slabs (sum, sum of squares per pixel block; the E[x^2] - mean^2 form of gn_prep, groups in
-//   fp64), with the scale-shift embedding folded in;
-// * staging: the input rows the tile's taps read -- all C0 + C1 channels (virtual concat) -- are loaded once, with
-//   every load issued before any wait, transformed (affine + SiLU, once per element) and stored to LDS as
-//   [pixel slot][C] rows with a 16-byte-chunk XOR swizzle (conflict-free ds_read_b128 fragments); a zero slot serves
-//   every padding tap; the raw input at the tile's pixels is kept beside it for the 1x1 skip segment;
-// * main loop: waves split the 32-channel chunks (and, when there are fewer than 8 chunks, the 16-pixel row blocks);
-//   per chunk 9 taps (1 for mode 3) x row blocks of v_mfma_f32_16x16x32_bf16 with A = weights (16 couts, from
-//   global/L2, the next chunk's fragments in flight) and B = the staged pixels;
-// * epilogue: the waves' partial tiles meet in LDS in a fixed order (deterministic), + bias / skip bias / per-sample
-//   bias / residual, bf16 16-byte stores, and the per-channel statistics of the rounded outputs (the slab rows the
-//   consumer's GroupNorm folds: 64-pixel rows, or one row per image).
+//   x 16 or 32 output channels; 512 threads = 8 waves, one workgroup per CU (LDS up to 160 KiB).  Where that leaves
+//   fewer than 256 workgroups the reduction (input channels, whole GroupNorm groups) is split into P parts, one
+//   workgroup each, combined inside the launch (below);
+// * prologue: every global operand is in flight at once -- the wave's weight fragments (buffer loads straight into
+//   registers, branch-free), and by LDS-DMA the input rows the tile's taps read (the part's channels of the virtual
+//   concat C0 | C1, [pixel slot][channel] rows with a 16-byte-chunk XOR swizzle), the raw 1x1-segment input, the
+//   producers' GroupNorm statistics slab rows, gamma / beta / scale-shift rows and the epilogue operands;
+// * GroupNorm: the affine of every input channel folded from the statistics (E[x^2] - mean^2, group sums in fp64 by
+//   a butterfly over the group's lanes), the scale-shift embedding folded in; applied + SiLU in place in LDS;
+// * main loop: waves split the 32-channel chunks (and the 16-pixel row blocks); per chunk 9 taps (1 for mode 3) x
+//   row blocks of v_mfma_f32_16x16x32_bf16, A = weights (registers), B = the staged pixels (ds_read_b128);
+// * epilogue: the waves' partial tiles meet in LDS in a fixed order (deterministic); with P > 1 every part stores its
+//   fp32 tile write-through (sc1) and takes a ticket, the last part sums all P in part order (the result does not
+//   depend on arrival order); + bias / skip bias / per-sample bias / residual, bf16 16-byte stores, and the
+//   per-channel statistics of the rounded outputs (the slab rows the consumer's GroupNorm folds).
+//
+// Measured: each workgroup's phases are latency chains of a few microseconds each, so a launch
+// costs ~15 us whatever its size; it replaces three to four launches at the ~5 us floor.
 #include <cstdlib>
 #include "common.h"
 #include "../../include/fmdiff.h"
 
 namespace {
 
-constexpr int NT = 512;
+#ifndef FMD_SMALL_NT
+#define FMD_SMALL_NT 512
+#endif
+// 8 waves per workgroup, one workgroup per CU.  -DFMD_SMALL_NT=256 builds 4-wave workgroups, two per CU where the
+// LDS plan allows, whose phases run out of step: measured no better on the latent UNet
+constexpr int NT = FMD_SMALL_NT;
+constexpr int NW = NT / 64;
 constexpr int TPX = 64;    // output pixels per tile
 constexpr int LDS_MAX = 160 * 1024;
 
@@ -96,7 +106,7 @@ extern "C" int fmd_debug_small_ts(void* host, int nblocks, int clear) {
 FMD_DEV int swz(int c16, int slot, int cmask) { return (c16 & ~cmask) | ((c16 ^ slot) & cmask); }
 
 template <int BC>
-__global__ __launch_bounds__(NT) void conv_small_kernel(const SArgs A) {
+__global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A) {
   constexpr int NCB = BC / 16;   // 16-cout MFMA blocks per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const fmd_conv_small_desc& d = A.d;
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(NT) void conv_small_kernel(const SArgs A) {
   // then the 1x1 segment's chunks cp, cp + CP, ...  All of its weight fragments (<= 36, plan) are loaded up front into
   // registers, so the MFMA loop never waits on memory: bq[(k*9 + t)*NCB + cb] (3x3), bq[k*NCB + cb] (1x1 main), the
   // skip chunks from bq[SKB + k*NCB + cb]
-  const int CP = A.cp, RG = 8 / CP, NRB = 4 / RG;
+  const int CP = A.cp, RG = NW / CP, NRB = 4 / RG;
   const int cp = wid % CP, rg = wid / CP;
   const int nrbv = (vpx + 15) >> 4;    // row blocks holding valid pixels
   const int l16 = lane & 15, kq = lane >> 4;
@@ -718,7 +728,7 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
   // every weight fragment of a wave in 36 registers: main chunks per wave <= 4 / NCB (3x3) or 36 / NCB (1x1), the
   // 1x1 segment's <= 4, and together within 36
   auto frag_ok = [&](int bc, int P) {
-    const int nch = C / P / 32, cp = nch >= 8 ? 8 : nch >= 4 ? 4 : 2;
+    const int nch = C / P / 32, cp = nch >= NW ? NW : nch >= 4 ? 4 : 2;
     const int ncb = bc / 16, kw = (nch + cp - 1) / cp, kw2 = (C23 / P / 32 + cp - 1) / cp;
     const int mainf = kw * A->T * ncb;
     return !(kw2 > 4 || (A->T == 9 && kw > 4 / ncb) || mainf > 36 || (C23 && mainf > 36 - 4 * ncb));
@@ -755,7 +765,7 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
     const int tpx = A->whole ? A->S * A->HWo : TPX;
     const int in_b = (A->slots + 1) * Cs * 2;
     const int raw_b = tpx * A->C23s * 2;
-    const int red_b = 8 * TPX * A->bc * 4;
+    const int red_b = NW * TPX * A->bc * 4;
     const int body = in_b + raw_b > red_b ? in_b + raw_b : red_b;
     A->off_raw = in_b;
     A->off_ab = (body + 15) / 16 * 16;
@@ -776,7 +786,7 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
       A->cmask2 = c238 % 16 == 0 ? 15 : c238 % 8 == 0 ? 7 : c238 % 4 == 0 ? 3 : 1;
       A->fd_c23 = make_fdiv(c238 > 0 ? c238 : 1);
       const int nch = Cs / 32;
-      A->cp = nch >= 8 ? 8 : nch >= 4 ? 4 : 2;
+      A->cp = nch >= NW ? NW : nch >= 4 ? 4 : 2;
       A->gn = gn;
       A->fd_c8 = make_fdiv(c8);
       A->fd_rowslots = make_fdiv(A->in_rows * d->Ws);
@@ -787,7 +797,8 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
       A->fd_c2 = make_fdiv(2 * Cs);
       A->fd_cs = make_fdiv(Cs);
       A->cg_lanes = gn && Cg <= 64 && (Cg & (Cg - 1)) == 0 ? Cg : 0;
-      A->lnrb = A->cp == 8 ? 2 : A->cp == 4 ? 1 : 0;   // NRB = 4 / (8 / cp)
+      const int nrb = 4 * A->cp / NW;                  // NRB = 4 / (NW / cp)
+      A->lnrb = nrb == 4 ? 2 : nrb == 2 ? 1 : 0;
       return total;
     }
     if (!A->whole || A->S == 1) return -7;

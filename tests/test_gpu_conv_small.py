@@ -44,9 +44,11 @@ CASES = {
 
 @pytest.fixture(autouse=True)
 def _small_conv_on(monkeypatch):
-    """The kernel under test, whatever the SMALL_CONV default of runtime/tuning.py."""
+    """The kernel under test, whatever the SMALL_CONV defaults of runtime/tuning.py (the level cap is a speed
+    choice; the kernel takes 32^2 too)."""
     from fmdiff.runtime import ops
     monkeypatch.setattr(ops, "SMALL_CONV", True)
+    monkeypatch.setattr(ops, "SMALL_CONV_MAX_HW", 1024)
 
 
 def _bf(t):
@@ -159,6 +161,8 @@ def _run_small(p, split=None, x0=None, check_only=False):
 def test_conv_small_vs_torch(name, split):
     """split 0: the plan's parts (the in-launch combine wherever the grid is small), 1: one workgroup per tile."""
     p = _make(name)
+    if split == 1 and not _run_small(p, 1, check_only=True):
+        pytest.skip("the plan takes this problem only as parts of the reduction")   # the 1x1 segment's registers
     ref = _reference(p)
     out, st = _run_small(p, split)
     torch.cuda.synchronize()
@@ -238,16 +242,17 @@ def test_conv_small_split_combine(name):
     ops = p["ops"]
     x0a = p["x0"].to(DEV)
     x0b = (x0a.float() * -0.7 + 0.3).to(torch.bfloat16)
-    base, _ = _run_small(p, 1, x0a)
-    Ps = [P for P in (2, 4, 8, 16) if _run_small(p, P, x0a, check_only=True)]
-    assert Ps, "no forced split qualifies"
+    Ps = [P for P in (1, 2, 4, 8, 16) if _run_small(p, P, x0a, check_only=True)]
+    assert len(Ps) >= 2, "fewer than two part counts qualify"
+    base, _ = _run_small(p, Ps[0], x0a)   # the fewest parts the plan takes (1 where the registers allow)
+    Ps = Ps[1:]
     solo = {}
     for P in Ps:
         outs = [_run_small(p, P, x)[0].clone() for x in (x0a, x0b)]
         solo[P] = outs
         err = (outs[0].float() - base.float()).abs().max().item()
         scale = base.float().abs().max().item()
-        print(f"[conv_small split] {name} P={P}: vs unsplit {err / scale:.2e}")
+        print(f"[conv_small split] {name} P={P}: vs the fewest parts {err / scale:.2e}")
         assert err <= 4e-3 * scale
     torch.cuda.synchronize()
     for rep in range(3):   # interleaved part counts and inputs, no synchronisation in between

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 i=0
 for setting in $AB; do
   i=$((i + 1))
-  env $setting timeout -k 10 200 python tools/bench_latent.py ${LATENT_ARGS} > gpurun_out/abl_$i.json 2> gpurun_out/abl_$i.err
+  env ${setting//;/ } timeout -k 10 200 python tools/bench_latent.py ${LATENT_ARGS} > gpurun_out/abl_$i.json 2> gpurun_out/abl_$i.err
   rc=$?; echo "$setting rc=$rc $(grep -o '"images_per_sec": [0-9.]*\|"sample": [0-9.]*' gpurun_out/abl_$i.json | tr '\n' ' ')"
   [ $rc -eq 0 ] || exit $rc
 done

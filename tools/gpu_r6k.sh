@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 6: conv_small with 4-wave workgroups (two per CU) vs 8-wave: parity, phases, config D A/B.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r6k
+V=flow-matching-and-diffusion-models_amd/fmdiff/lib/variants
+timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread -m gpu tests/test_gpu_conv_small.py \
+  > gpurun_out/r6k/tests_small.log 2>&1
+rc=$?; tail -3 gpurun_out/r6k/tests_small.log; [ $rc -eq 0 ] || exit $rc
+FMD_LIB=$V/libfmdiff_ts.so timeout -k 10 300 python tools/small_abl.py > gpurun_out/r6k/abl.txt 2>&1; rc=$?; cat gpurun_out/r6k/abl.txt; [ $rc -eq 0 ] || exit $rc
+AB="FMD_TUNE=SMALL_CONV=0 FMD_TUNE=SMALL_CONV=1,SMALL_CONV_MAX_HW=256 FMD_LIB=$V/libfmdiff_nt512.so;FMD_TUNE=SMALL_CONV=1,SMALL_CONV_MAX_HW=256 FMD_TUNE=SMALL_CONV=1 FMD_TUNE=SMALL_CONV=0" timeout -k 10 600 bash tools/ab_latent.sh || exit $?
+A="FMD_TUNE=SMALL_CONV=1" B="FMD_TUNE=SMALL_CONV=0" timeout -k 10 650 bash tools/ab_prof_latent.sh || exit $?
