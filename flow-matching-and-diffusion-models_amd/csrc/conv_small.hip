@@ -66,13 +66,15 @@ struct SArgs {
   int slots;        // staged pixel slots (the zero slot is index `slots`)
   int cmask;        // 16-byte-chunk swizzle mask
   int C23, C23s, cmask2;   // 1x1 segment channels (all, per part) and their swizzle mask
-  int off_raw, off_ab, off_mr, off_gs, off_ep;   // LDS byte offsets (input region at 0)
+  int off_raw, off_ab, off_mr, off_gs, off_ep, off_st;   // LDS byte offsets (input region at 0)
   int cp;           // chunk parts (waves per row-block group)
   int gn;
   int bc;           // output channels per workgroup (16 or 32: the template instance)
   FDiv fd_c8, fd_rowslots, fd_ws, fd_c23, fd_hwo, fd_wo, fd_cg, fd_c2, fd_cs;   // fixed divisors (host magic)
   int cg_lanes;     // GroupNorm channels per group when a power of two <= 64 (the butterfly fold), else 0
+  double inv_cnt;   // 1 / (channels per group x pixels per image)
   int lnrb;         // log2 of the row blocks per wave
+  int kw;           // 32-channel chunks per wave (the template instance, 1..4)
 };
 
 #ifdef FMD_SMALL_DBG
@@ -105,7 +107,42 @@ extern "C" int fmd_debug_small_ts(void* host, int nblocks, int clear) {
 
 FMD_DEV int swz(int c16, int slot, int cmask) { return (c16 & ~cmask) | ((c16 ^ slot) & cmask); }
 
-template <int BC>
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+// a double from the lane DPP control CTRL names (both halves moved by v_mov_b32_dpp: no LDS round trip)
+template <int CTRL>
+FMD_DEV double dpp_d(double v) {
+  const i32x2 x = __builtin_bit_cast(i32x2, v);
+  i32x2 y;
+  y.x = __builtin_amdgcn_update_dpp(0, x.x, CTRL, 0xF, 0xF, true);
+  y.y = __builtin_amdgcn_update_dpp(0, x.y, CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, y);
+}
+// sum over aligned groups of g = 2^k <= 64 lanes, every lane of a group ends with the same value (the pairings are
+// symmetric and fp addition commutes): quad xor 1, xor 2, row half-mirror, row mirror, then lane xor 16 / 32
+FMD_DEV double group_sum(double v, int g) {
+  if (g >= 2) v += dpp_d<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  if (g >= 4) v += dpp_d<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  if (g >= 8) v += dpp_d<0x141>(v);   // row_half_mirror
+  if (g >= 16) v += dpp_d<0x140>(v);  // row_mirror
+  if (g >= 32) {                      // ds_swizzle, bit mode: xor 16 within 32 lanes
+    const i32x2 x = __builtin_bit_cast(i32x2, v);
+    i32x2 y;
+    y.x = __builtin_amdgcn_ds_swizzle(x.x, 0x401F);
+    y.y = __builtin_amdgcn_ds_swizzle(x.y, 0x401F);
+    v += __builtin_bit_cast(double, y);
+  }
+  if (g >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+// the same over aligned groups of 8 lanes, fp32
+FMD_DEV float sum8(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  return v;
+}
+
+template <int BC, int KW>   // KW: 32-channel chunks per wave (plan), so only the fragments used are loaded
 __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A) {
   constexpr int NCB = BC / 16;   // 16-cout MFMA blocks per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -180,15 +217,15 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
   const int nch = SDBG(4) ? 0 : Cs >> 5;
   const bool keep_raw = C23 > 0;
   const int nch2 = C23 >> 5;
-  constexpr int NB = 36, SKB = NB - 4 * NCB, KM9 = 4 / NCB, KM1 = NB / NCB;
-  bf16x8 bq[NB];
+  bf16x8 bq[KW * 9 * NCB];   // 3x3: [k][tap][cb]; 1x1: the first KW * NCB as [k][cb]
+  bf16x8 bs[4 * NCB];        // the 1x1 segment's [k][cb]
   {
     const auto rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.wgt, 0, d.K * T * C * 2, 0x00020000);
     const unsigned wl = (unsigned)(((k0 + l16) * T * C + cs0 + kq * 8) * 2);   // this lane's row, bytes
     const unsigned wcb = 16u * T * C * 2;                                       // between the 16-cout blocks
     if (T == 9) {
 #pragma unroll
-      for (int k = 0; k < KM9; ++k)
+      for (int k = 0; k < KW; ++k)
 #pragma unroll
         for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -199,7 +236,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
           }
     } else {
 #pragma unroll
-      for (int k = 0; k < KM1; ++k)
+      for (int k = 0; k < KW; ++k)
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
           const int c = cp + k * CP;
@@ -217,7 +254,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
       for (int cb = 0; cb < NCB; ++cb) {
         const int c = cp + k * CP;
         const unsigned off = c < nch2 ? wl2 + (unsigned)(cb * 16 * A.C23 + c * 32) * 2 : OOR;
-        bq[SKB + k * NCB + cb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw2, off, 0, 0));
+        bs[k * NCB + cb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw2, off, 0, 0));
       }
   }
 
@@ -330,6 +367,28 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
       }
     }
   }
+  // The main loop's LDS addresses, one table for the workgroup: stab[pixel][tap] = the byte offset of the tap's input
+  // row (or the zero slot's), with the slot's low swizzle bits (sl & cmask) * 16 in the low bits -- rowb is a
+  // multiple of 16 * (cmask + 1), so they are free -- and a fragment address is (sb ^ (c16 & cmask) * 16) +
+  // (c16 & ~cmask) * 16.  Each thread fills one or two of the TPX x 9 entries (pure ALU, while the loads above are
+  // in flight) instead of every lane computing its own 36.
+  int* stab = (int*)(smem + A.off_st);   // [TPX][12]
+  {
+    const int sm = d.mode == 1 ? 2 : 1, shf = d.mode == 2 ? 1 : 0;
+    const int Hl = d.mode == 2 ? d.Ho : d.Hs, Wl = d.mode == 2 ? d.Wo : d.Ws;
+    const int zsb = A.slots * rowb + (A.slots & A.cmask) * 16;
+    for (int e = tid; e < TPX * 9; e += NT) {
+      const int p = e / 9, t = e - p * 9;
+      const int s = A.whole ? fdiv(p, A.fd_hwo) : 0;
+      const int rem = A.whole ? p - s * A.HWo : oy0 * d.Wo + p;
+      const int oy = fdiv(rem, A.fd_wo), ox = rem - oy * d.Wo;
+      const int ky = T == 1 ? 1 : t / 3, kx = T == 1 ? 1 : t - (t / 3) * 3;
+      const int yy = oy * sm + ky - 1, xx = ox * sm + kx - 1;
+      const int sl = (s * A.in_rows - iy_lo + (yy >> shf)) * d.Ws + (xx >> shf);
+      const bool ok = p < vpx && t < T && yy >= 0 && yy < Hl && xx >= 0 && xx < Wl;
+      stab[p * 12 + t] = ok ? sl * rowb + (sl & A.cmask) * 16 : zsb;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
   __syncthreads();
   STS(2);
@@ -342,7 +401,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
     // lanes of one wave), sums its slab rows, the group totals meet by an fp64 butterfly over the Cg lanes, and every
     // lane forms its own (a, b) -- no serial per-group loop, one barrier
     const int Cg = A.cg_lanes;
-    const double cnt = (double)Cg * A.HWs;
+    const double inv_cnt = A.inv_cnt;
     for (int i0 = 0; i0 < nS * Cs; i0 += NT) {   // the same trip count in every wave: the shuffles see whole groups
       const int i = i0 + tid;
       const bool act = i < nS * Cs;
@@ -357,16 +416,12 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
         f0.x += x0.x; f0.y += x0.y; f1.x += x1.x; f1.y += x1.y;
       }
       if (e < E) { const float2 x0 = p[(size_t)e * m]; f0.x += x0.x; f0.y += x0.y; }
-      double t1 = (double)(f0.x + f1.x), t2 = (double)(f0.y + f1.y);
-      for (int o = 1; o < Cg; o <<= 1) {
-        t1 += __shfl_xor(t1, o, 64);
-        t2 += __shfl_xor(t2, o, 64);
-      }
+      const double t1 = group_sum((double)(f0.x + f1.x), Cg), t2 = group_sum((double)(f0.y + f1.y), Cg);
       if (act) {
-        const double mean = t1 / cnt;
-        double var = t2 / cnt - mean * mean;
+        const double mean = t1 * inv_cnt;
+        double var = t2 * inv_cnt - mean * mean;
         if (var < 0) var = 0;
-        const float mf = (float)mean, rs = (float)(1.0 / sqrt(var + (double)d.eps));
+        const float mf = (float)mean, rs = rsqrtf((float)var + d.eps);
         float a = rs * gam[cl];
         float b = bet[cl] - mf * a;
         if (d.emb) {
@@ -464,37 +519,18 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
   // per (row block, tap): the LDS byte offset of this lane's pixel row (or the zero slot's), with the slot's low
   // swizzle bits (sl & cmask) * 16 in the low bits -- rowb is a multiple of 16 * (cmask + 1), so they are free -- and
   // a fragment address is (sb ^ (c16 & cmask) * 16) + (c16 & ~cmask) * 16
-  const int sm = d.mode == 1 ? 2 : 1, shf = d.mode == 2 ? 1 : 0;
-  const int Hl = d.mode == 2 ? d.Ho : d.Hs, Wl = d.mode == 2 ? d.Wo : d.Ws;
-  const int zsb = A.slots * rowb + (A.slots & A.cmask) * 16;
+
+  const int c16m_mask = A.cmask;
   int slotv[4][9];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int p = (rg * NRB + r) * 16 + l16;
-    const bool pv = r < NRB && p < vpx;
-    const int s = A.whole ? fdiv(p, A.fd_hwo) : 0;
-    const int rem = A.whole ? p - s * A.HWo : oy0 * d.Wo + p;
-    const int oy = fdiv(rem, A.fd_wo), ox = rem - oy * d.Wo;
-    const int srow = s * A.in_rows - iy_lo;
-    int rowoff[3], coloff[3];
-    bool vy[3], vx[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int yy = oy * sm + k - 1, xx = ox * sm + k - 1;
-      vy[k] = yy >= 0 && yy < Hl;
-      vx[k] = xx >= 0 && xx < Wl;
-      rowoff[k] = (srow + (yy >> shf)) * d.Ws;
-      coloff[k] = xx >> shf;
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = T == 1 ? 1 : t / 3, kx = T == 1 ? 1 : t % 3;
-      const int sl = rowoff[ky] + coloff[kx];
-      slotv[r][t] = pv && t < T && vy[ky] && vx[kx] ? sl * rowb + (sl & A.cmask) * 16 : zsb;
-    }
+    if (r >= NRB) continue;
+    const int4* q = (const int4*)(stab + ((rg * NRB + r) * 16 + l16) * 12);
+    const int4 v0 = q[0], v1 = q[1];
+    slotv[r][0] = v0.x; slotv[r][1] = v0.y; slotv[r][2] = v0.z; slotv[r][3] = v0.w;
+    slotv[r][4] = v1.x; slotv[r][5] = v1.y; slotv[r][6] = v1.z; slotv[r][7] = v1.w;
+    slotv[r][8] = stab[((rg * NRB + r) * 16 + l16) * 12 + 8];
   }
-  const int c16m_mask = A.cmask;
-
   f32x4 acc[4][NCB];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
@@ -519,7 +555,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
 #endif
   if (T == 9) {
 #pragma unroll
-    for (int k = 0; k < KM9; ++k) {
+    for (int k = 0; k < KW; ++k) {
       const int c = cp + k * CP;
       if (c >= nch) break;
 #pragma unroll
@@ -527,7 +563,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < KM1; ++k) {
+    for (int k = 0; k < KW; ++k) {
       const int c = cp + k * CP;
       if (c >= nch) break;
       step(k * NCB, c, 0);
@@ -550,7 +586,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
         const int p = (rg * NRB + r) * 16 + l16;
         const bf16x8 bfr = *(const bf16x8*)(smem + A.off_raw + p * (C23 * 2) + swz(c16, p, A.cmask2) * 16);
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) acc[r][cb] = mfma16(bq[SKB + k * NCB + cb], bfr, acc[r][cb]);
+        for (int cb = 0; cb < NCB; ++cb) acc[r][cb] = mfma16(bs[k * NCB + cb], bfr, acc[r][cb]);
       }
     }
   }
@@ -661,11 +697,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
         t2 += x * x;
       }
     }
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
-      t1 += __shfl_xor(t1, o, 64);
-      t2 += __shfl_xor(t2, o, 64);
-    }
+    t1 = sum8(t1);
+    t2 = sum8(t2);
     if (part == 0 && row < nrows) {
       const size_t grow = A.whole ? (size_t)(n0 + row) : (size_t)n0 * A.tiles_per_n + (oy0 / A.trows);
       d.stats[(grow * d.K + k0 + co) * 2] = t1;
@@ -674,7 +707,10 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
   }
 }
 
-constexpr int SPLIT_WG = 256;   // automatic split: parts until the launch has this many workgroups (one per CU)
+#ifndef FMD_SMALL_SPLIT_WG
+#define FMD_SMALL_SPLIT_WG 256
+#endif
+constexpr int SPLIT_WG = FMD_SMALL_SPLIT_WG;   // automatic split: parts until the launch has this many workgroups
 
 int plan(const fmd_conv_small_desc* d, SArgs* A) {
   if (!d || d->N < 1 || d->K < 16 || !d->src0 || !d->wgt || !d->out) return -1;
@@ -731,7 +767,8 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
     const int nch = C / P / 32, cp = nch >= NW ? NW : nch >= 4 ? 4 : 2;
     const int ncb = bc / 16, kw = (nch + cp - 1) / cp, kw2 = (C23 / P / 32 + cp - 1) / cp;
     const int mainf = kw * A->T * ncb;
-    return !(kw2 > 4 || (A->T == 9 && kw > 4 / ncb) || mainf > 36 || (C23 && mainf > 36 - 4 * ncb));
+    // instances: 16 couts x 1..4 chunks per wave, 32 couts x 1 chunk (more would spill)
+    return !(kw2 > 4 || kw > (bc == 32 ? 1 : 4) || mainf > 36 || (C23 && mainf > 36 - 4 * ncb));
   };
   for (;;) {   // fewer images per tile until the LDS plan fits
     if (A->whole) A->ptiles = (d->N + A->S - 1) / A->S;
@@ -777,7 +814,9 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
     const int gs_b = gn ? A->S * Emax * Cs * 8 + 2 * Cs * 4 + (d->emb ? A->S * 2 * Cs * 4 : 0) : 0;
     A->off_ep = (A->off_gs + gs_b + 15) / 16 * 16;
     // + the epilogue operands: bias, skip bias, per-sample bias rows, the residual tile
-    const int total = A->off_ep + (2 + A->S) * bc * 4 + TPX * bc * 2;
+    A->off_st = A->off_ep + (2 + A->S) * bc * 4 + TPX * bc * 2;
+    // + the main loop's address table [TPX][12] ints
+    const int total = A->off_st + TPX * 12 * 4;
     if (total <= LDS_MAX && (!gn || A->S * Cs <= 8192)) {
       A->ctiles = d->K / A->bc;
       const int c8 = Cs / 8;
@@ -787,6 +826,7 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
       A->fd_c23 = make_fdiv(c238 > 0 ? c238 : 1);
       const int nch = Cs / 32;
       A->cp = nch >= NW ? NW : nch >= 4 ? 4 : 2;
+      A->kw = (nch + A->cp - 1) / A->cp;
       A->gn = gn;
       A->fd_c8 = make_fdiv(c8);
       A->fd_rowslots = make_fdiv(A->in_rows * d->Ws);
@@ -797,6 +837,7 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
       A->fd_c2 = make_fdiv(2 * Cs);
       A->fd_cs = make_fdiv(Cs);
       A->cg_lanes = gn && Cg <= 64 && (Cg & (Cg - 1)) == 0 ? Cg : 0;
+      A->inv_cnt = 1.0 / ((double)Cg * A->HWs);
       const int nrb = 4 * A->cp / NW;                  // NRB = 4 / (NW / cp)
       A->lnrb = nrb == 4 ? 2 : nrb == 2 ? 1 : 0;
       return total;
@@ -819,21 +860,26 @@ extern "C" int fmd_conv_small_split(const fmd_conv_small_desc* d) {
   return r < 0 ? r : A.P;
 }
 
+template <int BC, int KW>
+const void* kfn() { return (const void*)conv_small_kernel<BC, KW>; }
+
 extern "C" int fmd_conv_small(const fmd_conv_small_desc* d, fmd_stream_t s) {
   SArgs A;
   const int lds = plan(d, &A);
   if (lds < 0) return lds;
+  static const void* const fns[5] = {kfn<16, 1>(), kfn<16, 2>(), kfn<16, 3>(), kfn<16, 4>(), kfn<32, 1>()};
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)conv_small_kernel<16>, (const void*)conv_small_kernel<32>}) {
+    for (const void* f : fns) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
       if (e != hipSuccess) return (int)e;
     }
     attr = true;
   }
-  if (A.bc == 32)
-    hipLaunchKernelGGL(conv_small_kernel<32>, dim3(A.ptiles * A.ctiles * A.P), dim3(NT), lds, (hipStream_t)s, A);
-  else
-    hipLaunchKernelGGL(conv_small_kernel<16>, dim3(A.ptiles * A.ctiles * A.P), dim3(NT), lds, (hipStream_t)s, A);
+  if (A.kw < 1 || A.kw > 4 || (A.bc == 32 && A.kw != 1)) return -9;   // the plan allows no other instance
+  const void* f = fns[A.bc == 32 ? 4 : A.kw - 1];
+  void* args[] = {&A};
+  const hipError_t e = hipLaunchKernel(f, dim3(A.ptiles * A.ctiles * A.P), dim3(NT), args, lds, (hipStream_t)s);
+  if (e != hipSuccess) return (int)e;
   return (int)hipGetLastError();
 }
