@@ -60,7 +60,7 @@ struct SArgs {
   int trows;        // output rows per tile
   int tiles_per_n;  // pixel tiles per image (not whole)
   int ptiles, ctiles;
-  int P;            // parts of the reduction (input channels) per tile: one workgroup each, combined in-launch
+  int P, lgP;       // parts of the reduction (input channels) per tile (a power of two): one workgroup each
   int Cs;           // input channels per part (C / P)
   int in_rows;      // staged input rows per image
   int slots;        // staged pixel slots (the zero slot is index `slots`)
@@ -73,6 +73,7 @@ struct SArgs {
   FDiv fd_c8, fd_rowslots, fd_ws, fd_c23, fd_hwo, fd_wo, fd_cg, fd_c2, fd_cs;   // fixed divisors (host magic)
   int cg_lanes;     // GroupNorm channels per group when a power of two <= 64 (the butterfly fold), else 0
   double inv_cnt;   // 1 / (channels per group x pixels per image)
+  FDiv fd_pt;       // by ptiles
   int lnrb;         // log2 of the row blocks per wave
   int kw;           // 32-channel chunks per wave (the template instance, 1..4)
 };
@@ -89,17 +90,17 @@ extern "C" int fmd_debug_small_flags(int f) { return (int)hipMemcpyToSymbol(HIP_
 #define SDBG(bit) false
 #endif
 #ifdef FMD_SMALL_TS
-// phase timestamps (s_memrealtime, 100 MHz) of wave 0 of every workgroup: [block][10]; -DFMD_SMALL_TS alone adds
+// phase timestamps (s_memrealtime, 100 MHz) of wave 0 of every workgroup: [block][12]; -DFMD_SMALL_TS alone adds
 // only these (no flag loads, same register allocation as the product build, near enough)
 constexpr int TS_MAX = 4096;
-__device__ unsigned long long g_small_ts[TS_MAX * 10];
+__device__ unsigned long long g_small_ts[TS_MAX * 12];
 extern "C" int fmd_debug_small_ts(void* host, int nblocks, int clear) {
-  if (clear) return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_small_ts), host, sizeof(unsigned long long) * 10 * nblocks);
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_small_ts), sizeof(unsigned long long) * 10 * nblocks);
+  if (clear) return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_small_ts), host, sizeof(unsigned long long) * 12 * nblocks);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_small_ts), sizeof(unsigned long long) * 12 * nblocks);
 }
 #define STS(k)                                                                                      \
   do {                                                                                              \
-    if (tid == 0 && blockIdx.x < TS_MAX) g_small_ts[blockIdx.x * 10 + (k)] = wall_clock64();       \
+    if (tid == 0 && blockIdx.x < TS_MAX) g_small_ts[blockIdx.x * 12 + (k)] = wall_clock64();       \
   } while (0)
 #else
 #define STS(k) do { } while (0)
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
   // XCDs (each XCD's L2 holds its weight slice), the small input is shared
   const int nwg = A.ptiles * A.ctiles * A.P;
   const int bid = xcd_remap(blockIdx.x, nwg);
-  const int kp = bid % A.P, tile = bid / A.P;
-  const int pt = tile % A.ptiles, ct = tile / A.ptiles;
+  const int kp = bid & (A.P - 1), tile = bid >> A.lgP;   // P: a power of two
+  const int ct = fdiv(tile, A.fd_pt), pt = tile - ct * A.ptiles;
   const int k0 = ct * BC;
   const int cs0 = kp * Cs;   // this part's first input channel (of the virtual concat C0 | C1)
 
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
       }
   }
 
+  STS(10);
   // ---------------------------------------------------------------- (2) everything else global -> LDS by DMA
   // Input region: LDS unit q (16 bytes) is physical chunk u of slot q / C8, which holds logical chunk swz(u, slot)
   // (the swizzle is an involution); padding rows get zeros by ds_write.  Then the raw 1x1-segment input of the tile's
@@ -480,6 +482,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void conv_small_kernel(const SArgs A)
     __syncthreads();
   }
 
+  STS(11);
   // ---------------------------------------------------------------- (4) GroupNorm affine + SiLU, in place in LDS
   if (A.gn) {
     for (int q = tid; q < units; q += NT) {
@@ -838,6 +841,9 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
       A->fd_cs = make_fdiv(Cs);
       A->cg_lanes = gn && Cg <= 64 && (Cg & (Cg - 1)) == 0 ? Cg : 0;
       A->inv_cnt = 1.0 / ((double)Cg * A->HWs);
+      A->fd_pt = make_fdiv(A->ptiles);
+      A->lgP = 0;
+      while ((1 << A->lgP) < A->P) ++A->lgP;
       const int nrb = 4 * A->cp / NW;                  // NRB = 4 / (NW / cp)
       A->lnrb = nrb == 4 ? 2 : nrb == 2 ? 1 : 0;
       return total;

@@ -491,6 +491,7 @@ CONV_SMALL_MODES = {"s1": 0, "s2": 1, "up": 2, "point": 3}
 # forward-only small levels in one launch per conv (fmd_conv_small, runtime/tuning.py SMALL_CONV / SMALL_CONV_MAX_HW)
 SMALL_CONV = bool(tuning.get("SMALL_CONV"))
 SMALL_CONV_MAX_HW = tuning.get("SMALL_CONV_MAX_HW")
+SMALL_CONV_MAX_WORK = tuning.get("SMALL_CONV_MAX_WORK")
 SMALL_CONV_SPLIT = tuning.get("SMALL_CONV_SPLIT")
 # the in-launch combine of a split reduction: fp32 partial tiles + arrival tickets, one set per (device, stream) --
 # launches on one stream serialise, so they can share it; the tickets start at zero and every launch leaves them so
@@ -553,7 +554,7 @@ def conv_small_ok(shape0, K, *, C1=0, mode="s1", gn=None, skip=None, split=None)
         return False
     m = CONV_SMALL_MODES[mode]
     HWo = shape0[1] * shape0[2] * (4 if m == 2 else 1) // (4 if m == 1 else 1)
-    if HWo > SMALL_CONV_MAX_HW:
+    if HWo > SMALL_CONV_MAX_HW or HWo * (shape0[3] + C1) > SMALL_CONV_MAX_WORK:
         return False
     return _conv_small_query("fmd_conv_small_plan", shape0, K, C1, mode, gn, skip, split) > 0
 

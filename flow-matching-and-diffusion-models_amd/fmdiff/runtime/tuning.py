@@ -28,8 +28,9 @@ TABLE = {
     "GN_FUSED": (1, "small levels: GroupNorm statistics + affine + SiLU operand in one launch"),
     "CONV_GN": (1, "split-K conv1 -> GroupNorm-2 in the split combine (fmd_conv_gn)"),
     "SMALL_CONV": (1, "forward-only small levels: one launch per conv with the GroupNorm folded in (fmd_conv_small)"),
-    "SMALL_CONV_MAX_HW": (64, "fmd_conv_small only on outputs of at most this many pixels per image (8^2 and below: "
-                               "measured best for config D and the config B sampler, DESIGN.md round 6)"),
+    "SMALL_CONV_MAX_HW": (256, "fmd_conv_small only on outputs of at most this many pixels per image"),
+    "SMALL_CONV_MAX_WORK": (65536, "... and output pixels per image x input channels at most this (16^2 x 256: config D's "
+                                   "16^2 level, not config B's 512-channel one; DESIGN.md round 6)"),
     "SMALL_CONV_SPLIT": (0, "fmd_conv_small reduction parts combined in-launch: 0 plan's choice, 1 none, 2..16 forced"),
     # ---- split heuristics
     "CONV_GN_MIN_BLOCKS": (128, "fmd_conv_gn only from this many combine blocks up"),

@@ -49,6 +49,7 @@ def _small_conv_on(monkeypatch):
     from fmdiff.runtime import ops
     monkeypatch.setattr(ops, "SMALL_CONV", True)
     monkeypatch.setattr(ops, "SMALL_CONV_MAX_HW", 1024)
+    monkeypatch.setattr(ops, "SMALL_CONV_MAX_WORK", 1 << 30)
 
 
 def _bf(t):

@@ -312,6 +312,7 @@ def test_conv_small_plan_is_a_host_query(monkeypatch):
         pytest.skip(f"library not loadable here: {e}")
     monkeypatch.setattr(ops, "SMALL_CONV", True)
     monkeypatch.setattr(ops, "SMALL_CONV_MAX_HW", 1024)
+    monkeypatch.setattr(ops, "SMALL_CONV_MAX_WORK", 1 << 30)
     st64, st16 = ops.Stats(None, 64), ops.Stats(None, 16)
     gn = dict(st0=st64, st1=st64, groups=32, eps=1e-6)
     assert ops.conv_small_ok((8, 16, 16, 256), 128, C1=128, gn=gn, skip=(256, 128))      # 16^2 decoder concat

@@ -49,13 +49,13 @@ def phase_times(L, fn, name, flags=0):
     ts = L.fmd_debug_small_ts
     ts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     nb = 4096
-    buf = np.zeros(nb * 10, dtype=np.uint64)
+    buf = np.zeros(nb * 12, dtype=np.uint64)
     ts(buf.ctypes.data, nb, 1)
     torch.cuda.synchronize()
     fn()
     torch.cuda.synchronize()
     ts(buf.ctypes.data, nb, 0)
-    t = buf.reshape(nb, 10).astype(np.int64)
+    t = buf.reshape(nb, 12).astype(np.int64)
     t = t[t[:, 0] > 0]
     if not len(t):
         return
@@ -76,6 +76,10 @@ def phase_times(L, fn, name, flags=0):
             parts.append(f"{lab}: " + " ".join(f"{x:5.2f}" for x in d))
     end = np.where(t[:, 7] > 0, t[:, 7], np.where(t[:, 6] > 0, t[:, 6], t[:, 5]))
     parts.append(f"start spread {(t[:, 0].max() - t0) * 0.01:5.2f} end {(end.max() - t0) * 0.01:5.2f} wgs {len(t)}")
+    if (t[:, 10] > 0).any() and (t[:, 11] > 0).any():
+        w = np.median(t[:, 10] - t[:, 0]) * 0.01
+        f = np.median(t[:, 11] - t[:, 2]) * 0.01
+        parts.append(f"(weights issue {w:5.2f}, GN fold {f:5.2f})")
     if (t[:, 9] > 0).any():
         ok = t[:, 9] > 0
         d = (t[ok, 9] - t[ok, 8]) * 0.01
