@@ -775,9 +775,10 @@ int plan(const fmd_conv_small_desc* d, SArgs* A) {
   };
   for (;;) {   // fewer images per tile until the LDS plan fits
     if (A->whole) A->ptiles = (d->N + A->S - 1) / A->S;
-    // 32 output channels per workgroup (half the redundant staging per channel) while that still leaves >= 128
-    // workgroups; else 16 (twice the workgroups sharing the weight stream)
-    int bc = d->K % 32 == 0 && A->ptiles * (d->K / 32) >= 128 ? 32 : 16;
+    // 32 output channels per workgroup (half the redundant staging per channel) only where that still fills the chip
+    // unsplit; else 16, which halves the parts the reduction needs (the split's ticket and combine cost a workgroup
+    // ~2.5 us; config D's 16^2 level: 15.9 us at 32 couts x 2 parts)
+    int bc = d->K % 32 == 0 && A->ptiles * (d->K / 32) >= SPLIT_WG ? 32 : 16;
     int P = 1;
     for (;;) {
       const int nwg1 = A->ptiles * (d->K / bc);

@@ -333,5 +333,6 @@ def test_conv_small_plan_is_a_host_query(monkeypatch):
     assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=1) == 1
     assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=4) == 4
     assert ops.conv_small_split((8, 2, 2, 512), 512, C1=512, gn=gn2, split=3) < 0         # not a power of two
-    assert ops.conv_small_split((8, 32, 32, 128), 128, mode="s2", split=0) == 2             # 128 tiles -> 256
-    assert ops.conv_small_split((8, 16, 16, 128), 128, C1=128, gn=gn, skip=(128, 128), split=0) == 2
+    assert ops.conv_small_split((8, 32, 32, 128), 128, mode="s2", split=0) == 1             # 32 x 8 16-cout tiles
+    assert ops.conv_small_split((8, 16, 16, 128), 128, C1=128, gn=gn, skip=(128, 128), split=0) == 1
+    assert ops.conv_small_split((8, 8, 8, 256), 256, gn=gn, split=0) == 2                   # 8 x 16 tiles -> 256
