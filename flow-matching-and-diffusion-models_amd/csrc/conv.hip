@@ -870,6 +870,7 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
     rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= HALO_MIN_WG (32) workgroups of 16x16 tiles (x splits)
+  if (rc == 1 && d->fold_st0) return -13;   // the in-kernel GroupNorm fold runs only on the halo kernel
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->gout) return -9;                            // the prologue side output exists only on the halo path

@@ -761,7 +761,11 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
-  if (d->pro_a && d->C0 + d->C1 > CMAX) return 1;   // the GN affine table holds CMAX channels
+  if ((d->pro_a || d->fold_st0) && d->C0 + d->C1 > CMAX) return 1;   // the GN affine table holds CMAX channels
+  if (d->fold_st0 && (d3 || d->gout || d->pro_a || d->fold_G < 1 || (d->C0 + d->C1) % d->fold_G || d->fold_rows0 < 1 ||
+                      (d->Hs * d->Ws) % d->fold_rows0 ||
+                      (d->C1 && (!d->fold_st1 || d->fold_rows1 < 1 || (d->Hs * d->Ws) % d->fold_rows1))))
+    return 1;   // the in-kernel fold: 2-D, whole slab rows, one source of statistics per input
   if (d->gout && (d->C0 + d->C1) % BK) return 1;     // G side output: whole 32-channel chunks
   if ((long long)Nn * d->Hs * d->Ws * (d->C0 > d->C1 ? d->C0 : d->C1) >= (1LL << 31) ||
       (long long)Nn * d->Ho * d->Wo * (d->C2 > d->C3 ? d->C2 : d->C3) >= (1LL << 31)) return 1;   // 32-bit offsets
@@ -784,14 +788,17 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (A.splits > 1 && (A.splits - 1) * A.cps >= A.nchunk1) return 1;   // every split owns >= 1 chunk
   A.wt = (const bf16r*)d->wgt_tiled;
   A.wt2 = (const bf16r*)d->wgt2_tiled;
+  A.fold_E0 = d->fold_st0 ? d->Hs * d->Ws / d->fold_rows0 : 0;
+  A.fold_E1 = d->fold_st0 && d->C1 ? d->Hs * d->Ws / d->fold_rows1 : 0;
+  A.fold_inv = d->fold_st0 ? 1.0 / ((double)(A.C / d->fold_G) * d->Hs * d->Ws) : 0.0;
   A.dbg = g_dbg;
   A.tbuf = g_tbuf;
   const int nwg = Nn * A.tiles_x * A.tiles_y * A.ntc;
   if (nwg * A.splits < g_halo_min_wg) return 1;   // too few workgroups to fill the chip: the implicit GEMM wins
-  const int pro = d->pro_a ? (d->pro_silu ? 2 : 1) : 0;
+  const int pro = d->pro_a || d->fold_st0 ? (d->pro_silu ? 2 : 1) : 0;
   {   // the v9b kernel (csrc/conv_halo9.hip) takes every problem it supports
     const int rc9 = halo9_launch(A, pro, stream);
-    if (rc9 != 1) return rc9;
+    if (rc9 != 1 || d->fold_st0) return rc9;   // the fold exists only in v9b
   }
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);

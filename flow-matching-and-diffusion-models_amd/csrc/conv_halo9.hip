@@ -157,7 +157,68 @@ void conv3x3_halo9b(const HArgs A) {
   const bf16r* __restrict__ s2 = (const bf16r*)d.src2;
   const bf16r* __restrict__ s3 = (const bf16r*)d.src3;
 
-  if (PRO != 0) {
+  if (PRO != 0 && d.fold_st0) {
+    // The GroupNorm affine of the sample folded here from the producers' statistics slabs (forward only).  Channel
+    // totals: per source its sample's E slab rows x Cx channels are contiguous; thread u of (channel pair, row group)
+    // sums rows rg, rg + R, ... as 16-byte loads eight in flight, the R row groups meet in LDS (staging area, not in
+    // use yet) in fixed order.  Then per channel the group sums in fp64 (E[x^2] - mean^2, as gn_prep; rstd by the
+    // fp32 rsqrt), the affine and the scale-shift rows.
+    float2* tot = (float2*)smem;                       // [C] (sum, sum of squares)
+    f32x4* prt = (f32x4*)(smem + CMAX * 8);            // [R][pairs] partials
+    {
+      // both sources in one pass: pair index pi < P0 is src0's, the rest src1's
+      const int P0 = d.C0 >> 1, P = A.C >> 1, R = P >= NT9 ? 1 : NT9 / P;
+      for (int u = tid; u < P * R; u += NT9) {
+        const int rg = u / P, pi = u - rg * P;
+        const bool in0 = pi < P0;
+        const int pairs = in0 ? P0 : P - P0, pr = in0 ? pi : pi - P0, E = in0 ? A.fold_E0 : A.fold_E1;
+        const f32x4* base = (const f32x4*)(in0 ? d.fold_st0 : d.fold_st1) + (size_t)smp * E * pairs + pr;
+        f32x4 acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int e = rg;
+        for (; e + 7 * R < E; e += 8 * R) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += base[(size_t)(e + j * R) * pairs];
+        }
+        for (; e < E; e += R) acc[0] += base[(size_t)e * pairs];
+        prt[u] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+      }
+      __syncthreads();
+      for (int pi = tid; pi < P; pi += NT9) {
+        f32x4 t = prt[pi];
+        for (int rg = 1; rg < R; ++rg) t += prt[rg * P + pi];
+        tot[2 * pi] = make_float2(t[0], t[1]);
+        tot[2 * pi + 1] = make_float2(t[2], t[3]);
+      }
+      __syncthreads();
+    }
+    const int Cg = A.C / d.fold_G;
+    for (int c = tid; c < A.C; c += NT9) {
+      const int g0 = c - c % Cg;
+      double t1 = 0.0, t2 = 0.0;
+      for (int j = 0; j < Cg; ++j) {
+        const float2 t = tot[g0 + j];
+        t1 += t.x;
+        t2 += t.y;
+      }
+      const double mean = t1 * A.fold_inv;
+      double var = t2 * A.fold_inv - mean * mean;
+      if (var < 0) var = 0;
+      const float rs = rsqrtf((float)var + d.fold_eps);
+      float a = rs * (d.fold_gamma ? d.fold_gamma[c] : 1.f);
+      float bb = (d.fold_beta ? d.fold_beta[c] : 0.f) - (float)mean * a;
+      if (d.fold_emb) {
+        const float sc = 1.f + d.fold_emb[(size_t)smp * d.fold_emb_stride + c];
+        a *= sc;
+        bb = bb * sc + d.fold_emb[(size_t)smp * d.fold_emb_stride + A.C + c];
+      }
+      coef[c] = a;
+      coef[A.C + c] = bb;
+    }
+    if (tid < 8) coef[ZCOEF + tid] = 0.f;
+    __syncthreads();   // the staging area is free again
+  } else if (PRO != 0) {
     for (int i = tid; i < 2 * A.C; i += NT9)
       coef[i] = i < A.C ? d.pro_a[(size_t)smp * A.C + i] : d.pro_b[(size_t)smp * A.C + (i - A.C)];
     if (tid < 8) coef[ZCOEF + tid] = 0.f;
@@ -791,7 +852,7 @@ extern "C" int fmd_conv_s2d(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (d->stride != 2 || d->pad != 1 || (d->ks != 3 && d->ks != 4) || d->transposed || d->upsample) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;   // 3-D: the depth taps as chunks (kz, plane, block)
   if (d3 && d->Ds != 2 * d->Do) return 1;
-  if (d->src2 || d->gout || d->out_f32 || d->splits > 1) return 1;
+  if (d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->fold_st0) return 1;
   if (d->Hs != 2 * d->Ho || d->Ws != 2 * d->Wo || d->Ho % TH || d->Wo % TW) return 1;
   const int C = d->C0 + d->C1;
   if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;
@@ -847,7 +908,7 @@ extern "C" int fmd_conv_d2s(const fmd_conv_desc* d, fmd_stream_t stream) {
   if (!d->transposed || d->stride != 2 || d->pad != 1 || d->ks != 3 || d->upsample) return 1;
   const bool d3 = d->Do > 0 || d->Ds > 0;   // 3-D: 8 output classes, chunks (depth offset, block)
   if (d3 && d->Do != 2 * d->Ds) return 1;
-  if (d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->pro_a) return 1;
+  if (d->src2 || d->gout || d->out_f32 || d->splits > 1 || d->pro_a || d->fold_st0) return 1;
   if (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws || d->Hs % TH || d->Ws % TW) return 1;
   const int C = d->C0 + d->C1;
   if (C % BK || d->C0 % 8 || d->K % BCO || !d->wgt_tiled) return 1;

@@ -18,6 +18,8 @@ struct HArgs {
                           // (zeros outside; stored slice >> 1 under nearest-x2, dsrc = stored depth);
                           // per-sample tables (GN affine, bias_nc, ep_a/b) are indexed by slice / depth
   unsigned long long* tbuf;    // per-wave phase timestamps (compiled in only with -DFMD_HALO_TIME)
+  int fold_E0, fold_E1;        // d.fold_st0: statistics slab rows per image of src0 / src1
+  double fold_inv;             // 1 / (channels per group x pixels per image)
   int dbg;                     // debug ablations (fmd_debug_halo_flags; compiled in only with -DFMD_HALO_DBG):
                                // 1 no halo loads, 2 no transform, 4 no epilogue, 8 no weight DMA in the loop,
                                // 16 no SiLU' in the epilogue, 32 no statistics, 64 no side-tile loads

@@ -29,6 +29,8 @@ class ConvDesc(C.Structure):
         ("stats", p), ("ep_x0", p), ("ep_x1", p), ("ep_C0", i32), ("ep_a", p), ("ep_b", p),
         ("ws", p), ("splits", i32), ("force_generic", i32), ("wgt_tiled", p), ("wgt2_tiled", p),
         ("Ds", i32), ("Do", i32), ("gout", p),
+        ("fold_st0", p), ("fold_rows0", i32), ("fold_st1", p), ("fold_rows1", i32), ("fold_G", i32),
+        ("fold_eps", f32), ("fold_gamma", p), ("fold_beta", p), ("fold_emb", p), ("fold_emb_stride", i32),
     ]
 
 

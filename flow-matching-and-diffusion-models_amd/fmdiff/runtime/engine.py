@@ -628,10 +628,15 @@ class UNetEngine:
             # small level: statistics, affine and the materialised prologue in one launch from x0|x1
             a1, b1, mr1, t1 = ops.gn_fused_apply(x0.t, x1.t if x1 else None, g1.num_groups, g1.eps, g1.weight,
                                                  g1.bias)
+        elif ctx.tape is None and not mat1 and halo1 and len(sp) == 2 and ops.HALO_FOLD:
+            # forward only, halo conv1: the GroupNorm-1 affine folded inside the conv from the statistics slabs
+            a1 = b1 = mr1 = t1 = None
         else:
             a1, b1, mr1 = ops.gn_prep(_stats(x0), _stats(x1), N, HW, C0, C1, g1.num_groups, g1.eps, g1.weight,
                                       g1.bias)
             t1 = ops.gn_apply_fwd(x0.t, x1.t if x1 else None, a1, b1) if mat1 else None
+        pf1 = (dict(st0=_stats(x0), st1=_stats(x1), groups=g1.num_groups, eps=g1.eps, gamma=g1.weight, beta=g1.bias)
+               if a1 is None and t1 is None else None)
         halo2 = self._halo_ok(N, sp, Cout, Cout, pro=True)
         mat2 = _materialise(halo2, None, Cout, HW, len(sp) == 3) or bool(drop)   # dropout acts on the materialised operand
         fuse2 = mat2 and ops.gn_fused_eligible(HW, Cout, Cout, g2.num_groups)
@@ -645,7 +650,7 @@ class UNetEngine:
                       emb_stride=es if ss else 0, emb_mode=1 if ss else 0)
                  if fuse2 and not (add and ctx.tape is not None) else None)
         h, hst = ops.conv(t1 if t1 is not None else x0.t, Cout, w1, src1=src1,
-                          pro=None if t1 is not None else (a1, b1, True),
+                          pro=None if (t1 is not None or pf1 is not None) else (a1, b1, True), pro_fold=pf1,
                           bias=c1.bias, bias_nc=eo.contiguous() if add else None,
                           want_stats=(add and ctx.tape is not None) or not fuse2,
                           wgt_tiled=w1t, gout=gg1, gn=gnreq, **pk)
@@ -656,11 +661,15 @@ class UNetEngine:
             a2, b2, mr2, t2 = ops.gn_fused_apply(h, None, g2.num_groups, g2.eps, g2.weight, g2.bias,
                                                  emb=eo if ss else None, emb_stride=es if ss else 0,
                                                  emb_mode=1 if ss else 0)
+        elif ctx.tape is None and not mat2 and halo2 and len(sp) == 2 and hst is not None and ops.HALO_FOLD:
+            a2 = b2 = mr2 = None   # forward only, halo conv2: GroupNorm-2 folded inside the conv (as conv1)
         elif ss:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias, emb=eo,
                                       emb_stride=es, emb_mode=1)
         else:
             a2, b2, mr2 = ops.gn_prep(hst, None, N, HW, Cout, 0, g2.num_groups, g2.eps, g2.weight, g2.bias)
+        pf2 = (dict(st0=hst, groups=g2.num_groups, eps=g2.eps, gamma=g2.weight, beta=g2.bias, emb=eo if ss else None,
+                    emb_stride=es if ss else 0) if a2 is None and t2 is None else None)
         sk = m.skip_connection
         kw = {}
         if isinstance(sk, Identity):
@@ -684,7 +693,8 @@ class UNetEngine:
             ops.dropout_apply(t2, drop, seed, salt, out=t2)
         gg2 = (torch.empty_like(h) if keep_g and t2 is None and halo2 and not point2 and Cout % HALO_BK == 0
                else None)
-        out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2, pro=None if t2 is not None else (a2, b2, True),
+        out, ost = ops.conv(t2 if t2 is not None else h, Cout, w2,
+                            pro=None if (t2 is not None or pf2 is not None) else (a2, b2, True), pro_fold=pf2,
                             bias=c2.bias, want_stats="free", wgt_tiled=w2t, gout=gg2, **kw)
         o = Act(out, ost)
         if ctx.tape is None:

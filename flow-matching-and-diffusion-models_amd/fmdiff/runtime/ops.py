@@ -261,6 +261,10 @@ SPLIT_STATS_ROWS = 16   # pixels per statistics row of a split-K conv (FMD_SPLIT
 # halo split-K on the small levels: ~HALO_SPLIT_WG workgroups, >= HALO_MIN_CHUNKS 32-channel chunks per split,
 # <= HALO_SPLIT_CAP splits (env overrides for A/B runs)
 HALO_SPLIT_WG = tuning.get("HALO_SPLIT_WG")
+# forward-only GroupNorm folded in the halo conv's prologue from the statistics slabs (fmd_conv_desc.fold_*) where
+# the slab has at most HALO_FOLD_MAX_ROWS rows per image (runtime/tuning.py)
+HALO_FOLD = bool(tuning.get("HALO_FOLD"))
+HALO_FOLD_MAX_ROWS = tuning.get("HALO_FOLD_MAX_ROWS")
 HALO_MIN_CHUNKS = tuning.get("HALO_MIN_CHUNKS")
 HALO_SPLIT_CAP = tuning.get("HALO_SPLIT_CAP")
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (tuning HALO_MIN_WG, applied at _lib load)
@@ -340,7 +344,8 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
          pro=None, src2=None, src3=None, wgt2=None, bias=None, bias2=None, bias_nc=None, resid=None, out=None,
          out_f32=False,
          accumulate=False, want_stats=False, ep=None, splits=None, force_generic=False, wgt_tiled=None,
-         wgt2_tiled=None, gout=None, s2d_tiled=None, gn=None) -> Tuple[torch.Tensor, Optional[Stats]]:
+         wgt2_tiled=None, gout=None, s2d_tiled=None, gn=None,
+         pro_fold=None) -> Tuple[torch.Tensor, Optional[Stats]]:
     """Implicit-GEMM conv (see csrc/conv.hip, csrc/conv_halo.hip).  ``pro=(a, b, silu)``, ``ep=(x0, x1, a, b)``.
     ``want_stats``: True = per-channel statistics of the output (a separate fmd_channel_stats pass when the
     kernel cannot emit them); "free" = only when the kernel emits them (else None: Act statistics are then
@@ -348,6 +353,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     ``gout``: bf16 tensor shaped like the (concatenated) input; the halo path writes the prologue's output
     G = SiLU(a*x+b) into it (the weight gradient's operand).  Requires ``pro``, (C0+C1) % 32 == 0 and a
     halo-eligible problem (:func:`halo_eligible`); raises otherwise.
+    ``pro_fold``: dict(st0=Stats, st1=Stats or None, groups, eps, gamma, beta[, emb, emb_stride], silu) -- a
+    forward-only GroupNorm prologue in place of ``pro``: on the halo path each workgroup folds its sample's affine
+    from the statistics slabs (fmd_conv_desc.fold_*, no gn_prep launch); elsewhere it is folded by :func:`gn_prep`
+    first and passed as ``pro``.
     ``gn``: dict(groups, eps, gamma, beta[, emb, emb_stride, emb_mode]) -- when the conv runs split-K and
     :func:`conv_gn_eligible` holds, its combine also computes the GroupNorm + SiLU of the output (fmd_conv_gn)
     and stores ``gn["res"] = (a, b, mean_rstd, t)`` as :func:`gn_fused_apply` returns them; otherwise ``gn`` is
@@ -413,8 +422,20 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
                               pro is not None, ztaps=3))
     else:
         halo = not force_generic and halo_eligible(N, Hs, Ho, Wo, K, ks, stride, pad, upsample, transposed,
-                                                   C0 + C1, pro is not None)
+                                                   C0 + C1, pro is not None or pro_fold is not None)
     d.force_generic = int(force_generic)
+    fold = None
+    if pro_fold is not None:
+        if pro is not None:
+            raise ValueError("conv: pro and pro_fold are exclusive")
+        rows_ok = all(st is None or (Hs * Ws) % st.rows == 0 and (Hs * Ws) // st.rows <= HALO_FOLD_MAX_ROWS
+                      for st in (pro_fold["st0"], pro_fold.get("st1")))
+        if halo and not d3 and gout is None and s2d_tiled is None and HALO_FOLD and rows_ok:
+            fold = pro_fold
+            _set_fold(d, fold)
+        else:
+            pro = _fold_now(pro_fold, N, Hs * Ws, C0, C1)
+            d.pro_a, d.pro_b, d.pro_silu = _p(pro[0]), _p(pro[1]), int(pro[2])
     if s2d_tiled is not None:   # stride-2 on the halo kernel: one launch, statistics in its epilogue
         ok = (s2d_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, ks, Ds, Do) if not transposed else
               (ks == 3 and pro is None and d2s_eligible(N, Hs, Ws, Ho, Wo, K, C0 + C1, Ds, Do)))
@@ -476,7 +497,13 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         _lib.call("fmd_conv_gn", C.byref(d), C.byref(g), stream())
         gn["res"] = (a, b, mr, t)
         return out, None
-    _lib.call("fmd_conv", C.byref(d), stream())
+    rc = int(_lib.lib().fmd_conv(C.byref(d), stream()))
+    if rc == -13 and fold is not None:   # the halo kernel did not take it: the fold as its own launch
+        pro = _fold_now(fold, N, Hs * Ws, C0, C1)
+        _clear_fold(d)
+        d.pro_a, d.pro_b, d.pro_silu = _p(pro[0]), _p(pro[1]), int(pro[2])
+        rc = int(_lib.lib().fmd_conv(C.byref(d), stream()))
+    _lib.check(rc, "fmd_conv")
     if want_stats == "free":   # only statistics the kernel emits for free; the consumer derives others lazily
         return out, st
     if want_stats and not fused_stats:
@@ -485,6 +512,32 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         else:
             st = channel_stats(out)
     return out, st
+
+
+def _set_fold(d, f):
+    d.fold_st0, d.fold_rows0 = _p(f["st0"].slab), f["st0"].rows
+    if f.get("st1") is not None:
+        d.fold_st1, d.fold_rows1 = _p(f["st1"].slab), f["st1"].rows
+    d.fold_G, d.fold_eps = f["groups"], float(f["eps"])
+    d.fold_gamma, d.fold_beta = _p(f.get("gamma")), _p(f.get("beta"))
+    emb = f.get("emb")
+    d.fold_emb = _p(emb)
+    d.fold_emb_stride = (f.get("emb_stride") or emb.shape[-1]) if emb is not None else 0
+    d.pro_silu = int(f.get("silu", True))
+
+
+def _clear_fold(d):
+    d.fold_st0 = d.fold_st1 = d.fold_gamma = d.fold_beta = d.fold_emb = None
+    d.fold_rows0 = d.fold_rows1 = d.fold_G = d.fold_emb_stride = 0
+
+
+def _fold_now(f, N, HW, C0, C1):
+    """(a, b, silu) of a pro_fold dict by fmd_gn_prep (the fold as its own launch)."""
+    emb = f.get("emb")
+    a, b, _ = gn_prep(f["st0"], f.get("st1"), N, HW, C0, C1, f["groups"], f["eps"], f.get("gamma"), f.get("beta"),
+                      emb=emb, emb_stride=(f.get("emb_stride") or emb.shape[-1]) if emb is not None else 0,
+                      emb_mode=1 if emb is not None else 0)
+    return a, b, bool(f.get("silu", True))
 
 
 CONV_SMALL_MODES = {"s1": 0, "s2": 1, "up": 2, "point": 3}

@@ -79,6 +79,21 @@ typedef struct fmd_conv_desc {
                                halo path -- the weight gradient's operand, so the backward does not recompute
                                the GroupNorm+SiLU.  Requires pro_a, (C0+C1) % 32 == 0 and the halo path (fmd_conv
                                returns -9 otherwise); NULL = off */
+  const float* fold_st0;    /* forward-only GroupNorm prologue folded in the halo kernel (2-D, csrc/conv_halo9.hip),
+                               in place of pro_a / pro_b: each workgroup computes its sample's affine from the
+                               producers' statistics slab of src0 [N*Hs*Ws/fold_rows0][C0][2] (and of src1), the
+                               groups, eps, gamma, beta and the scale-shift rows -- gn_prep's fold, without its
+                               launch.  fmd_conv returns -13 when the v9b halo kernel does not take the problem
+                               (the caller folds with fmd_gn_prep instead).  NULL = off */
+  int32_t fold_rows0;
+  const float* fold_st1;
+  int32_t fold_rows1;
+  int32_t fold_G;
+  float fold_eps;
+  const float* fold_gamma;  /* [C0 + C1] or NULL */
+  const float* fold_beta;
+  const float* fold_emb;    /* scale-shift norm: [N][fold_emb_stride] scale | shift, or NULL */
+  int32_t fold_emb_stride;
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the
