@@ -336,3 +336,32 @@ def test_conv_small_plan_is_a_host_query(monkeypatch):
     assert ops.conv_small_split((8, 32, 32, 128), 128, mode="s2", split=0) == 1             # 32 x 8 16-cout tiles
     assert ops.conv_small_split((8, 16, 16, 128), 128, C1=128, gn=gn, skip=(128, 128), split=0) == 1
     assert ops.conv_small_split((8, 8, 8, 256), 256, gn=gn, split=0) == 2                   # 8 x 16 tiles -> 256
+
+
+def test_small_level_caps_and_fold_descriptor(monkeypatch):
+    """Host logic of the round-6 forward paths: the fmd_conv_small level caps of runtime/tuning.py (pixels, and
+    pixels x input channels: config D's 16^2 level in, config B's 512-channel 16^2 level out), and the halo fold's
+    descriptor fields (set from a pro_fold dict, cleared for the gn_prep fallback)."""
+    from fmdiff import _lib
+    from fmdiff.runtime import ops, tuning
+    try:
+        _lib.lib()
+    except (OSError, RuntimeError) as e:
+        pytest.skip(f"library not loadable here: {e}")
+    assert tuning.get("SMALL_CONV_MAX_HW") == 256 and tuning.get("SMALL_CONV_MAX_WORK") == 65536
+    monkeypatch.setattr(ops, "SMALL_CONV", True)
+    st = ops.Stats(None, 64)
+    gn = dict(st0=st, st1=st, groups=32, eps=1e-6)
+    assert ops.conv_small_ok((8, 16, 16, 128), 128, C1=128, gn=gn)            # 256 px x 256 ch: D's 16^2 concat
+    assert not ops.conv_small_ok((8, 16, 16, 512), 512, gn=dict(gn, st1=None))  # 256 x 512: B's 16^2 level
+    assert ops.conv_small_ok((8, 8, 8, 256), 256, C1=256, gn=gn)              # 64 x 512
+    assert not ops.conv_small_ok((8, 32, 32, 128), 128, gn=dict(gn, st1=None))  # 1,024 px: above the pixel cap
+    d = _lib.ConvDesc()
+    slab0, slab1 = torch.zeros(4), torch.zeros(4)
+    f = dict(st0=ops.Stats(slab0, 64), st1=ops.Stats(slab1, 16), groups=32, eps=1e-5, gamma=None, beta=None,
+             emb=torch.zeros(8, 512), silu=True)
+    ops._set_fold(d, f)
+    assert d.fold_st0 == slab0.data_ptr() and d.fold_rows0 == 64 and d.fold_rows1 == 16 and d.fold_G == 32
+    assert abs(d.fold_eps - 1e-5) < 1e-12 and d.fold_emb_stride == 512 and d.pro_silu == 1
+    ops._clear_fold(d)
+    assert not d.fold_st0 and not d.fold_st1 and not d.fold_emb and d.fold_G == 0 and d.fold_rows0 == 0
