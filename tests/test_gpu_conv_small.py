@@ -261,3 +261,26 @@ def test_conv_small_split_combine(name):
         torch.cuda.synchronize()
         for P, i, o in got:
             assert torch.equal(o, solo[P][i]), (rep, P, i)
+
+
+def test_conv_small_split_combine_under_uneven_load():
+    """The in-launch combine with the chip busy elsewhere (MI355X_MICROARCH.md: test hand-offs under UNEVEN load):
+    a large GEMM runs on a second stream while the split convs are launched 30 times on this one, so the parts of a
+    tile start and finish at scattered times and the reducer may be any of them; every output equals the solo
+    result bit for bit."""
+    p = _make("s1_2_cat", seed=7)
+    x0 = p["x0"].to(DEV)
+    solo, _ = _run_small(p, 8, x0)
+    solo = solo.clone()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    a = torch.randn(8192, 8192, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            a = (a @ a).clamp_(-1, 1)
+    for _ in range(30):
+        outs.append(_run_small(p, 8, x0)[0])
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert torch.equal(o, solo), i
