@@ -866,11 +866,14 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   if (d->splits > 1 && (!d->ws || (d->stats && (!rows_ok || d->out_f32 || d->accumulate)))) return -5;
   (void)C;
   fmd_conv_desc dm = *d;
-  if (d->splits > 1) dm.stats = nullptr;
+  const bool tk = d->splits > 1 && d->tickets && combine;   // split-K combined inside the halo launch
+  if (!tk) dm.tickets = nullptr;
+  if (d->splits > 1 && !tk) dm.stats = nullptr;
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
     rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= HALO_MIN_WG (32) workgroups of 16x16 tiles (x splits)
   if (rc == 1 && d->fold_st0) return -13;   // the in-kernel GroupNorm fold runs only on the halo kernel
+  if (tk) return rc == 1 ? -14 : rc;        // the in-launch combine likewise (the caller splits the two-launch way)
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->gout) return -9;                            // the prologue side output exists only on the halo path

@@ -757,7 +757,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const bool d3 = d->Do > 0 || d->Ds > 0;
   if (d3 && d->Do != (d->upsample ? 2 * d->Ds : d->Ds)) return 1;   // 3-D: stride-1 3x3x3 (nearest-x2)
   const int Nn = d3 ? d->N * d->Do : d->N;                // images (3-D: depth slices)
-  if (d->splits > 1 && (!d->ws || d->stats)) return 1;
+  if (d->splits > 1 && (!d->ws || (d->stats && !d->tickets))) return 1;   // ticketed splits: statistics in the epilogue
   if (d->Ho % TH || d->Wo % TW) return 1;
   if (d->upsample ? (d->Ho != 2 * d->Hs || d->Wo != 2 * d->Ws) : (d->Ho != d->Hs || d->Wo != d->Ws)) return 1;
   if (!d->wgt_tiled || (d->src2 && !d->wgt2_tiled)) return 1;
@@ -798,7 +798,7 @@ extern "C" int fmd_conv_halo(const fmd_conv_desc* d, fmd_stream_t stream) {
   const int pro = d->pro_a || d->fold_st0 ? (d->pro_silu ? 2 : 1) : 0;
   {   // the v9b kernel (csrc/conv_halo9.hip) takes every problem it supports
     const int rc9 = halo9_launch(A, pro, stream);
-    if (rc9 != 1 || d->fold_st0) return rc9;   // the fold exists only in v9b
+    if (rc9 != 1 || d->fold_st0 || (d->tickets && A.splits > 1)) return rc9;   // the fold and the in-launch combine exist only in v9b
   }
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(nwg, A.splits);

@@ -574,7 +574,71 @@ void conv3x3_halo9b(const HArgs A) {
     const int cl = q ? ((pr - 18) & 15) : pr;
     return (2 * pb + q) * TW + cl;
   };
-  if (A.splits > 1) {
+  if constexpr (THT == 8 && MODE == 0) {   // (compiled only where its registers fit: the 8-row 3x3 tiles)
+  if (A.splits > 1 && d.tickets) {
+    // Split-K combined inside the launch (MI355X_MICROARCH.md, inter-workgroup visibility: a counter hand-off with a
+    // write-through payload; the same protocol as csrc/conv_small.hip).  Each part stores its accumulators in their
+    // register layout (16-byte pieces [part][pixel block][quarter][thread] of the tile's slab of d.ws) with sc1
+    // stores, every wave drains them, then ONE lane takes the tile's ticket; the part drawing splits - 1 resets it
+    // and sums the parts in part order (its own from registers, the same values it stored), so the result does not
+    // depend on which part arrives last, then runs the unsplit epilogue below.
+    constexpr int SLOT = NPB * 16;   // floats per thread and part
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(d.ws + (size_t)b * A.splits * NT9 * SLOT, 0,
+                                                      A.splits * NT9 * SLOT * 4, 0x00020000);
+    auto piece = [&](int s, int pb, int j) { return (((s * NPB + pb) * 4 + j) * NT9 + tid) * 16; };
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = f32x4{acc[pb][4 * j], acc[pb][4 * j + 1], acc[pb][4 * j + 2], acc[pb][4 * j + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, piece(split, pb, j), 0, 16);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* const last = (int*)coef;   // the affine table is dead after the chunk loop; the epilogue does not touch it
+    if (tid == 0) {
+      auto* tk = (__attribute__((address_space(1))) unsigned*)(d.tickets + b);
+      const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = t == (unsigned)(A.splits - 1);
+      if (is_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = is_last;
+    }
+    __syncthreads();
+    if (!*last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x16 tot[NPB];
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tot[pb][e] = 0.f;
+    for (int s = 0; s < A.splits; ++s) {
+      if (s == split) {
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) tot[pb] += acc[pb];
+      } else {
+        u32x4 v[NPB * 4];
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[pb * 4 + j] = __builtin_amdgcn_raw_buffer_load_b128(rs, piece(s, pb, j), 0, 16);
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 f = __builtin_bit_cast(f32x4, v[pb * 4 + j]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tot[pb][4 * j + e] += f[e];
+          }
+      }
+    }
+    const float bv = epi[32 * wid + r];   // the summed bias, after the parts
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[pb][e] = tot[pb][e] + bv;
+  }
+  }
+  if (A.splits > 1 && !(THT == 8 && MODE == 0 && d.tickets)) {
     float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
     const int co = co0 + 32 * wid + r;
     if (co < K) {
@@ -741,9 +805,12 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const fmd_conv_desc* d = &A.d;
   if (d->gout) return 1;
   if (d->upsample && d->src2) return 1;
-  if (A.splits <= 1 && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
+  const bool tk = A.splits > 1 && d->tickets;   // split-K with the in-launch combine and the unsplit epilogue
+  if ((A.splits <= 1 || tk) && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
   if (A.splits > 1 && (d->out_f32 || d->accumulate)) return 1;
+  if (tk && (A.depth || d->n_tickets < (long long)A.d.N * A.tiles_x * (d->Ho / 8) * A.ntc)) return 1;
   const long long nwg16 = (long long)A.d.N * A.tiles_x * A.tiles_y * A.ntc * A.splits;
+  if (tk && !(nwg16 < g_th8_max_wg && d->Ho % 8 == 0)) return 1;   // the combine exists in the 8-row instances only
   if (nwg16 < g_th8_max_wg && d->Ho % 8 == 0) {
     HArgs A8 = A;
     A8.tiles_y = d->Ho / 8;

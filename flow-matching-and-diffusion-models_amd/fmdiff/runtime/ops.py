@@ -265,6 +265,9 @@ HALO_SPLIT_WG = tuning.get("HALO_SPLIT_WG")
 # the slab has at most HALO_FOLD_MAX_ROWS rows per image (runtime/tuning.py)
 HALO_FOLD = bool(tuning.get("HALO_FOLD"))
 HALO_FOLD_MAX_ROWS = tuning.get("HALO_FOLD_MAX_ROWS")
+# split-K halo convs (2-D) combine their parts inside the launch (fmd_conv_desc.tickets; statistics from the conv
+# epilogue with 64-pixel rows) instead of the splitk_reduce_rows launch
+HALO_TICKET = bool(tuning.get("HALO_TICKET"))
 HALO_MIN_CHUNKS = tuning.get("HALO_MIN_CHUNKS")
 HALO_SPLIT_CAP = tuning.get("HALO_SPLIT_CAP")
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (tuning HALO_MIN_WG, applied at _lib load)
@@ -474,12 +477,17 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.ws, d.splits = _p(ws), splits
     else:
         d.splits = 1
+    # the halo kernel's in-launch combine (mirrors halo9_launch's conditions: 2-D, whole 128-cout tiles, the unsplit
+    # epilogue's forms)
+    ticket = (halo and splits > 1 and HALO_TICKET and not d3 and K % 128 == 0 and not out_f32 and not accumulate
+              and not (resid is not None and ep is not None))
     st = None
-    # statistics from the conv epilogue (no split) or from the split-K combine (csrc/conv.hip splitk_reduce_rows)
+    # statistics from the conv epilogue (no split, or the in-launch combine) or from the split-K combine launch
+    # (csrc/conv.hip splitk_reduce_rows)
     fused_stats = want_stats and (max(Do, 1) * Ho * Wo) % 64 == 0 and (
         (splits == 1 and M % bpx == 0) or (splits > 1 and K % 4 == 0 and not out_f32 and not accumulate))
     if fused_stats:
-        rows = 64 if splits == 1 else SPLIT_STATS_ROWS
+        rows = 64 if splits == 1 or ticket else SPLIT_STATS_ROWS
         slab = torch.empty((M // rows, K, 2), device=dev, dtype=F32)
         d.stats = _p(slab)
         st = Stats(slab, rows)
@@ -497,7 +505,16 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         _lib.call("fmd_conv_gn", C.byref(d), C.byref(g), stream())
         gn["res"] = (a, b, mr, t)
         return out, None
+    if ticket:
+        d.tickets, d.n_tickets = _p(_small_workspace(dev)[1]), SMALL_TICKETS
     rc = int(_lib.lib().fmd_conv(C.byref(d), stream()))
+    if rc == -14:   # the halo kernel did not take the in-launch combine: the combine launch (16-pixel statistics rows)
+        d.tickets, d.n_tickets = None, 0
+        if st is not None:
+            slab = torch.empty((M // SPLIT_STATS_ROWS, K, 2), device=dev, dtype=F32)
+            d.stats = _p(slab)
+            st = Stats(slab, SPLIT_STATS_ROWS)
+        rc = int(_lib.lib().fmd_conv(C.byref(d), stream()))
     if rc == -13 and fold is not None:   # the halo kernel did not take it: the fold as its own launch
         pro = _fold_now(fold, N, Hs * Ws, C0, C1)
         _clear_fold(d)

@@ -94,6 +94,12 @@ typedef struct fmd_conv_desc {
   const float* fold_beta;
   const float* fold_emb;    /* scale-shift norm: [N][fold_emb_stride] scale | shift, or NULL */
   int32_t fold_emb_stride;
+  int32_t* tickets;         /* split-K combined inside the halo launch (2-D v9b, splits > 1): [n_tickets] arrival
+                               counters, zero on entry and left zero; d->ws holds the parts' fp32 tiles (same
+                               [splits][M][K] size) and the statistics come from the conv epilogue with 64-pixel
+                               rows.  fmd_conv returns -14 when the halo kernel does not take the problem this way
+                               (the caller runs the two-launch split instead).  NULL = the separate combine launch */
+  int32_t n_tickets;
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the
