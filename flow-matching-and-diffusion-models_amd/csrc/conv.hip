@@ -306,7 +306,66 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(const KArgs A) {
 
   // ------------------------------------------------------------ epilogue
   const int K = d.K;
-  if (d.splits > 1) {
+  if constexpr (!GNA) {
+  if (d.splits > 1 && d.tickets) {
+    // Split-K combined inside the launch (the protocol of csrc/conv_halo9.hip / conv_small.hip: MI355X_MICROARCH.md,
+    // inter-workgroup visibility, a counter hand-off with a write-through payload).  Each part stores its
+    // accumulators in their register layout (16-byte pieces [part][i][j][thread] of the tile's slab of d.ws, sc1),
+    // drains, one lane takes the tile's ticket; the part drawing the last one resets it, sums the parts in part order
+    // (its own from registers) and runs the unsplit epilogue below.  The launcher admits whole tiles only.
+    constexpr int SLOT = TM * TN * 4;   // floats per thread and part
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(d.ws + (size_t)b * d.splits * NT * SLOT, 0,
+                                                      d.splits * NT * SLOT * 4, 0x00020000);
+    auto piece = [&](int s, int i, int j) { return (((s * TM + i) * TN + j) * NT + tid) * 16; };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, piece(split, i, j), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* const last = (int*)lds;   // the staging buffers are dead after the main loop; the epilogue does not use them
+    if (tid == 0) {
+      auto* tk = (__attribute__((address_space(1))) unsigned*)(d.tickets + b);
+      const unsigned t = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = t == (unsigned)(d.splits - 1);
+      if (is_last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = is_last;
+    }
+    __syncthreads();
+    if (!*last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x4 tot[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int s = 0; s < d.splits; ++s) {
+      if (s == split) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) tot[i][j] += acc[i][j];
+      } else {
+        u32x4 v[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, piece(s, i, j), 0, 16);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) tot[i][j] += __builtin_bit_cast(f32x4, v[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = tot[i][j];
+  }
+  }
+  if (d.splits > 1 && !(!GNA && d.tickets)) {
     float* ws = d.ws + (size_t)split * A.Mfull * K;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -834,11 +893,21 @@ int launch(const fmd_conv_desc* d, hipStream_t s, const fmd_gn_apply_desc* g = n
   A.ntp = (A.M + BPX - 1) / BPX;
   A.ntc = (d->K + BCO - 1) / BCO;
   A.stats_rows = 64;
+  // split-K combined inside the launch (d->tickets): whole tiles, no parity classes; the statistics then come from the
+  // unsplit epilogue with one row per wave's pixel range (BPX / WN pixels)
+  const bool tk = splits > 1 && d->tickets;
+  if (tk && (GNA || A.par || A.M % BPX || d->K % BCO || d->out_f32 || d->accumulate ||
+             d->n_tickets < A.ntp * A.ntc))
+    return -14;
   if (d->stats) {
     // every wave's pixel range must be one image and full
     const int wrows = BPX / WN;
-    if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1 || (A.par && HWq % 64))
+    if (tk) {
+      if ((Dz * d->Ho * d->Wo) % wrows != 0 || d->tickets_rows != wrows) return -14;
+      A.stats_rows = wrows;
+    } else if (wrows != 64 || (Dz * d->Ho * d->Wo) % 64 != 0 || A.M % BPX != 0 || splits > 1 || (A.par && HWq % 64)) {
       return -11;
+    }
   }
   dim3 grid(A.ntp * A.ntc, splits, A.par ? (d->Do > 0 ? 8 : 4) : 1);
   hipLaunchKernelGGL((conv_igemm<BCO, BPX, WM, WN, BK, GNA>), grid, dim3(256), 0, s, A);
@@ -866,14 +935,15 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   if (d->splits > 1 && (!d->ws || (d->stats && (!rows_ok || d->out_f32 || d->accumulate)))) return -5;
   (void)C;
   fmd_conv_desc dm = *d;
-  const bool tk = d->splits > 1 && d->tickets && combine;   // split-K combined inside the halo launch
+  const bool tk = d->splits > 1 && d->tickets && combine;   // split-K combined inside the launch
   if (!tk) dm.tickets = nullptr;
   if (d->splits > 1 && !tk) dm.stats = nullptr;
   int rc = 1;
   if (d->K > 16 && !d->force_generic)
     rc = fmd_conv_halo(&dm, stream);   // 3x3 stride-1 problems with >= HALO_MIN_WG (32) workgroups of 16x16 tiles (x splits)
   if (rc == 1 && d->fold_st0) return -13;   // the in-kernel GroupNorm fold runs only on the halo kernel
-  if (tk) return rc == 1 ? -14 : rc;        // the in-launch combine likewise (the caller splits the two-launch way)
+  // a ticketed problem the halo kernel declined runs ticketed on the implicit GEMM, or not at all (-14: the caller
+  // splits the two-launch way; the statistics' row size differs)
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->gout) return -9;                            // the prologue side output exists only on the halo path
@@ -889,7 +959,7 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
       rc = launch<128, 128, 2, 2, 64>(&dm, s);
   }
   if (rc) return rc;
-  if (d->splits > 1 && combine) {
+  if (d->splits > 1 && combine && !tk) {
     if (rows_ok) {
       hipLaunchKernelGGL(splitk_reduce_rows, dim3(M / FMD_SPLIT_STATS_ROWS, (d->K + 63) / 64), dim3(256), 0, s, *d, M);
     } else {

@@ -808,7 +808,9 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const bool tk = A.splits > 1 && d->tickets;   // split-K with the in-launch combine and the unsplit epilogue
   if ((A.splits <= 1 || tk) && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
   if (A.splits > 1 && (d->out_f32 || d->accumulate)) return 1;
-  if (tk && (A.depth || d->n_tickets < (long long)A.d.N * A.tiles_x * (d->Ho / 8) * A.ntc)) return 1;
+  if (tk && (A.depth || d->n_tickets < (long long)A.d.N * A.tiles_x * (d->Ho / 8) * A.ntc ||
+             (d->stats && d->tickets_rows != 64)))
+    return 1;
   const long long nwg16 = (long long)A.d.N * A.tiles_x * A.tiles_y * A.ntc * A.splits;
   if (tk && !(nwg16 < g_th8_max_wg && d->Ho % 8 == 0)) return 1;   // the combine exists in the 8-row instances only
   if (nwg16 < g_th8_max_wg && d->Ho % 8 == 0) {

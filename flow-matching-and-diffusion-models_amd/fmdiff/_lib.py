@@ -31,7 +31,7 @@ class ConvDesc(C.Structure):
         ("Ds", i32), ("Do", i32), ("gout", p),
         ("fold_st0", p), ("fold_rows0", i32), ("fold_st1", p), ("fold_rows1", i32), ("fold_G", i32),
         ("fold_eps", f32), ("fold_gamma", p), ("fold_beta", p), ("fold_emb", p), ("fold_emb_stride", i32),
-        ("tickets", p), ("n_tickets", i32),
+        ("tickets", p), ("n_tickets", i32), ("tickets_rows", i32),
     ]
 
 

@@ -268,6 +268,7 @@ HALO_FOLD_MAX_ROWS = tuning.get("HALO_FOLD_MAX_ROWS")
 # split-K halo convs (2-D) combine their parts inside the launch (fmd_conv_desc.tickets; statistics from the conv
 # epilogue with 64-pixel rows) instead of the splitk_reduce_rows launch
 HALO_TICKET = bool(tuning.get("HALO_TICKET"))
+SPLIT_TICKET = bool(tuning.get("SPLIT_TICKET"))   # the implicit GEMM's split-K likewise (whole tiles)
 HALO_MIN_CHUNKS = tuning.get("HALO_MIN_CHUNKS")
 HALO_SPLIT_CAP = tuning.get("HALO_SPLIT_CAP")
 # fewest halo workgroups (tiles x splits); mirrors fmd_halo_set_min_workgroups (tuning HALO_MIN_WG, applied at _lib load)
@@ -477,17 +478,25 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.ws, d.splits = _p(ws), splits
     else:
         d.splits = 1
-    # the halo kernel's in-launch combine (mirrors halo9_launch's conditions: 2-D, whole 128-cout tiles, the unsplit
-    # epilogue's forms)
-    ticket = (halo and splits > 1 and HALO_TICKET and not d3 and K % 128 == 0 and not out_f32 and not accumulate
-              and not (resid is not None and ep is not None))
+    # split-K combined inside the conv launch (fmd_conv_desc.tickets), mirroring the kernels' conditions -- the halo
+    # kernel: 2-D, whole 128-cout tiles, the unsplit epilogue's forms, statistics rows of 64 pixels; the implicit GEMM:
+    # 2-D, whole pixel and cout tiles, no parity classes, one statistics row per wave (bpx / 2 pixels, 64 for K <= 16)
+    par = transposed and stride == 2 and ks == 3 and pad == 1 and Ho % 2 == 0 and Wo % 2 == 0
+    if halo:
+        ticket = (splits > 1 and HALO_TICKET and not d3 and K % 128 == 0 and not out_f32 and not accumulate
+                  and not (resid is not None and ep is not None))
+        trows = 64
+    else:
+        ticket = (splits > 1 and SPLIT_TICKET and not d3 and not par and M % bpx == 0 and K % bco == 0
+                  and not out_f32 and not accumulate)
+        trows = 64 if K <= 16 else bpx // 2
     st = None
     # statistics from the conv epilogue (no split, or the in-launch combine) or from the split-K combine launch
     # (csrc/conv.hip splitk_reduce_rows)
     fused_stats = want_stats and (max(Do, 1) * Ho * Wo) % 64 == 0 and (
         (splits == 1 and M % bpx == 0) or (splits > 1 and K % 4 == 0 and not out_f32 and not accumulate))
     if fused_stats:
-        rows = 64 if splits == 1 or ticket else SPLIT_STATS_ROWS
+        rows = 64 if splits == 1 else trows if ticket else SPLIT_STATS_ROWS
         slab = torch.empty((M // rows, K, 2), device=dev, dtype=F32)
         d.stats = _p(slab)
         st = Stats(slab, rows)
@@ -506,10 +515,10 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         gn["res"] = (a, b, mr, t)
         return out, None
     if ticket:
-        d.tickets, d.n_tickets = _p(_small_workspace(dev)[1]), SMALL_TICKETS
+        d.tickets, d.n_tickets, d.tickets_rows = _p(_small_workspace(dev)[1]), SMALL_TICKETS, trows
     rc = int(_lib.lib().fmd_conv(C.byref(d), stream()))
     if rc == -14:   # the halo kernel did not take the in-launch combine: the combine launch (16-pixel statistics rows)
-        d.tickets, d.n_tickets = None, 0
+        d.tickets, d.n_tickets, d.tickets_rows = None, 0, 0
         if st is not None:
             slab = torch.empty((M // SPLIT_STATS_ROWS, K, 2), device=dev, dtype=F32)
             d.stats = _p(slab)

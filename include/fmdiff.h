@@ -60,7 +60,8 @@ typedef struct fmd_conv_desc {
   int32_t out_f32;
   int32_t accumulate;       /* out += result */
   float* stats;             /* slab [M/64][K][2] of per-64-pixel partial sums, or NULL; with splits > 1
-                               [M/FMD_SPLIT_STATS_ROWS][K][2] (written by the split-K combine) */
+                               [M/FMD_SPLIT_STATS_ROWS][K][2] (written by the split-K combine), or
+                               [M/tickets_rows][K][2] when the split is combined inside the launch (tickets) */
   const void* ep_x0;        /* data-gradient epilogue: x = forward GN input at (p, c); if ep_a: */
                             /*   out *= silu'(ep_a*x+ep_b); stats become (sum out, sum out*x) */
   const void* ep_x1;
@@ -94,12 +95,15 @@ typedef struct fmd_conv_desc {
   const float* fold_beta;
   const float* fold_emb;    /* scale-shift norm: [N][fold_emb_stride] scale | shift, or NULL */
   int32_t fold_emb_stride;
-  int32_t* tickets;         /* split-K combined inside the halo launch (2-D v9b, splits > 1): [n_tickets] arrival
-                               counters, zero on entry and left zero; d->ws holds the parts' fp32 tiles (same
-                               [splits][M][K] size) and the statistics come from the conv epilogue with 64-pixel
-                               rows.  fmd_conv returns -14 when the halo kernel does not take the problem this way
-                               (the caller runs the two-launch split instead).  NULL = the separate combine launch */
+  int32_t* tickets;         /* split-K (splits > 1) combined inside the conv launch (2-D: the v9b halo kernel or the
+                               implicit GEMM on whole tiles): [n_tickets] arrival counters, zero on entry and left
+                               zero; d->ws holds the parts' fp32 tiles (same [splits][M][K] size) and the statistics
+                               come from the conv epilogue, one row per tickets_rows pixels (64 on the halo kernel,
+                               the wave's pixel range on the implicit GEMM).  fmd_conv returns -14 when the kernel
+                               that takes the problem cannot combine it so or would write other rows (the caller then
+                               runs the two-launch split).  NULL = the separate combine launch */
   int32_t n_tickets;
+  int32_t tickets_rows;     /* pixels per statistics row the caller allocated for a ticketed conv with stats */
 } fmd_conv_desc;
 
 /* Dispatches 3x3 stride-1 forward-gather problems with >= 128 16x16 output tiles to the

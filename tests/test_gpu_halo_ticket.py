@@ -102,3 +102,67 @@ def test_halo_ticket_combine_under_uneven_load(monkeypatch):
         got, sgot = O.conv(x0, K, w, want_stats=True, **kw)
         assert torch.equal(got, ref) and torch.equal(sgot.slab, sref.slab), i
     torch.cuda.synchronize()
+
+
+# implicit-GEMM problems that run split-K (csrc/conv.hip conv_igemm): name -> (N, Hs, C, K, ks, stride, transposed,
+# extras); every one with whole tiles, so ticketed (statistics one row per wave: bpx / 2 pixels, 64 for K <= 64)
+GEN = {
+    "s2_32to16": (8, 32, 256, 256, 3, 2, False, ("pro",)),
+    "pw_8": (8, 8, 512, 512, 1, 1, False, ("resid",)),
+    "s1_4_tiny": (8, 4, 512, 512, 3, 1, False, ("pro", "bias_nc")),
+    "k64_16": (8, 16, 256, 64, 3, 1, False, ("pro", "generic")),
+    "generic_32_resid": (8, 32, 256, 256, 3, 1, False, ("pro", "resid", "generic")),
+    "dgrad_t_16": (8, 16, 512, 256, 3, 1, True, ("ep",)),
+}
+
+
+def _gen_args(name, O):
+    N, Hs, C, K, ks, st, tr, ex = GEN[name]
+    g = torch.Generator().manual_seed(sum(map(ord, name)) + 7)
+    Ho = Hs // st if ks == 3 and st == 2 else Hs
+
+    def r(*s, sc=1.0):
+        return (torch.randn(*s, generator=g) * sc).to(DEV)
+
+    x0 = r(N, Hs, Hs, C).to(torch.bfloat16)
+    wt = r(K, C, ks, ks, sc=1 / (ks * C ** 0.5))
+    w = O.prep_weights(wt.transpose(0, 1).contiguous(), 1) if tr else O.prep_weights(wt, 0)
+    kw = dict(ks=ks, stride=st, pad=ks // 2, transposed=tr, bias=r(K, sc=0.1), force_generic="generic" in ex)
+    if tr:   # data gradient of a stride-1 3x3 conv over K -> C: the weights of its forward, transposed gather
+        kw["bias"] = None
+    if "pro" in ex:
+        kw["pro"] = ((torch.rand(N, C, generator=g) + 0.5).to(DEV), r(N, C, sc=0.2), True)
+    if "bias_nc" in ex:
+        kw["bias_nc"] = r(N, K, sc=0.1)
+    if "resid" in ex:
+        kw["resid"] = r(N, Ho, Ho, K).to(torch.bfloat16)
+    if "ep" in ex:
+        kw["ep"] = (r(N, Ho, Ho, K).to(torch.bfloat16), None, (torch.rand(N, K, generator=g) + 0.5).to(DEV),
+                    r(N, K, sc=0.2))
+    return x0, w, kw, (N, Ho, K)
+
+
+@pytest.mark.parametrize("name", list(GEN))
+def test_split_ticket_combine_implicit_gemm(name, monkeypatch):
+    from fmdiff.runtime import ops as O
+    x0, w, kw, (N, Ho, K) = _gen_args(name, O)
+    K_out = K
+    monkeypatch.setattr(O, "SPLIT_TICKET", True)
+    a, sa = O.conv(x0, K_out, w, want_stats=True, **kw)
+    a2, sa2 = O.conv(x0, K_out, w, want_stats=True, **kw)
+    monkeypatch.setattr(O, "SPLIT_TICKET", False)
+    b, sb = O.conv(x0, K_out, w, want_stats=True, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a2) and torch.equal(sa.slab, sa2.slab)
+    af, bf = a.float(), b.float()
+    err = (af - bf).abs().max().item()
+    assert err <= 8e-3 * bf.abs().max().item(), (name, err)
+    if (Ho * Ho) % 64 == 0:   # statistics from the kernel (else a separate channel_stats pass, not under test)
+        # the off run took the two-launch split (16-pixel rows), the on run the ticketed one (one row per wave)
+        assert sb.rows == O.SPLIT_STATS_ROWS and sa.rows in (32, 64), (sa.rows, sb.rows)
+        y = a.double().reshape(N, -1, K_out)
+        q = y * kw["ep"][0].double().reshape(N, -1, K_out) if "ep" in kw else y * y
+        tot = sa.slab.double().reshape(N, -1, K_out, 2).sum(1)
+        for c, t in ((0, y), (1, q)):
+            assert ((tot[..., c] - t.sum(1)).abs() <= 1e-5 * t.abs().sum(1) + 1e-6).all(), (name, c)
+    assert int(O._small_workspace(a.device)[1].abs().sum()) == 0
