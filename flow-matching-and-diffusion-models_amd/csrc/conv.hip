@@ -944,6 +944,7 @@ static int conv_run(const fmd_conv_desc* d, fmd_stream_t stream, bool combine) {
   if (rc == 1 && d->fold_st0) return -13;   // the in-kernel GroupNorm fold runs only on the halo kernel
   // a ticketed problem the halo kernel declined runs ticketed on the implicit GEMM, or not at all (-14: the caller
   // splits the two-launch way; the statistics' row size differs)
+  if (rc == 1 && tk && (!d->wgt || (d->src2 && !d->wgt2) || d->gout)) return -14;
   if (rc == 1) {
     if (!d->wgt || (d->src2 && !d->wgt2)) return -8;   // only halo tiles were supplied, but the halo path declined
     if (d->gout) return -9;                            // the prologue side output exists only on the halo path

@@ -102,7 +102,7 @@ FMD_DEV void fence8_(float (&y)[8]) {
 template <bool UP, int PRO, int MODE = 0, int THT = TH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void conv3x3_halo9b(const HArgs A) {
-  static_assert(THT == TH || THT == 8, "16- or 8-row tiles");
+  static_assert(THT == TH || THT == 8 || THT == 4, "16-, 8- or 4-row tiles");
   using G = G9<UP, THT>;
   constexpr int NPB = THT / 2;               // 32-pixel blocks (2 rows) per wave
   constexpr int OUT_T = THT * TW * BCO * 2;
@@ -412,8 +412,19 @@ void conv3x3_halo9b(const HArgs A) {
   // groups ahead of their MFMAs (sched_group_barrier: 8 reads, then 4 MFMAs + 4 reads per group), so each group's
   // LDS latency hides under the previous group's 4 x 32 MFMA cycles instead of every MFMA waiting on its read
   auto tap_mma = [&](int tap, int hb, const bf16x8 (&bq)[2]) {
-    constexpr int NG = NPB / 4;   // groups of 4 pixel blocks per k-half
     bf16x8 af[2 * NPB];
+    if constexpr (NPB < 4) {   // 4-row tiles: both k-halves' reads, then their MFMAs
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) af[s * NPB + pb] = *(const bf16x8*)(smem + hb + aoff(tap, s, pb));
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) acc[pb] = mfma32(af[s * NPB + pb], bq[s], acc[pb]);
+      return;
+    }
+    constexpr int NG = NPB / 4 > 0 ? NPB / 4 : 1;   // groups of 4 pixel blocks per k-half
 #pragma unroll
     for (int g = 0; g < 2 * NG; ++g)
 #pragma unroll
@@ -574,7 +585,7 @@ void conv3x3_halo9b(const HArgs A) {
     const int cl = q ? ((pr - 18) & 15) : pr;
     return (2 * pb + q) * TW + cl;
   };
-  if constexpr (THT == 8 && MODE == 0) {   // (compiled only where its registers fit: the 8-row 3x3 tiles)
+  if constexpr (THT <= 8 && MODE == 0) {   // (compiled only where its registers fit: the 8- and 4-row 3x3 tiles)
   if (A.splits > 1 && d.tickets) {
     // Split-K combined inside the launch (MI355X_MICROARCH.md, inter-workgroup visibility: a counter hand-off with a
     // write-through payload; the same protocol as csrc/conv_small.hip).  Each part stores its accumulators in their
@@ -638,7 +649,7 @@ void conv3x3_halo9b(const HArgs A) {
       for (int e = 0; e < 16; ++e) acc[pb][e] = tot[pb][e] + bv;
   }
   }
-  if (A.splits > 1 && !(THT == 8 && MODE == 0 && d.tickets)) {
+  if (A.splits > 1 && !(THT <= 8 && MODE == 0 && d.tickets)) {
     float* ws = d.ws + (size_t)split * d.N * Ho * Wo * K;
     const int co = co0 + 32 * wid + r;
     if (co < K) {
@@ -776,6 +787,10 @@ namespace {
 // grids of fewer workgroups than this (16-row tiles x splits) run 8-row tiles: at 128^2 / 64^2 a 16-row grid is one
 // round of 512 (or 256) workgroups whose prologues and epilogues all coincide (0 = never)
 int g_th8_max_wg = 1024;
+// 8-row grids (tiles x splits) of fewer workgroups than this run 4-row tiles (plain 3x3 only; 0 = never): the latent
+// UNet's 32^2 convs are 64 tiles x 2-4 parts on 256 CUs (config D 121.6 -> 124.8 (256) -> 126.5 img/s (512); 1024 takes
+// the config B sampler's 64^2 level too: 26.2 -> 25.5 img/s)
+int g_th4_max_wg = 512;
 
 template <int THT>
 int halo9_go(const HArgs& A, int pro, fmd_stream_t stream) {
@@ -808,17 +823,26 @@ int halo9_launch(const HArgs& A, int pro, fmd_stream_t stream) {
   const bool tk = A.splits > 1 && d->tickets;   // split-K with the in-launch combine and the unsplit epilogue
   if ((A.splits <= 1 || tk) && (d->K % BCO || d->out_f32 || d->accumulate || (d->resid && d->ep_x0))) return 1;
   if (A.splits > 1 && (d->out_f32 || d->accumulate)) return 1;
-  if (tk && (A.depth || d->n_tickets < (long long)A.d.N * A.tiles_x * (d->Ho / 8) * A.ntc ||
+  if (tk && (A.depth || d->n_tickets < (long long)A.d.N * A.tiles_x * (d->Ho / 4) * A.ntc ||
              (d->stats && d->tickets_rows != 64)))
     return 1;
   const long long nwg16 = (long long)A.d.N * A.tiles_x * A.tiles_y * A.ntc * A.splits;
-  if (tk && !(nwg16 < g_th8_max_wg && d->Ho % 8 == 0)) return 1;   // the combine exists in the 8-row instances only
+  if (tk && !(nwg16 < g_th8_max_wg && d->Ho % 8 == 0)) return 1;   // the combine exists in the 8- and 4-row instances
   if (nwg16 < g_th8_max_wg && d->Ho % 8 == 0) {
     HArgs A8 = A;
     A8.tiles_y = d->Ho / 8;
+    if (2 * nwg16 < g_th4_max_wg && !A.depth) {   // 4-row tiles: twice the 8-row grid, still under one round
+      A8.tiles_y = d->Ho / 4;
+      return halo9_go<4>(A8, pro, stream);
+    }
     return halo9_go<8>(A8, pro, stream);
   }
   return halo9_go<TH>(A, pro, stream);
+}
+
+extern "C" int fmd_halo_set_th4_max_workgroups(int32_t n) {
+  g_th4_max_wg = n < 0 ? 0 : n;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------------------------------------------

@@ -128,6 +128,7 @@ SIGNATURES = {
     "fmd_sched_step": [C.POINTER(SchedStepDesc), p],
     "fmd_halo_set_min_workgroups": [i32],
     "fmd_halo_set_th8_max_workgroups": [i32],
+    "fmd_halo_set_th4_max_workgroups": [i32],
     "fmd_conv_gn_set_block_channels": [i32],
     "fmd_gn_bwd_apply": [p, p, p, i32, i32, i64, i32, p, p, p, p, p, i32, p, i32, p],
     "fmd_prep_weights": [p, i32, i32, i32, i32, i32, i32, p, p],
@@ -200,6 +201,8 @@ def lib():
             check(L.fmd_halo_set_min_workgroups(tuning.get("HALO_MIN_WG")), "fmd_halo_set_min_workgroups")
         if tuning.overridden("HALO_TH8_MAX_WG"):
             check(L.fmd_halo_set_th8_max_workgroups(tuning.get("HALO_TH8_MAX_WG")), "fmd_halo_set_th8_max_workgroups")
+        if tuning.overridden("HALO_TH4_MAX_WG"):
+            check(L.fmd_halo_set_th4_max_workgroups(tuning.get("HALO_TH4_MAX_WG")), "fmd_halo_set_th4_max_workgroups")
         if tuning.overridden("CONV_GN_CB"):
             check(L.fmd_conv_gn_set_block_channels(tuning.get("CONV_GN_CB")), "fmd_conv_gn_set_block_channels")
         _lib = L

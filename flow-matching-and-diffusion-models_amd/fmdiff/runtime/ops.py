@@ -484,7 +484,7 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
     par = transposed and stride == 2 and ks == 3 and pad == 1 and Ho % 2 == 0 and Wo % 2 == 0
     if halo:
         ticket = (splits > 1 and HALO_TICKET and not d3 and K % 128 == 0 and not out_f32 and not accumulate
-                  and not (resid is not None and ep is not None))
+                  and not (resid is not None and ep is not None) and gout is None)
         trows = 64
     else:
         ticket = (splits > 1 and SPLIT_TICKET and not d3 and not par and M % bpx == 0 and K % bco == 0

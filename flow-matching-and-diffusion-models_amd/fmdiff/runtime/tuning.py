@@ -49,6 +49,7 @@ TABLE = {
     "HALO_SPLIT_CAP": (16, "halo conv split-K: most splits"),
     "HALO_MIN_WG": (32, "halo conv only from this many workgroups (tiles x cout tiles x splits) up"),
     "HALO_TH8_MAX_WG": (1024, "halo conv: 8-row tiles for grids of fewer 16-row workgroups than this (0: never)"),
+    "HALO_TH4_MAX_WG": (512, "halo conv: 4-row tiles for 8-row grids of fewer workgroups than this (0: never)"),
     "WGRAD_MIN_STEPS": (8, "generic weight gradient: at least this many 32-pixel steps per split"),
     "WGRAD_CU_MULT": (4, "generic weight gradient: target workgroups per CU"),
     "WGRAD_HALO_WG": (0, "halo weight gradient: target workgroups (0 = one per CU)"),

@@ -167,6 +167,9 @@ int fmd_halo_set_min_workgroups(int32_t n);
  * instead (twice the workgroups: the 128^2 / 64^2 levels would otherwise be one lock-step round); 0 = never.  A
  * tuning hook (tuning table HALO_TH8_MAX_WG). */
 int fmd_halo_set_th8_max_workgroups(int32_t n);
+/* 8-row grids (tiles x splits) with fewer workgroups than n (default 512) run 4-row tiles instead (plain 2-D 3x3:
+ * the latent UNet's 32^2 convs would otherwise fill half the CUs); 0 = never.  Tuning table HALO_TH4_MAX_WG. */
+int fmd_halo_set_th4_max_workgroups(int32_t n);
 /* Fewest channels per combine block of fmd_conv_gn (4, 8, 16, 32 or 64; default 4):
  * a block owns max(cb, K / G) channels = whole groups.  Returns -1 for any other value.  A tuning hook; the host's
  * conv_gn_eligible mirror reads ops.CONV_GN_CB. */

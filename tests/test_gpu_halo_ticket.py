@@ -166,3 +166,40 @@ def test_split_ticket_combine_implicit_gemm(name, monkeypatch):
         for c, t in ((0, y), (1, q)):
             assert ((tot[..., c] - t.sum(1)).abs() <= 1e-5 * t.abs().sum(1) + 1e-6).all(), (name, c)
     assert int(O._small_workspace(a.device)[1].abs().sum()) == 0
+
+
+# problems whose 8-row halo grid is under one round of the chip: 4-row tiles (fmd_halo_set_th4_max_workgroups)
+TH4 = {
+    "latent32_c128": (8, 32, 128, 0, 128, False, ("pro", "bias_nc")),
+    "latent32_skip_c128": (8, 32, 128, 0, 128, False, ("pro", "seg2")),
+    "up32_c128": (8, 32, 128, 0, 128, True, ("pro",)),
+    "b16_k256": (8, 16, 256, 0, 256, False, ("pro", "resid")),
+}
+
+
+@pytest.mark.parametrize("name", list(TH4))
+def test_halo_4row_tiles_match_8row(name, monkeypatch):
+    """4-row tiles accumulate every output element over the same (chunk, tap, k-half) sequence as 8-row tiles and
+    the split parts own the same chunks: outputs bit-identical, statistics rows the same 64-pixel blocks (permuted),
+    per-sample totals equal."""
+    from fmdiff import _lib
+    from fmdiff.runtime import ops as O, tuning
+    CASES[name] = TH4[name]
+    try:
+        x0, w, kw, (N, H, C, K) = _args(name, O)
+    finally:
+        del CASES[name]
+    L = _lib.lib()
+    outs = []
+    try:
+        for th4 in (tuning.get("HALO_TH4_MAX_WG"), 0):
+            assert L.fmd_halo_set_th4_max_workgroups(th4) == 0
+            outs.append(O.conv(x0, K, w, want_stats=True, **kw))
+            torch.cuda.synchronize()
+    finally:
+        L.fmd_halo_set_th4_max_workgroups(tuning.get("HALO_TH4_MAX_WG"))
+    (a, sa), (b, sb) = outs
+    assert torch.equal(a, b), name
+    ta = sa.slab.double().reshape(N, -1, K, 2).sum(1)
+    tb = sb.slab.double().reshape(N, -1, K, 2).sum(1)
+    assert torch.allclose(ta, tb, rtol=1e-12, atol=1e-9), name
