@@ -1036,14 +1036,21 @@ class UNetEngine:
         if t_steps is None:
             return
         S = t_steps.shape[0]
-        t_all = t_steps.float().repeat_interleave(N)      # row i*N + n = step i, sample n
+        # every sample of a step shares its t: the MLP runs once per step (its kernels are row-independent, so
+        # each row is bit-identical to a per-sample evaluation) and row i of the table holds N copies
+        # (i*N + n = step i, sample n) -- 8x fewer launches than one row per (step, sample)
+        t_u = t_steps.float().contiguous()
         embs, eos = [], []
-        for r0 in range(0, S * N, 32):                    # the linear kernels take <= 32 rows per launch
-            ctx = self.time_mlp(t_all[r0:r0 + 32].contiguous(), False, min(32, S * N - r0))
+        for r0 in range(0, S, 32):                        # the linear kernels take <= 32 rows per launch
+            ctx = self.time_mlp(t_u[r0:r0 + 32].contiguous(), False, min(32, S - r0))
             embs.append(ctx.emb)
             eos.append(ctx.eo_all)
-        emb = torch.cat(embs).view(S, -1)
-        eo = torch.cat(eos).view(S, -1) if eos[0] is not None else None
+
+        def per_sample(x):
+            return x[:, None, :].expand(S, N, x.shape[1]).reshape(S, -1)
+
+        emb = per_sample(torch.cat(embs))
+        eo = per_sample(torch.cat(eos)) if eos[0] is not None else None
         self._tt = dict(N=N, index=index, emb=emb, eo=eo, emb_cols=embs[0].shape[1],
                         eo_cols=eos[0].shape[1] if eo is not None else 0)
 

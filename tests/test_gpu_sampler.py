@@ -111,3 +111,25 @@ def test_fused_ddpm_sampler_graph_reuse_draws_fresh_noise(golden):
     assert fs._graph is graph and not torch.equal(a, b)
     c = FusedSampler(model, _sched("ddpm"), 6).sample(init, cond, generator=torch.Generator(DEV).manual_seed(2))
     assert torch.equal(b, c)
+
+
+def test_time_table_rows_equal_per_sample_mlp(golden):
+    """The sampler's precomputed time-embedding table (engine.set_time_table) evaluates the time MLP and the
+    grouped ResBlock projections once per step and repeats each row for the N samples of the batch; every
+    (step, sample) row must equal the MLP evaluated on that sample's own t, bit for bit (the kernels are
+    row-independent)."""
+    from fmdiff.pipelines.train.fused import FusedFlowSampler
+    model, _ = _model(golden)
+    sampler = FusedFlowSampler(model, 7)
+    eng = sampler.eng
+    N = 3
+    ts = torch.linspace(999.0, 11.0, 7, device=DEV)
+    idx = torch.zeros(1, device=DEV, dtype=torch.int32)
+    eng.set_time_table(ts, N, idx)
+    tt = eng._tt
+    eng.set_time_table(None)
+    with torch.no_grad():
+        ctx = eng.time_mlp(ts.repeat_interleave(N).contiguous(), False, 7 * N)
+    assert torch.equal(tt["emb"].view(7 * N, -1), ctx.emb)
+    if tt["eo"] is not None:
+        assert torch.equal(tt["eo"].view(7 * N, -1), ctx.eo_all)
