@@ -478,18 +478,9 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         d.ws, d.splits = _p(ws), splits
     else:
         d.splits = 1
-    # split-K combined inside the conv launch (fmd_conv_desc.tickets), mirroring the kernels' conditions -- the halo
-    # kernel: 2-D, whole 128-cout tiles, the unsplit epilogue's forms, statistics rows of 64 pixels; the implicit GEMM:
-    # 2-D, whole pixel and cout tiles, no parity classes, one statistics row per wave (bpx / 2 pixels, 64 for K <= 16)
-    par = transposed and stride == 2 and ks == 3 and pad == 1 and Ho % 2 == 0 and Wo % 2 == 0
-    if halo:
-        ticket = (splits > 1 and HALO_TICKET and not d3 and K % 128 == 0 and not out_f32 and not accumulate
-                  and not (resid is not None and ep is not None) and gout is None)
-        trows = 64
-    else:
-        ticket = (splits > 1 and SPLIT_TICKET and not d3 and not par and M % bpx == 0 and K % bco == 0
-                  and not out_f32 and not accumulate)
-        trows = 64 if K <= 16 else bpx // 2
+    ticket, trows = split_ticket(halo, splits, K, M, bpx, bco, d3=d3, transposed=transposed, stride=stride, ks=ks,
+                                 pad=pad, Ho=Ho, Wo=Wo, out_f32=out_f32, accumulate=accumulate,
+                                 resid_and_ep=resid is not None and ep is not None, gout=gout is not None)
     st = None
     # statistics from the conv epilogue (no split, or the in-launch combine) or from the split-K combine launch
     # (csrc/conv.hip splitk_reduce_rows)
@@ -538,6 +529,22 @@ def conv(src0, K, wgt, *, src1=None, ks=3, stride=1, pad=1, upsample=False, tran
         else:
             st = channel_stats(out)
     return out, st
+
+
+def split_ticket(halo, splits, K, M, bpx, bco, *, d3=False, transposed=False, stride=1, ks=3, pad=1, Ho=0, Wo=0,
+                 out_f32=False, accumulate=False, resid_and_ep=False, gout=False):
+    """(ticket, rows): whether a split-K conv combines its parts inside the launch (fmd_conv_desc.tickets), and the
+    pixels per statistics row its epilogue then writes -- mirroring the kernels' conditions.  The halo kernel
+    (csrc/conv_halo9.hip halo9_launch): 2-D, whole 128-cout tiles, the unsplit epilogue's forms, no G side output,
+    rows of 64 pixels.  The implicit GEMM (csrc/conv.hip launch): 2-D, whole pixel and cout tiles, no parity classes
+    (transposed stride-2 3x3), one row per wave's pixels (bpx / 2; 64 for K <= 16, whose tile has 4 waves across)."""
+    if splits <= 1 or d3 or out_f32 or accumulate:
+        return False, 0
+    if halo:
+        return bool(HALO_TICKET and K % 128 == 0 and not resid_and_ep and not gout), 64
+    par = transposed and stride == 2 and ks == 3 and pad == 1 and Ho % 2 == 0 and Wo % 2 == 0
+    ok = SPLIT_TICKET and not par and M % bpx == 0 and K % bco == 0
+    return bool(ok), (64 if K <= 16 else bpx // 2)
 
 
 def _set_fold(d, f):

@@ -365,3 +365,31 @@ def test_small_level_caps_and_fold_descriptor(monkeypatch):
     assert abs(d.fold_eps - 1e-5) < 1e-12 and d.fold_emb_stride == 512 and d.pro_silu == 1
     ops._clear_fold(d)
     assert not d.fold_st0 and not d.fold_st1 and not d.fold_emb and d.fold_G == 0 and d.fold_rows0 == 0
+
+
+def test_split_ticket_decision_mirrors_the_kernels(monkeypatch):
+    """runtime/ops.split_ticket: which split-K convs combine inside their launch and the statistics rows they then
+    write (the kernels return -14 otherwise, tests/test_gpu_halo_ticket.py): the halo kernel on whole 128-cout tiles
+    with 64-pixel rows, never with a G side output, a residual + data-gradient epilogue, 3-D or fp32 / accumulating
+    outputs; the implicit GEMM (opt-in, SPLIT_TICKET) on whole tiles without parity classes, one row per wave."""
+    from fmdiff.runtime import ops
+    monkeypatch.setattr(ops, "HALO_TICKET", True)
+    monkeypatch.setattr(ops, "SPLIT_TICKET", False)
+    st = ops.split_ticket
+    assert st(True, 2, 128, 8192, 256, 128) == (True, 64)             # latent 32^2 ResBlock conv
+    assert st(True, 1, 128, 8192, 256, 128) == (False, 0)             # unsplit: nothing to combine
+    assert st(True, 2, 64, 8192, 256, 64)[0] is False                 # partial 128-cout tile
+    assert st(True, 2, 128, 8192, 256, 128, gout=True)[0] is False    # G side output (the round-3 kernel)
+    assert st(True, 2, 128, 8192, 256, 128, resid_and_ep=True)[0] is False
+    assert st(True, 2, 128, 8192, 256, 128, d3=True)[0] is False
+    assert st(True, 4, 256, 8192, 256, 128, out_f32=True)[0] is False
+    assert st(False, 16, 256, 2048, 64, 128)[0] is False               # implicit GEMM: off by default
+    monkeypatch.setattr(ops, "SPLIT_TICKET", True)
+    assert st(False, 16, 256, 2048, 64, 128) == (True, 32)            # 64-pixel tiles: 32-pixel rows per wave
+    assert st(False, 4, 64, 2048, 128, 64) == (True, 64)
+    assert st(False, 4, 16, 4096, 256, 16) == (True, 64)              # K <= 16: 4 waves across 256 pixels
+    assert st(False, 8, 256, 2000, 64, 128)[0] is False                # ragged pixel tile
+    assert st(False, 8, 256, 2048, 64, 128, transposed=True, stride=2, ks=3, pad=1, Ho=32, Wo=32)[0] is False
+    assert st(False, 8, 256, 2048, 64, 128, transposed=True, stride=1, ks=3, pad=1, Ho=16, Wo=16)[0] is True
+    monkeypatch.setattr(ops, "HALO_TICKET", False)
+    assert st(True, 2, 128, 8192, 256, 128)[0] is False
