@@ -52,6 +52,8 @@ S2D_HALO = bool(tuning.get("S2D_HALO"))
 S2D_3D = S2D_HALO and bool(tuning.get("S2D_3D"))
 # ResBlock 3x3 convs on 1x1 images run as their centre tap (WeightCache.center); POINT_1X1=0 for A/B runs
 POINT_1X1 = bool(tuning.get("POINT_1X1"))
+# forward-only self-attention at the fmd_conv_small levels: both projections on it (runtime/tuning.py SMALL_ATTN)
+SMALL_ATTN = bool(tuning.get("SMALL_ATTN"))
 # training, 3-D fused-prologue halo convs (MAT3D=0): the conv writes G = SiLU(GN(x)) for the weight gradient
 # (fmd_conv_desc.gout), which would otherwise recompute G once per depth tap.  Not on 2-D: there the extra
 # 2 B/element of HBM writes cost the forward more than the weight gradient saves.
@@ -857,6 +859,25 @@ class UNetEngine:
             lin = None
         else:
             raise NotImplementedError(type(m).__name__)
+        if ctx.tape is None and len(sp) == 2 and SMALL_ATTN:
+            # forward only, small level: the GroupNorm folded into the qkv projection and the output projection with
+            # its residual and statistics, one fmd_conv_small launch each (no gn_prep, split-K combine or
+            # channel_stats launches)
+            rows = 64 if T % 64 == 0 else T
+            gnq = dict(st0=x.stats if x.stats is not None else ops.Stats(None, rows), groups=norm.num_groups,
+                       eps=norm.eps, silu=False)
+            if (ops.conv_small_ok((N, H, W, Cc), 3 * inner, mode="point", gn=gnq) and
+                    ops.conv_small_ok((N, H, W, inner), Cc, mode="point")):
+                gnq.update(st0=_stats(x), gamma=norm.weight, beta=norm.bias)
+                qkv, _ = ops.conv_small(x4, 3 * inner, self.wc.get(wq, 0), mode="point", gn=gnq, bias=bq,
+                                        want_stats=False)
+                if lin is not None:
+                    o, _ = ops.linear_attention_fwd(qkv, T, heads, dh, raw, lin)
+                else:
+                    o, _ = ops.attention_fwd(qkv, T, heads, dh, raw)
+                out, st = ops.conv_small(o.view(N, H, W, inner), Cc, self.wc.get(wo, 0), mode="point", bias=bo,
+                                         resid=x4)
+                return Act(out.view(x.t.shape), st)
         a, b, mr = ops.gn_prep(_stats(x), None, N, T, Cc, 0, norm.num_groups, norm.eps, norm.weight, norm.bias)
         qkv, _ = ops.conv(x4, 3 * inner, self.wc.get(wq, 0), ks=1, pad=0, pro=(a, b, False), bias=bq)
         if lin is not None:
