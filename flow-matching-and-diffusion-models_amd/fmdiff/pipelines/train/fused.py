@@ -380,7 +380,7 @@ class FusedTrainStep:
         # multi-rank: thread-local capture, so the process group's watchdog thread may keep querying its
         # (already completed) events while this thread records
         mode = "thread_local" if self._split else "global"
-        with torch.cuda.graph(g, capture_error_mode=mode):
+        with torch.cuda.graph(g, stream=ops.capture_stream(), capture_error_mode=mode):
             if self._split:
                 self._graph_loss = self._fwd_bwd(*self._static)
             else:
@@ -390,7 +390,7 @@ class FusedTrainStep:
         if self._split and self.overlap:   # each later bucket's backward segments as a graph in the same pool
             for b in range(1, len(self.seg_buckets)):
                 gb = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gb, pool=g.pool(), capture_error_mode=mode):
+                with torch.cuda.graph(gb, pool=g.pool(), stream=ops.capture_stream(), capture_error_mode=mode):
                     self._bwd_bucket(b)
                 self._graphs.append(gb)
 
@@ -606,7 +606,7 @@ class FusedSampler:
         if timing is not None:   # the capture is set-up, not model time: keep it out of model_seconds
             torch.cuda.synchronize()
             tc = time.perf_counter()
-        with torch.cuda.graph(g, capture_error_mode=mode):   # records, does not execute: the counter stays
+        with torch.cuda.graph(g, stream=ops.capture_stream(), capture_error_mode=mode):   # records, does not execute
             self._one()
         if timing is not None:
             torch.cuda.synchronize()

@@ -586,6 +586,23 @@ SMALL_TICKETS = 4096
 _small_ws = {}
 
 
+_cap_streams = {}
+
+
+def capture_stream():
+    """The stream graph captures run on: a side stream whose in-launch-combine workspace (tickets zeroed) is created
+    before the first capture, so a capture records no fill of it (a fresh per-stream workspace allocated inside the
+    capture would replay its zero-fill every step)."""
+    idx = torch.cuda.current_device()
+    s = _cap_streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(idx)
+        with torch.cuda.stream(s):
+            _small_workspace(torch.device("cuda", idx))
+        _cap_streams[idx] = s
+    return s
+
+
 def _small_workspace(dev):
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     ws = _small_ws.get(key)
