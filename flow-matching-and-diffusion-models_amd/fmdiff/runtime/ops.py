@@ -587,12 +587,15 @@ _small_ws = {}
 
 
 _cap_streams = {}
+CAPTURE_STREAM = bool(tuning.get("CAPTURE_STREAM"))
 
 
 def capture_stream():
     """The stream graph captures run on: a side stream whose in-launch-combine workspace (tickets zeroed) is created
     before the first capture, so a capture records no fill of it (a fresh per-stream workspace allocated inside the
     capture would replay its zero-fill every step)."""
+    if not CAPTURE_STREAM:
+        return None   # torch's own capture stream
     idx = torch.cuda.current_device()
     s = _cap_streams.get(idx)
     if s is None:

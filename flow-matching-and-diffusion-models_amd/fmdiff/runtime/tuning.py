@@ -32,6 +32,7 @@ TABLE = {
     "HALO_TICKET": (1, "split-K halo convs combined inside the launch (arrival tickets) instead of a combine launch"),
     "SPLIT_TICKET": (0, "... and split-K implicit-GEMM convs on whole tiles likewise (off: their 8-16 parts make one "
                         "workgroup's serial combine slower than the combine launch -- train 369.6 -> 363.5 img/s)"),
+    "CAPTURE_STREAM": (1, "graph captures on a side stream whose in-launch-combine workspace exists beforehand"),
     "SMALL_ATTN": (1, "forward-only small levels: attention's qkv (GroupNorm folded) and output projections on fmd_conv_small"),
     "SMALL_CONV": (1, "forward-only small levels: one launch per conv with the GroupNorm folded in (fmd_conv_small)"),
     "SMALL_CONV_MAX_HW": (256, "fmd_conv_small only on outputs of at most this many pixels per image"),
